@@ -1,0 +1,254 @@
+#!/usr/bin/env python
+"""Headline benchmark: QSGD-MaxNorm 4-bit encode+pack of a device-resident
+100M-fp32 gradient bucket (BASELINE.json metric / configs[1]).
+
+One step = the encode of one rank's bucket exactly as the data-parallel
+reducer runs it: local max-norm (HIP) -> all_reduce MAX of the 4-byte norm
+(RCCL, N > 1 only) -> fused quantize + stochastic round + carry-free pack
+(HIP, Philox draws).  value = grad floats encoded by ALL ranks per second
+(weak scaling: every rank owns a full bucket).
+
+Also reported (not part of `value`): per-kernel HIP-event times and the
+roofline of the dominant kernel (k_qsgd_encode), the decode, the full
+encode -> RCCL all_reduce(SUM, packed words) -> decode path, the
+reference-parity (torch MT19937) encode, and the CPU oracle on the host
+cores (rank 0, N = 1).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "gradient-compression_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--bits", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-oracle sample budget (0 = skip)")
+    ap.add_argument("--no-extras", action="store_true", help="skip decode / reduce-path / parity-mode legs")
+    return ap.parse_args()
+
+
+def _events(torch, fn, reps):
+    """mean ms of fn() over reps, HIP events on the current stream."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _traffic(kernel: str, n: int, bits: int):
+    """HBM bytes per launch from the committed PMC profile (profiles/), if it
+    was collected for this exact workload; else None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel]
+        if d.get("n") == n and d.get("bits") == bits:
+            return k["hbm_bytes_per_launch"]
+    except Exception:
+        pass
+    return None
+
+
+def cpu_baseline(n: int, bits: int, budget_s: float):
+    """The CPU oracle (oracle/gcodec_oracle.c, scalar C, 1 thread) running the
+    reference's CPU algorithm — max-norm, one MT19937 draw per element
+    (torch.bernoulli), quantize, pack — on the same 100M-element bucket."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    x = O.gen_input(n, seed=42)
+    done, t_tot, passes = 0, 0.0, 0
+    while t_tot < budget_s or passes == 0:
+        t0 = time.perf_counter()
+        norm = O.absmax(x)
+        mt = O.MT19937(42 + passes)
+        rng = O.stream_rng(mt.draws(n))
+        O.qsgd_encode(x, norm, bits, 1, rng)
+        t_tot += time.perf_counter() - t0
+        done += n
+        passes += 1
+        del rng
+    del x
+    np.random.default_rng(0)
+    return {"value": done / t_tot, "unit": "grad-floats/s", "cores": 1, "kind": "port",
+            "sample": f"{passes} full encode pass(es) of the {n}-fp32 bucket (absmax + MT19937 draws + "
+                      f"quantize + pack, {bits}-bit), {t_tot:.1f} s on 1 host thread"}
+
+
+def main():
+    args = _args()
+    import torch
+    import torch.distributed as dist
+
+    import gcodec
+    from gcodec import codec
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    n, bits, K, Wm = args.n, args.bits, args.steps, args.warmup
+
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.randn(n, device=dev, generator=g, dtype=torch.float32).mul_(0.01)
+    gen = gcodec.Generator(42 + rank, "philox")
+    lanes = codec.qsgd_layout(n, bits, world)
+    M = lanes.plane_words
+    words = torch.empty(M, dtype=torch.int32, device=dev)
+    norm = torch.empty(1, dtype=torch.float32, device=dev)
+
+    def norm_step():
+        codec.absmax(x, out=norm)
+        if world > 1:
+            dist.all_reduce(norm, op=dist.ReduceOp.MAX)
+
+    def encode_step():
+        codec.qsgd_encode(x, norm, bits, gen.reserve(n), world, out=words, lanes=lanes)
+
+    def step():
+        norm_step()
+        encode_step()
+
+    for _ in range(Wm):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    ms_step = el / K * 1e3
+    value = world * n * K / el
+
+    # ---- per-kernel HIP-event timing (same stream the kernels launch on) ----
+    reps = max(K, 10)
+    ms_absmax = _events(torch, lambda: codec.absmax(x, out=norm), reps)
+    if world > 1:
+        dist.all_reduce(norm, op=dist.ReduceOp.MAX)
+    ms_encode = _events(torch, encode_step, reps)
+    enc_bytes = 4 * n + 4 * M  # read x once, write the packed words
+    achieved = enc_bytes / (ms_encode * 1e-3) / 1e9
+    step_bytes = 8 * n + 4 * M  # + the max-norm read of x
+
+    out = {
+        "metric": "grad-floats/sec encode+pack (device-resident), 100M fp32 bucket; % HBM peak",
+        "value": value,
+        "unit": "grad-floats/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": Wm,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32->u32 (int lanes)",
+        "data": "synthetic N(0, 0.01) fp32 bucket generated on device; Philox4x32-10 draws",
+        "config": {"workload": f"QSGD-MN {bits}-bit encode+pack, {n} fp32 per rank, W={world} carry-free "
+                               f"{lanes.bits}-bit lanes x{lanes.per_word}/word",
+                   "global_batch": n * world, "parallelism": f"dp{world}",
+                   "step": "absmax -> all_reduce(MAX) if N>1 -> quantize+round+pack"},
+        "pct_hbm_peak_step": 100.0 * step_bytes * K / el / 1e9 / HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_qsgd_encode", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": _traffic("k_qsgd_encode", n, bits),
+                     "bytes_per_launch": enc_bytes, "ms_per_launch": ms_encode},
+        "kernels_ms": {"k_absmax": ms_absmax, "k_qsgd_encode": ms_encode},
+    }
+
+    if not args.no_extras:
+        # decode of the (W-summed) words, 1/W folded in
+        dec = torch.empty(n, dtype=torch.float32, device=dev)
+        ms_dec = _events(torch, lambda: codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec,
+                                                           lanes=lanes), reps)
+        out["kernels_ms"]["k_qsgd_decode"] = ms_dec
+        out["decode_gbs"] = (4 * M + 4 * n) / (ms_dec * 1e-3) / 1e9
+
+        # full DP path: norm -> encode -> all_reduce(SUM words) -> decode
+        def path():
+            step()
+            if world > 1:
+                dist.all_reduce(words)
+            codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
+
+        for _ in range(2):
+            path()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            path()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        pel = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([pel], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            pel = t.item()
+        out["reduce_path"] = {"grad_floats_per_s": world * n * K / pel, "ms_per_step": pel / K * 1e3,
+                              "packed_bytes_per_rank": 4 * M,
+                              "steps": "absmax, all_reduce MAX, encode, all_reduce SUM (RCCL), decode + 1/W"}
+        del dec
+
+        # reference-parity mode: torch CPU-generator (MT19937) stream, generated on the GPU
+        n_mt = min(n, 10_000_000)
+        pgen = gcodec.Generator(0, "torch")
+        torch.manual_seed(42)
+        xs = x[:n_mt]
+        nm = codec.absmax(xs)
+        lm = codec.qsgd_layout(n_mt, bits, 1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        codec.qsgd_encode(xs, nm, bits, pgen.reserve(n_mt), 1, lanes=lm)
+        torch.cuda.synchronize()
+        out["torch_parity_mode"] = {"n": n_mt, "grad_floats_per_s": n_mt / (time.perf_counter() - t0),
+                                    "note": "MT19937 stream generated serially by one workgroup, then encode"}
+
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(n, bits, args.cpu_seconds)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

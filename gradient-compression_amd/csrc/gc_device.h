@@ -1,0 +1,135 @@
+// gc_device.h — device-side building blocks shared by the gcodec kernels.
+//
+// gfx950 (CDNA4) only: 64-lane waves, fp32 denormals preserved (no FTZ), no
+// FMA contraction (built with -ffp-contract=off), IEEE correctly-rounded fp32
+// division (hipcc default for HIP device code).  The per-element arithmetic is
+// the reference's, operation for operation (compressors.py:299-316).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gc {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// ---------------------------------------------------------------------------
+// Random draws.  KIND 0 = Philox4x32-10 (counter-based, launch-invariant),
+// KIND 1 = caller stream (level-major: stream[level*n + i]).
+// ---------------------------------------------------------------------------
+struct RngArgs {
+    uint64_t seed;
+    uint64_t offset;
+    const uint32_t *stream;
+    uint64_t n;  // elements per level in the stream
+};
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1)
+{
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        uint4 o;
+        o.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        o.y = (uint32_t)p1;
+        o.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        o.w = (uint32_t)p0;
+        c = o;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// Four draws for elements i0..i0+3 (i0 % 4 == 0) at scale `level`.
+template <int KIND>
+__device__ __forceinline__ uint4 draws4(const RngArgs &r, uint32_t level, uint64_t i0)
+{
+    if constexpr (KIND == 0) {
+        const uint64_t g = i0 >> 2;
+        uint4 c;
+        c.x = (uint32_t)g;
+        c.y = ((uint32_t)(g >> 32) & 0xffffu) | (level << 16);
+        c.z = (uint32_t)r.offset;
+        c.w = (uint32_t)(r.offset >> 32);
+        return philox4x32_10(c, (uint32_t)r.seed, (uint32_t)(r.seed >> 32));
+    } else {
+        const uint32_t *p = r.stream + (uint64_t)level * r.n + i0;
+        const uint64_t left = i0 < r.n ? r.n - i0 : 0;
+        uint4 d;
+        d.x = left > 0 ? p[0] : 0u;
+        d.y = left > 1 ? p[1] : 0u;
+        d.z = left > 2 ? p[2] : 0u;
+        d.w = left > 3 ? p[3] : 0u;
+        return d;
+    }
+}
+
+// One draw (gather / unaligned paths).
+template <int KIND>
+__device__ __forceinline__ uint32_t draw1(const RngArgs &r, uint32_t level, uint64_t i)
+{
+    if constexpr (KIND == 0) {
+        const uint4 d = draws4<0>(r, level, i & ~(uint64_t)3);
+        const uint32_t j = (uint32_t)(i & 3);
+        return j == 0 ? d.x : (j == 1 ? d.y : (j == 2 ? d.z : d.w));
+    } else {
+        return r.stream[(uint64_t)level * r.n + i];
+    }
+}
+
+__device__ __forceinline__ uint32_t pick(const uint4 &v, int j)
+{
+    return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ float pickf(const float4 &v, int j)
+{
+    return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
+// ---------------------------------------------------------------------------
+// One element of the stochastic quantizer (compressors.py:299-316):
+//   l = RN(RN(|x| / norm) * s); fl = trunc(l); p = l - fl (exact, in [0,1));
+//   xi = fl + (u < p), u = (r & 0xFFFFFF) * 2^-24; q = sign(x) * xi.
+// Returns xi (>= 0) and the sign separately; NaN/inf quotient -> 0
+// (the reference raises there; documented divergence).
+// ---------------------------------------------------------------------------
+struct QElem {
+    int32_t xi;
+    int32_t sg;
+};
+
+__device__ __forceinline__ QElem q_elem(float x, float norm, float s, uint32_t r)
+{
+    const float a = fabsf(x);
+    const float ql = a / norm;  // IEEE division, as torch's div
+    const bool ok = ql <= 3.0e38f;
+    const float l = fminf(ql * s, 1073741824.0f);
+    const int32_t fl = (int32_t)l;
+    const float p = l - (float)fl;
+    const float u = (float)(r & 0xFFFFFFu) * 0x1p-24f;
+    QElem e;
+    e.xi = ok ? fl + (u < p ? 1 : 0) : 0;
+    e.sg = (x > 0.0f) ? 1 : ((x < 0.0f) ? -1 : 0);
+    return e;
+}
+
+__device__ __forceinline__ int32_t q_signed(float x, float norm, float s, uint32_t r)
+{
+    const QElem e = q_elem(x, norm, s, r);
+    return e.sg * e.xi;
+}
+
+// ---------------------------------------------------------------------------
+// wave64 / block reductions
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+}  // namespace gc

@@ -1,0 +1,558 @@
+// multiscale.hip — multi-scale / two-scale QSGD-MaxNorm on gfx950
+// (compressors.py:754-826 QSGDMaxNormMultiScaleCompressor, and for two levels
+// compressors.py:612-680 QSGDMaxNormTwoScaleCompressor, reducer.py:1454-1715).
+//
+// The reference materialises an L x n float32 cache of every level's
+// quantisation (compress_cache, 778-797), then a resolution mask (799-807), a
+// MIN all-reduce of the int8 mask, and a select (809-817).  Here there is no
+// cache: the mask kernel quantises every level on the fly and emits the mask
+// as thermometer lanes (field k = [m >= k], k = 1..L-1), which a SUM
+// all-reduce turns into the MIN over ranks (m = #fields whose sum == W); the
+// select kernel recomputes only the chosen level with the SAME counter-based
+// draw, so nothing but x is read twice.
+#include "gc_device.h"
+#include "gc_host.h"
+
+namespace gc {
+
+struct LevelsArg {
+    uint32_t count;
+    int32_t maxv;  // 2^bits[0] - 1 (compressors.py:800)
+    float s[GC_MAX_LEVELS];
+};
+
+__device__ __forceinline__ float sel_level(const LevelsArg &lv, uint32_t m)
+{
+    float s = lv.s[0];
+#pragma unroll
+    for (int l = 1; l < GC_MAX_LEVELS; ++l)
+        if ((uint32_t)l < lv.count && m == (uint32_t)l)
+            s = lv.s[l];
+    return s;
+}
+
+template <int MODE>
+__device__ __forceinline__ float4 load4m(const float *__restrict__ x, const int64_t *__restrict__ idx, uint64_t i0,
+                                         uint64_t n)
+{
+    if (MODE == 0 && i0 + 4 <= n)
+        return *reinterpret_cast<const float4 *>(x + i0);
+    float4 v;
+    v.x = i0 + 0 < n ? (MODE == 2 ? x[idx[i0 + 0]] : x[i0 + 0]) : 0.0f;
+    v.y = i0 + 1 < n ? (MODE == 2 ? x[idx[i0 + 1]] : x[i0 + 1]) : 0.0f;
+    v.z = i0 + 2 < n ? (MODE == 2 ? x[idx[i0 + 2]] : x[i0 + 2]) : 0.0f;
+    v.w = i0 + 3 < n ? (MODE == 2 ? x[idx[i0 + 3]] : x[i0 + 3]) : 0.0f;
+    return v;
+}
+
+// resolution level of 4 elements: last level whose |q| <= maxv (level 0 always)
+template <int KIND>
+__device__ __forceinline__ uint4 ms_levels4(const float4 &v, float norm, const LevelsArg &lv, const RngArgs &rng,
+                                            uint64_t i0)
+{
+    uint4 m = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t l = 1; l < lv.count; ++l) {
+        const uint4 r = draws4<KIND>(rng, l, i0);
+        const float s = lv.s[l];
+        if (q_elem(v.x, norm, s, r.x).xi <= lv.maxv) m.x = l;
+        if (q_elem(v.y, norm, s, r.y).xi <= lv.maxv) m.y = l;
+        if (q_elem(v.z, norm, s, r.z).xi <= lv.maxv) m.z = l;
+        if (q_elem(v.w, norm, s, r.w).xi <= lv.maxv) m.w = l;
+    }
+    return m;
+}
+// Level 0 needs no draw for the mask: |q_0| <= s_0 = maxv always (its draws
+// are still "consumed" by the stream layout: level l uses block l).
+
+// q of 4 elements at their own levels m (same draws as the mask pass)
+template <int KIND>
+__device__ __forceinline__ int4 ms_select4(const float4 &v, float norm, const LevelsArg &lv, const RngArgs &rng,
+                                           uint64_t i0, uint4 m)
+{
+    int4 q = make_int4(0, 0, 0, 0);
+    for (uint32_t l = 0; l < lv.count; ++l) {
+        if (m.x != l && m.y != l && m.z != l && m.w != l)
+            continue;
+        const uint4 r = draws4<KIND>(rng, l, i0);
+        const float s = lv.s[l];
+        if (m.x == l) q.x = q_signed(v.x, norm, s, r.x);
+        if (m.y == l) q.y = q_signed(v.y, norm, s, r.y);
+        if (m.z == l) q.z = q_signed(v.z, norm, s, r.z);
+        if (m.w == l) q.w = q_signed(v.w, norm, s, r.w);
+    }
+    return q;
+}
+
+struct MaskArg {
+    const uint32_t *words;
+    uint64_t M;       // words per field stream
+    uint32_t w;       // lane bits
+    uint32_t fields;  // count - 1
+    uint32_t world;
+};
+
+// common level of elements pos..pos+3 (pos % 4 == 0, same plane) from W-summed fields
+__device__ __forceinline__ uint4 mask_levels4(const MaskArg &mk, uint64_t i0)
+{
+    const uint64_t plane = i0 / mk.M, pos = i0 - plane * mk.M;
+    const uint32_t sh = (uint32_t)plane * mk.w;
+    const uint32_t msk = (1u << mk.w) - 1u;
+    uint4 m = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t f = 0; f < mk.fields; ++f) {
+        const uint4 wd = *reinterpret_cast<const uint4 *>(mk.words + f * mk.M + pos);
+        m.x += ((wd.x >> sh) & msk) == mk.world;
+        m.y += ((wd.y >> sh) & msk) == mk.world;
+        m.z += ((wd.z >> sh) & msk) == mk.world;
+        m.w += ((wd.w >> sh) & msk) == mk.world;
+    }
+    return m;
+}
+
+template <int LM, int KIND, int MODE>
+__global__ __launch_bounds__(kBlock) void k_ms_mask_encode(const float *__restrict__ x, const int64_t *__restrict__ idx,
+                                                           uint64_t n, const float *__restrict__ normp, LevelsArg lv,
+                                                           RngArgs rng, uint64_t M, uint32_t w, uint32_t fields,
+                                                           uint32_t *__restrict__ mask_words)
+{
+    const float norm = *normp;
+    const uint64_t quads = M >> 2;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
+        uint4 acc[GC_MAX_LEVELS - 1];
+#pragma unroll
+        for (int f = 0; f < GC_MAX_LEVELS - 1; ++f)
+            acc[f] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int j = 0; j < LM; ++j) {
+            const uint64_t i0 = (uint64_t)j * M + 4 * t;
+            if (i0 < n) {
+                const float4 v = load4m<MODE>(x, idx, i0, n);
+                const uint4 m = ms_levels4<KIND>(v, norm, lv, rng, i0);
+                const uint32_t sh = (uint32_t)j * w;
+#pragma unroll
+                for (int f = 0; f < GC_MAX_LEVELS - 1; ++f) {
+                    if ((uint32_t)f < fields) {
+                        acc[f].x |= (uint32_t)(m.x > (uint32_t)f) << sh;
+                        acc[f].y |= (uint32_t)(m.y > (uint32_t)f && i0 + 1 < n) << sh;
+                        acc[f].z |= (uint32_t)(m.z > (uint32_t)f && i0 + 2 < n) << sh;
+                        acc[f].w |= (uint32_t)(m.w > (uint32_t)f && i0 + 3 < n) << sh;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < GC_MAX_LEVELS - 1; ++f)
+            if ((uint32_t)f < fields)
+                *reinterpret_cast<uint4 *>(mask_words + (uint64_t)f * M + 4 * t) = acc[f];
+    }
+}
+
+template <int LQ, int KIND, int MODE>
+__global__ __launch_bounds__(kBlock) void k_ms_select_encode(const float *__restrict__ x,
+                                                             const int64_t *__restrict__ idx, uint64_t n,
+                                                             const float *__restrict__ normp, LevelsArg lv,
+                                                             RngArgs rng, MaskArg mk, uint64_t Mq, uint32_t wq,
+                                                             int32_t qmax, uint32_t *__restrict__ words)
+{
+    const float norm = *normp;
+    const uint64_t quads = Mq >> 2;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int k = 0; k < LQ; ++k) {
+            const uint64_t i0 = (uint64_t)k * Mq + 4 * t;
+            if (i0 < n) {
+                const float4 v = load4m<MODE>(x, idx, i0, n);
+                const uint4 m = mask_levels4(mk, i0);
+                const int4 q = ms_select4<KIND>(v, norm, lv, rng, i0, m);
+                const uint32_t sh = (uint32_t)k * wq;
+                acc.x |= (uint32_t)(min(max(q.x, -qmax), qmax) + qmax) << sh;
+                acc.y |= (i0 + 1 < n ? (uint32_t)(min(max(q.y, -qmax), qmax) + qmax) : 0u) << sh;
+                acc.z |= (i0 + 2 < n ? (uint32_t)(min(max(q.z, -qmax), qmax) + qmax) : 0u) << sh;
+                acc.w |= (i0 + 3 < n ? (uint32_t)(min(max(q.w, -qmax), qmax) + qmax) : 0u) << sh;
+            }
+        }
+        *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
+    }
+}
+
+__device__ __forceinline__ float ms_dq(int32_t Q, float norm, float s, int order, float alpha)
+{
+    const float d = order ? (norm / s) * (float)Q : ((float)Q * norm) / s;
+    return d * alpha;
+}
+
+template <int LQ, int MODE>
+__global__ __launch_bounds__(kBlock) void k_ms_decode(const uint32_t *__restrict__ words, MaskArg mk,
+                                                      const int64_t *__restrict__ idx, uint64_t n,
+                                                      const float *__restrict__ normp, LevelsArg lv, uint64_t Mq,
+                                                      uint32_t wq, int32_t sub, int order, float alpha,
+                                                      float *__restrict__ out)
+{
+    const float norm = *normp;
+    const uint32_t msk = wq >= 32 ? 0xffffffffu : ((1u << wq) - 1u);
+    const uint64_t quads = Mq >> 2;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
+        const uint4 wd = *reinterpret_cast<const uint4 *>(words + 4 * t);
+#pragma unroll
+        for (int k = 0; k < LQ; ++k) {
+            const uint64_t i0 = (uint64_t)k * Mq + 4 * t;
+            if (i0 < n) {
+                const uint4 m = mask_levels4(mk, i0);
+                const uint32_t sh = (uint32_t)k * wq;
+                float4 o;
+                o.x = ms_dq((int32_t)((wd.x >> sh) & msk) - sub, norm, sel_level(lv, m.x), order, alpha);
+                o.y = ms_dq((int32_t)((wd.y >> sh) & msk) - sub, norm, sel_level(lv, m.y), order, alpha);
+                o.z = ms_dq((int32_t)((wd.z >> sh) & msk) - sub, norm, sel_level(lv, m.z), order, alpha);
+                o.w = ms_dq((int32_t)((wd.w >> sh) & msk) - sub, norm, sel_level(lv, m.w), order, alpha);
+                if (MODE == 0 && i0 + 4 <= n) {
+                    *reinterpret_cast<float4 *>(out + i0) = o;
+                } else {
+                    for (int e = 0; e < 4; ++e)
+                        if (i0 + e < n)
+                            out[MODE == 2 ? idx[i0 + e] : i0 + e] = pickf(o, e);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// unpacked (int8 mask / int8|int32 q) forms — the literal compressor drop-in
+// ---------------------------------------------------------------------------
+template <int KIND, int MODE>
+__global__ __launch_bounds__(kBlock) void k_ms_quantize_mask(const float *__restrict__ x, uint64_t n,
+                                                             const float *__restrict__ normp, LevelsArg lv,
+                                                             RngArgs rng, int8_t *__restrict__ mask)
+{
+    const float norm = *normp;
+    const uint64_t groups = (n + 3) >> 2;
+    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t i0 = g << 2;
+        const float4 v = load4m<MODE>(x, nullptr, i0, n);
+        const uint4 m = ms_levels4<KIND>(v, norm, lv, rng, i0);
+        for (int e = 0; e < 4; ++e)
+            if (i0 + e < n)
+                mask[i0 + e] = (int8_t)pick(m, e);
+    }
+}
+
+template <int KIND, int MODE, typename QT>
+__global__ __launch_bounds__(kBlock) void k_ms_select_quantize(const float *__restrict__ x, uint64_t n,
+                                                               const float *__restrict__ normp, LevelsArg lv,
+                                                               RngArgs rng, const int8_t *__restrict__ mask,
+                                                               QT *__restrict__ q)
+{
+    const float norm = *normp;
+    const uint64_t groups = (n + 3) >> 2;
+    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t i0 = g << 2;
+        const float4 v = load4m<MODE>(x, nullptr, i0, n);
+        uint4 m;
+        m.x = (uint32_t)mask[i0];
+        m.y = i0 + 1 < n ? (uint32_t)mask[i0 + 1] : 0u;
+        m.z = i0 + 2 < n ? (uint32_t)mask[i0 + 2] : 0u;
+        m.w = i0 + 3 < n ? (uint32_t)mask[i0 + 3] : 0u;
+        const int4 qq = ms_select4<KIND>(v, norm, lv, rng, i0, m);
+        if (i0 + 0 < n) q[i0 + 0] = (QT)qq.x;
+        if (i0 + 1 < n) q[i0 + 1] = (QT)qq.y;
+        if (i0 + 2 < n) q[i0 + 2] = (QT)qq.z;
+        if (i0 + 3 < n) q[i0 + 3] = (QT)qq.w;
+    }
+}
+
+template <typename QT>
+__global__ __launch_bounds__(kBlock) void k_ms_dequantize(const QT *__restrict__ q, const int8_t *__restrict__ mask,
+                                                          uint64_t n, const float *__restrict__ normp, LevelsArg lv,
+                                                          int order, float alpha, float *__restrict__ out)
+{
+    const float norm = *normp;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+        out[i] = ms_dq((int32_t)q[i], norm, sel_level(lv, (uint32_t)mask[i]), order, alpha);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ms_mask_unpack(MaskArg mk, uint64_t n, int8_t *__restrict__ mask)
+{
+    const uint32_t msk = (1u << mk.w) - 1u;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t plane = i / mk.M, pos = i - plane * mk.M;
+        uint32_t m = 0;
+        for (uint32_t f = 0; f < mk.fields; ++f)
+            m += ((mk.words[f * mk.M + pos] >> ((uint32_t)plane * mk.w)) & msk) == mk.world;
+        mask[i] = (int8_t)m;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static LevelsArg levels_arg(const gc_levels *lv)
+{
+    LevelsArg a;
+    a.count = lv->count;
+    a.maxv = (int32_t)((1u << lv->bits[0]) - 1u);
+    for (int i = 0; i < GC_MAX_LEVELS; ++i)
+        a.s[i] = i < (int)lv->count ? (float)((1u << lv->bits[i]) - 1u) : 1.0f;
+    return a;
+}
+
+static int check_rng_ms(const gc_rng *r, const char *what)
+{
+    GC_REQUIRE(r, "%s: null rng", what);
+    GC_REQUIRE(r->kind == GC_RNG_PHILOX || r->kind == GC_RNG_STREAM, "%s: unknown rng kind", what);
+    GC_REQUIRE(r->kind != GC_RNG_STREAM || r->stream, "%s: STREAM rng without stream", what);
+    return GC_OK;
+}
+
+static RngArgs rng_args_ms(const gc_rng *r, uint64_t n)
+{
+    RngArgs a;
+    a.seed = r->seed;
+    a.offset = r->offset;
+    a.stream = r->stream;
+    a.n = n;
+    return a;
+}
+
+static int check_mask_lanes(const gc_lanes *ml, const gc_levels *lv, uint64_t n, const char *what)
+{
+    int rc = check_lanes(ml, n, what);
+    if (rc)
+        return rc;
+    GC_REQUIRE(ml->range == 1 && ml->offset == 0, "%s: mask lanes not made by gc_ms_mask_layout", what);
+    GC_REQUIRE(lv->count >= 2, "%s: needs >= 2 levels", what);
+    return GC_OK;
+}
+
+static int check_q_lanes(const gc_lanes *ql, const gc_levels *lv, uint64_t n, const char *what)
+{
+    int rc = check_lanes(ql, n, what);
+    if (rc)
+        return rc;
+    gc_lanes ref;
+    if ((rc = gc_ms_layout(n, lv, ql->world, &ref)))
+        return rc;
+    GC_REQUIRE(ref.offset == ql->offset && ref.range == ql->range, "%s: q lanes not made by gc_ms_layout", what);
+    return GC_OK;
+}
+
+static MaskArg mask_arg(const uint32_t *w, const gc_lanes *ml, uint32_t count)
+{
+    MaskArg m;
+    m.words = w;
+    m.M = ml->plane_words;
+    m.w = ml->bits;
+    m.fields = count - 1;
+    m.world = ml->world;
+    return m;
+}
+
+#define GC_DISPATCH_L2(L, ...)                                                   \
+    switch (L) {                                                                 \
+    case 1: { constexpr int LL = 1; __VA_ARGS__; } break;                        \
+    case 2: { constexpr int LL = 2; __VA_ARGS__; } break;                        \
+    case 3: { constexpr int LL = 3; __VA_ARGS__; } break;                        \
+    case 4: { constexpr int LL = 4; __VA_ARGS__; } break;                        \
+    case 5: { constexpr int LL = 5; __VA_ARGS__; } break;                        \
+    case 6: { constexpr int LL = 6; __VA_ARGS__; } break;                        \
+    case 8: { constexpr int LL = 8; __VA_ARGS__; } break;                        \
+    case 10: { constexpr int LL = 10; __VA_ARGS__; } break;                      \
+    case 16: { constexpr int LL = 16; __VA_ARGS__; } break;                      \
+    case 32: { constexpr int LL = 32; __VA_ARGS__; } break;                      \
+    default: return fail(GC_EINVAL, "unsupported lanes per word %u", (unsigned)(L)); \
+    }
+
+}  // namespace gc
+
+using namespace gc;
+
+extern "C" {
+
+int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, const gc_levels *levels,
+                      const gc_rng *rng, const gc_lanes *mask_lanes, uint32_t *mask_words, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_levels(levels, "gc_ms_mask_encode")) || (rc = check_rng_ms(rng, "gc_ms_mask_encode")) ||
+        (rc = check_mask_lanes(mask_lanes, levels, n, "gc_ms_mask_encode")))
+        return rc;
+    GC_REQUIRE(norm && mask_words && (n == 0 || x), "gc_ms_mask_encode: null pointer");
+    GC_REQUIRE(aligned16(mask_words), "gc_ms_mask_encode: mask_words must be 16-byte aligned");
+    if (mask_lanes->plane_words == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const LevelsArg la = levels_arg(levels);
+    const RngArgs ra = rng_args_ms(rng, n);
+    const int mode = idx ? 2 : (aligned16(x) ? 0 : 1);
+    const unsigned grid = grid_for(mask_lanes->plane_words >> 2);
+    const uint64_t M = mask_lanes->plane_words;
+    const uint32_t w = mask_lanes->bits, fields = levels->count - 1;
+#define GC_ME(KIND_, MODE_)                                                                                       \
+    GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_encode<LL, KIND_, MODE_>), dim3(grid),    \
+                                                            dim3(kBlock), 0, st, x, idx, n, norm, la, ra, M, w,  \
+                                                            fields, mask_words))
+    if (rng->kind == GC_RNG_PHILOX) {
+        if (mode == 0) { GC_ME(0, 0); } else if (mode == 1) { GC_ME(0, 1); } else { GC_ME(0, 2); }
+    } else {
+        if (mode == 0) { GC_ME(1, 0); } else if (mode == 1) { GC_ME(1, 1); } else { GC_ME(1, 2); }
+    }
+#undef GC_ME
+    return launch_status("gc_ms_mask_encode");
+}
+
+int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, const gc_levels *levels,
+                        const gc_rng *rng, const uint32_t *mask_words, const gc_lanes *mask_lanes,
+                        const gc_lanes *q_lanes, uint32_t *words, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_levels(levels, "gc_ms_select_encode")) || (rc = check_rng_ms(rng, "gc_ms_select_encode")) ||
+        (rc = check_mask_lanes(mask_lanes, levels, n, "gc_ms_select_encode")) ||
+        (rc = check_q_lanes(q_lanes, levels, n, "gc_ms_select_encode")))
+        return rc;
+    GC_REQUIRE(norm && mask_words && words && (n == 0 || x), "gc_ms_select_encode: null pointer");
+    GC_REQUIRE(aligned16(words) && aligned16(mask_words), "gc_ms_select_encode: words must be 16-byte aligned");
+    if (q_lanes->plane_words == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const LevelsArg la = levels_arg(levels);
+    const RngArgs ra = rng_args_ms(rng, n);
+    const MaskArg mk = mask_arg(mask_words, mask_lanes, levels->count);
+    const int mode = idx ? 2 : (aligned16(x) ? 0 : 1);
+    const unsigned grid = grid_for(q_lanes->plane_words >> 2);
+    const uint64_t Mq = q_lanes->plane_words;
+    const uint32_t wq = q_lanes->bits;
+    const int32_t qmax = (int32_t)q_lanes->offset;
+#define GC_SE(KIND_, MODE_)                                                                                        \
+    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_encode<LL, KIND_, MODE_>), dim3(grid),       \
+                                                         dim3(kBlock), 0, st, x, idx, n, norm, la, ra, mk, Mq, wq, \
+                                                         qmax, words))
+    if (rng->kind == GC_RNG_PHILOX) {
+        if (mode == 0) { GC_SE(0, 0); } else if (mode == 1) { GC_SE(0, 1); } else { GC_SE(0, 2); }
+    } else {
+        if (mode == 0) { GC_SE(1, 0); } else if (mode == 1) { GC_SE(1, 1); } else { GC_SE(1, 2); }
+    }
+#undef GC_SE
+    return launch_status("gc_ms_select_encode");
+}
+
+int gc_ms_decode(const uint32_t *words, const uint32_t *mask_words, const int64_t *idx, uint64_t n, const float *norm,
+                 const gc_levels *levels, const gc_lanes *mask_lanes, const gc_lanes *q_lanes, int order, float alpha,
+                 float *out, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_levels(levels, "gc_ms_decode")) ||
+        (rc = check_mask_lanes(mask_lanes, levels, n, "gc_ms_decode")) ||
+        (rc = check_q_lanes(q_lanes, levels, n, "gc_ms_decode")))
+        return rc;
+    GC_REQUIRE(mask_lanes->world == q_lanes->world, "gc_ms_decode: mask and q lanes sized for different worlds");
+    GC_REQUIRE(norm && mask_words && words && (n == 0 || out), "gc_ms_decode: null pointer");
+    GC_REQUIRE(order == 0 || order == 1, "gc_ms_decode: order must be 0 (multi-scale) or 1 (two-scale)");
+    GC_REQUIRE(aligned16(words) && aligned16(mask_words), "gc_ms_decode: words must be 16-byte aligned");
+    if (q_lanes->plane_words == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const LevelsArg la = levels_arg(levels);
+    const MaskArg mk = mask_arg(mask_words, mask_lanes, levels->count);
+    const int mode = idx ? 2 : (aligned16(out) ? 0 : 1);
+    const unsigned grid = grid_for(q_lanes->plane_words >> 2);
+    const int32_t sub = (int32_t)(q_lanes->world * q_lanes->offset);
+#define GC_MD(MODE_)                                                                                               \
+    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_decode<LL, MODE_>), dim3(grid), dim3(kBlock), 0, st, \
+                                                         words, mk, idx, n, norm, la, q_lanes->plane_words,        \
+                                                         q_lanes->bits, sub, order, alpha, out))
+    if (mode == 0) { GC_MD(0); } else if (mode == 1) { GC_MD(1); } else { GC_MD(2); }
+#undef GC_MD
+    return launch_status("gc_ms_decode");
+}
+
+int gc_ms_mask_unpack(const uint32_t *mask_words, const gc_lanes *mask_lanes, uint32_t levels_count, int8_t *mask,
+                      gc_stream_t stream)
+{
+    GC_REQUIRE(mask_lanes && mask_words, "gc_ms_mask_unpack: null pointer");
+    int rc = check_lanes(mask_lanes, mask_lanes->n, "gc_ms_mask_unpack");
+    if (rc)
+        return rc;
+    GC_REQUIRE(levels_count >= 2 && levels_count <= GC_MAX_LEVELS, "gc_ms_mask_unpack: bad level count");
+    GC_REQUIRE(mask_lanes->n == 0 || mask, "gc_ms_mask_unpack: null mask");
+    if (mask_lanes->n == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_ms_mask_unpack, dim3(grid_for(mask_lanes->n)), dim3(kBlock), 0, st,
+                       mask_arg(mask_words, mask_lanes, levels_count), mask_lanes->n, mask);
+    return launch_status("gc_ms_mask_unpack");
+}
+
+int gc_ms_quantize_mask(const float *x, uint64_t n, const float *norm, const gc_levels *levels, const gc_rng *rng,
+                        int8_t *mask, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_levels(levels, "gc_ms_quantize_mask")) || (rc = check_rng_ms(rng, "gc_ms_quantize_mask")))
+        return rc;
+    GC_REQUIRE(n == 0 || (x && norm && mask), "gc_ms_quantize_mask: null pointer");
+    if (n == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const LevelsArg la = levels_arg(levels);
+    const RngArgs ra = rng_args_ms(rng, n);
+    const unsigned grid = grid_for((n + 3) >> 2);
+    const bool vec = aligned16(x);
+    if (rng->kind == GC_RNG_PHILOX) {
+        if (vec) hipLaunchKernelGGL((k_ms_quantize_mask<0, 0>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, ra, mask);
+        else hipLaunchKernelGGL((k_ms_quantize_mask<0, 1>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, ra, mask);
+    } else {
+        if (vec) hipLaunchKernelGGL((k_ms_quantize_mask<1, 0>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, ra, mask);
+        else hipLaunchKernelGGL((k_ms_quantize_mask<1, 1>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, ra, mask);
+    }
+    return launch_status("gc_ms_quantize_mask");
+}
+
+int gc_ms_select_quantize(const float *x, uint64_t n, const float *norm, const gc_levels *levels, const gc_rng *rng,
+                          const int8_t *mask, void *q, uint32_t q_dtype, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_levels(levels, "gc_ms_select_quantize")) || (rc = check_rng_ms(rng, "gc_ms_select_quantize")))
+        return rc;
+    GC_REQUIRE(q_dtype == GC_I8 || q_dtype == GC_I32, "gc_ms_select_quantize: q_dtype must be GC_I8 or GC_I32");
+    GC_REQUIRE(n == 0 || (x && norm && mask && q), "gc_ms_select_quantize: null pointer");
+    if (n == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const LevelsArg la = levels_arg(levels);
+    const RngArgs ra = rng_args_ms(rng, n);
+    const unsigned grid = grid_for((n + 3) >> 2);
+    const bool vec = aligned16(x);
+#define GC_SQ(KIND_, MODE_, QT_)                                                                                \
+    hipLaunchKernelGGL((k_ms_select_quantize<KIND_, MODE_, QT_>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, \
+                       ra, mask, reinterpret_cast<QT_ *>(q))
+    if (rng->kind == GC_RNG_PHILOX) {
+        if (q_dtype == GC_I8) { if (vec) GC_SQ(0, 0, int8_t); else GC_SQ(0, 1, int8_t); }
+        else { if (vec) GC_SQ(0, 0, int32_t); else GC_SQ(0, 1, int32_t); }
+    } else {
+        if (q_dtype == GC_I8) { if (vec) GC_SQ(1, 0, int8_t); else GC_SQ(1, 1, int8_t); }
+        else { if (vec) GC_SQ(1, 0, int32_t); else GC_SQ(1, 1, int32_t); }
+    }
+#undef GC_SQ
+    return launch_status("gc_ms_select_quantize");
+}
+
+int gc_ms_dequantize(const void *q, uint32_t q_dtype, const int8_t *mask, uint64_t n, const float *norm,
+                     const gc_levels *levels, int order, float alpha, float *out, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_levels(levels, "gc_ms_dequantize")))
+        return rc;
+    GC_REQUIRE(q_dtype == GC_I8 || q_dtype == GC_I32, "gc_ms_dequantize: q_dtype must be GC_I8 or GC_I32");
+    GC_REQUIRE(order == 0 || order == 1, "gc_ms_dequantize: order must be 0 or 1");
+    GC_REQUIRE(n == 0 || (q && mask && norm && out), "gc_ms_dequantize: null pointer");
+    if (n == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const LevelsArg la = levels_arg(levels);
+    if (q_dtype == GC_I8)
+        hipLaunchKernelGGL((k_ms_dequantize<int8_t>), dim3(grid_for(n)), dim3(kBlock), 0, st,
+                           reinterpret_cast<const int8_t *>(q), mask, n, norm, la, order, alpha, out);
+    else
+        hipLaunchKernelGGL((k_ms_dequantize<int32_t>), dim3(grid_for(n)), dim3(kBlock), 0, st,
+                           reinterpret_cast<const int32_t *>(q), mask, n, norm, la, order, alpha, out);
+    return launch_status("gc_ms_dequantize");
+}
+
+}  // extern "C"

@@ -1,0 +1,498 @@
+// qsgd.hip — QSGD-MaxNorm hot path on gfx950:
+//   k_absmax        max-norm scan            (reducer.py:516 buffer.abs().max())
+//   k_qsgd_encode   quantize + stochastic round + carry-free lane pack
+//                   (compressors.py:299-316 fused with the packing step)
+//   k_qsgd_decode   unpack W-summed lanes + dequantize + 1/W
+//                   (compressors.py:318-321, reducer.py:544-549)
+//   k_qsgd_quantize / k_qsgd_dequantize   unpacked int8/int32 drop-ins
+//   k_lane_pack / k_lane_unpack           packing of already-quantized ints
+//
+// Memory-bound streaming kernels.  Planar lane layout: word j of the packed
+// stream holds elements j + k*M (k < L), so a thread that owns words
+// 4t..4t+3 reads L fully coalesced float4s (one per plane) and writes one
+// uint4: 16 B/lane on every HBM access, no LDS and no cross-lane shuffles.
+// The element group i0..i0+3 of each float4 is also one Philox block.
+#include "gc_device.h"
+#include "gc_host.h"
+
+namespace gc {
+
+__device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
+
+// ---------------------------------------------------------------------------
+// max-norm: uint max over |x| bit patterns (exact, order-free, NaN wins like
+// torch.max), wave64 shuffle tree, 4 wave partials in LDS, one atomic/block.
+// ---------------------------------------------------------------------------
+template <int MODE>  // 0: float4 dense, 1: scalar dense, 2: gather
+__global__ __launch_bounds__(kBlock) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
+                                                   uint64_t n, uint32_t *__restrict__ out)
+{
+    uint32_t m = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if constexpr (MODE == 0) {
+        const float4 *x4 = reinterpret_cast<const float4 *>(x);
+        const uint64_t n4 = n >> 2;
+        for (; t + 3 * stride < n4; t += 4 * stride) {
+            const float4 a = x4[t], b = x4[t + stride], c = x4[t + 2 * stride], d = x4[t + 3 * stride];
+            m = max(m, max(max(absbits(a.x), absbits(a.y)), max(absbits(a.z), absbits(a.w))));
+            m = max(m, max(max(absbits(b.x), absbits(b.y)), max(absbits(b.z), absbits(b.w))));
+            m = max(m, max(max(absbits(c.x), absbits(c.y)), max(absbits(c.z), absbits(c.w))));
+            m = max(m, max(max(absbits(d.x), absbits(d.y)), max(absbits(d.z), absbits(d.w))));
+        }
+        for (; t < n4; t += stride) {
+            const float4 a = x4[t];
+            m = max(m, max(max(absbits(a.x), absbits(a.y)), max(absbits(a.z), absbits(a.w))));
+        }
+        if (blockIdx.x == 0 && threadIdx.x < (n & 3))
+            m = max(m, absbits(x[(n4 << 2) + threadIdx.x]));
+    } else {
+        for (; t < n; t += stride)
+            m = max(m, absbits(MODE == 2 ? x[idx[t]] : x[t]));
+    }
+    m = wave_max_u32(m);
+    __shared__ uint32_t part[kBlock / 64];
+    if ((threadIdx.x & 63) == 0)
+        part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = max(max(part[0], part[1]), max(part[2], part[3]));
+        if (m)
+            atomicMax(out, m);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// encode: lane(k) of word j = clamp(q(x[kM + j]), -qmax, qmax) + qmax
+// ---------------------------------------------------------------------------
+template <int MODE>
+__device__ __forceinline__ float4 load4(const float *__restrict__ x, const int64_t *__restrict__ idx, uint64_t i0,
+                                        uint64_t n)
+{
+    if (MODE == 0 && i0 + 4 <= n)
+        return *reinterpret_cast<const float4 *>(x + i0);
+    float4 v;
+    v.x = i0 + 0 < n ? (MODE == 2 ? x[idx[i0 + 0]] : x[i0 + 0]) : 0.0f;
+    v.y = i0 + 1 < n ? (MODE == 2 ? x[idx[i0 + 1]] : x[i0 + 1]) : 0.0f;
+    v.z = i0 + 2 < n ? (MODE == 2 ? x[idx[i0 + 2]] : x[i0 + 2]) : 0.0f;
+    v.w = i0 + 3 < n ? (MODE == 2 ? x[idx[i0 + 3]] : x[i0 + 3]) : 0.0f;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t lane_of(float x, float norm, float s, uint32_t r, int32_t qmax, bool valid)
+{
+    int32_t q = q_signed(x, norm, s, r);
+    q = min(max(q, -qmax), qmax);
+    return valid ? (uint32_t)(q + qmax) : 0u;
+}
+
+template <int L, int KIND, int MODE>
+__global__ __launch_bounds__(kBlock) void k_qsgd_encode(const float *__restrict__ x, const int64_t *__restrict__ idx,
+                                                        uint64_t n, const float *__restrict__ normp, float s,
+                                                        int32_t qmax, uint32_t w, uint64_t M, RngArgs rng,
+                                                        uint32_t *__restrict__ words)
+{
+    const float norm = *normp;
+    const uint64_t quads = M >> 2;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+        // fully unrolled for L <= 16: the compiler hoists the L independent
+        // float4 loads ahead of the arithmetic (L x 16 B in flight per lane)
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            const uint64_t i0 = (uint64_t)k * M + 4 * t;
+            if (i0 < n) {
+                const float4 xv = load4<MODE>(x, idx, i0, n);
+                const uint4 r = draws4<KIND>(rng, 0, i0);
+                const uint32_t sh = (uint32_t)k * w;
+                acc.x |= lane_of(xv.x, norm, s, r.x, qmax, true) << sh;
+                acc.y |= lane_of(xv.y, norm, s, r.y, qmax, i0 + 1 < n) << sh;
+                acc.z |= lane_of(xv.z, norm, s, r.z, qmax, i0 + 2 < n) << sh;
+                acc.w |= lane_of(xv.w, norm, s, r.w, qmax, i0 + 3 < n) << sh;
+            }
+        }
+        *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// decode: out = RN(RN(c * (lane - W*qoff)) * alpha), c = RN(norm / s)
+// ---------------------------------------------------------------------------
+template <int MODE>
+__device__ __forceinline__ void store4(float *__restrict__ out, const int64_t *__restrict__ idx, uint64_t i0,
+                                       uint64_t n, float4 v)
+{
+    if (MODE == 0 && i0 + 4 <= n) {
+        *reinterpret_cast<float4 *>(out + i0) = v;
+        return;
+    }
+    if (i0 + 0 < n)
+        out[MODE == 2 ? idx[i0 + 0] : i0 + 0] = v.x;
+    if (i0 + 1 < n)
+        out[MODE == 2 ? idx[i0 + 1] : i0 + 1] = v.y;
+    if (i0 + 2 < n)
+        out[MODE == 2 ? idx[i0 + 2] : i0 + 2] = v.z;
+    if (i0 + 3 < n)
+        out[MODE == 2 ? idx[i0 + 3] : i0 + 3] = v.w;
+}
+
+__device__ __forceinline__ float dq(uint32_t word, uint32_t sh, uint32_t mask, int32_t sub, float c, float alpha)
+{
+    const int32_t Q = (int32_t)((word >> sh) & mask) - sub;
+    const float d = c * (float)Q;
+    return d * alpha;
+}
+
+template <int L, int MODE>
+__global__ __launch_bounds__(kBlock) void k_qsgd_decode(const uint32_t *__restrict__ words,
+                                                        const int64_t *__restrict__ idx, uint64_t n,
+                                                        const float *__restrict__ normp, float s, int32_t sub,
+                                                        uint32_t w, uint64_t M, float alpha, float *__restrict__ out)
+{
+    const float c = *normp / s;
+    const uint32_t mask = w >= 32 ? 0xffffffffu : ((1u << w) - 1u);
+    const uint64_t quads = M >> 2;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
+        const uint4 wd = *reinterpret_cast<const uint4 *>(words + 4 * t);
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            const uint64_t i0 = (uint64_t)k * M + 4 * t;
+            if (i0 < n) {
+                const uint32_t sh = (uint32_t)k * w;
+                float4 o;
+                o.x = dq(wd.x, sh, mask, sub, c, alpha);
+                o.y = dq(wd.y, sh, mask, sub, c, alpha);
+                o.z = dq(wd.z, sh, mask, sub, c, alpha);
+                o.w = dq(wd.w, sh, mask, sub, c, alpha);
+                store4<MODE>(out, idx, i0, n, o);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// unpacked quantize / dequantize (the literal compress()/decompress() drop-in)
+// ---------------------------------------------------------------------------
+template <int KIND, int MODE, typename QT>
+__global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float *__restrict__ x, uint64_t n,
+                                                          const float *__restrict__ normp, float s, uint32_t level,
+                                                          RngArgs rng, QT *__restrict__ q, int8_t *__restrict__ le,
+                                                          int32_t le_max)
+{
+    const float norm = *normp;
+    const uint64_t groups = (n + 3) >> 2;
+    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t i0 = g << 2;
+        const float4 v = load4<MODE>(x, nullptr, i0, n);
+        const uint4 r = draws4<KIND>(rng, level, i0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (i0 + e < n) {
+                const QElem qe = q_elem(pickf(v, e), norm, s, pick(r, e));
+                q[i0 + e] = (QT)(qe.sg * qe.xi);
+                if (le)
+                    le[i0 + e] = (int8_t)(qe.xi <= le_max ? 1 : 0);
+            }
+        }
+    }
+}
+
+template <typename QT>
+__global__ __launch_bounds__(kBlock) void k_qsgd_dequantize(const QT *__restrict__ q, uint64_t n,
+                                                            const float *__restrict__ normp, float s, float alpha,
+                                                            float *__restrict__ out)
+{
+    const float c = *normp / s;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const float d = c * (float)(int32_t)q[i];
+        out[i] = d * alpha;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// lane pack / unpack of integer arrays
+// ---------------------------------------------------------------------------
+template <int L, typename QT>
+__global__ __launch_bounds__(kBlock) void k_lane_pack(const QT *__restrict__ q, uint64_t n, int32_t off, uint32_t w,
+                                                      uint64_t M, uint32_t *__restrict__ words)
+{
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < M; j += (uint64_t)gridDim.x * kBlock) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            const uint64_t i = (uint64_t)k * M + j;
+            if (i < n)
+                acc |= (uint32_t)((int32_t)q[i] + off) << ((uint32_t)k * w);
+        }
+        words[j] = acc;
+    }
+}
+
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_lane_unpack(const uint32_t *__restrict__ words, uint64_t n, int32_t sub,
+                                                        uint32_t w, uint64_t M, int32_t *__restrict__ q)
+{
+    const uint32_t mask = w >= 32 ? 0xffffffffu : ((1u << w) - 1u);
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < M; j += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t wd = words[j];
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            const uint64_t i = (uint64_t)k * M + j;
+            if (i < n)
+                q[i] = (int32_t)((wd >> ((uint32_t)k * w)) & mask) - sub;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+static RngArgs rng_args(const gc_rng *r, uint64_t n)
+{
+    RngArgs a;
+    a.seed = r->seed;
+    a.offset = r->offset;
+    a.stream = r->stream;
+    a.n = n;
+    return a;
+}
+
+static int check_rng(const gc_rng *r, const char *what)
+{
+    GC_REQUIRE(r, "%s: null rng", what);
+    GC_REQUIRE(r->kind == GC_RNG_PHILOX || r->kind == GC_RNG_STREAM, "%s: unknown rng kind %u", what, r->kind);
+    GC_REQUIRE(r->kind != GC_RNG_STREAM || r->stream, "%s: STREAM rng without a stream pointer", what);
+    return GC_OK;
+}
+
+#define GC_DISPATCH_L(L, ...)                                                    \
+    switch (L) {                                                                 \
+    case 1: { constexpr int LL = 1; __VA_ARGS__; } break;                        \
+    case 2: { constexpr int LL = 2; __VA_ARGS__; } break;                        \
+    case 3: { constexpr int LL = 3; __VA_ARGS__; } break;                        \
+    case 4: { constexpr int LL = 4; __VA_ARGS__; } break;                        \
+    case 5: { constexpr int LL = 5; __VA_ARGS__; } break;                        \
+    case 6: { constexpr int LL = 6; __VA_ARGS__; } break;                        \
+    case 8: { constexpr int LL = 8; __VA_ARGS__; } break;                        \
+    case 10: { constexpr int LL = 10; __VA_ARGS__; } break;                      \
+    case 16: { constexpr int LL = 16; __VA_ARGS__; } break;                      \
+    case 32: { constexpr int LL = 32; __VA_ARGS__; } break;                      \
+    default: return fail(GC_EINVAL, "unsupported lanes per word %u", (unsigned)(L)); \
+    }
+
+template <int L, int KIND, int MODE>
+static void launch_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, float s, int32_t qmax,
+                          const gc_lanes *ln, RngArgs ra, uint32_t *words, hipStream_t st)
+{
+    const uint64_t quads = ln->plane_words >> 2;
+    hipLaunchKernelGGL((k_qsgd_encode<L, KIND, MODE>), dim3(grid_for(quads)), dim3(kBlock), 0, st, x, idx, n, norm,
+                       s, qmax, ln->bits, ln->plane_words, ra, words);
+}
+
+}  // namespace gc
+
+using namespace gc;
+
+extern "C" {
+
+int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, gc_stream_t stream)
+{
+    GC_REQUIRE(norm, "gc_absmax_f32: null norm");
+    GC_REQUIRE(n == 0 || x, "gc_absmax_f32: null x");
+    hipStream_t st = as_stream(stream);
+    if (hipMemsetAsync(norm, 0, sizeof(float), st) != hipSuccess)
+        return launch_status("gc_absmax_f32 memset");
+    if (n == 0)
+        return GC_OK;
+    uint32_t *o = reinterpret_cast<uint32_t *>(norm);
+    if (idx)
+        hipLaunchKernelGGL((k_absmax<2>), dim3(grid_for(n)), dim3(kBlock), 0, st, x, idx, n, o);
+    else if (aligned16(x))
+        hipLaunchKernelGGL((k_absmax<0>), dim3(grid_for(n >> 2)), dim3(kBlock), 0, st, x, idx, n, o);
+    else
+        hipLaunchKernelGGL((k_absmax<1>), dim3(grid_for(n)), dim3(kBlock), 0, st, x, idx, n, o);
+    return launch_status("gc_absmax_f32");
+}
+
+int gc_qsgd_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, uint32_t bits,
+                   const gc_lanes *lanes, const gc_rng *rng, uint32_t *words, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_bits(bits, "gc_qsgd_encode")) || (rc = check_lanes(lanes, n, "gc_qsgd_encode")) ||
+        (rc = check_rng(rng, "gc_qsgd_encode")))
+        return rc;
+    const uint32_t s = (1u << bits) - 1u;
+    GC_REQUIRE(lanes->offset == s && lanes->range == 2ull * s, "gc_qsgd_encode: lanes not made by gc_qsgd_layout");
+    GC_REQUIRE(norm && words, "gc_qsgd_encode: null norm/words");
+    GC_REQUIRE(n == 0 || x, "gc_qsgd_encode: null x");
+    GC_REQUIRE(aligned16(words), "gc_qsgd_encode: words must be 16-byte aligned");
+    if (lanes->plane_words == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const RngArgs ra = rng_args(rng, n);
+    const int mode = idx ? 2 : (aligned16(x) ? 0 : 1);
+    const float sf = (float)s;
+    const int32_t qmax = (int32_t)s;
+    if (rng->kind == GC_RNG_PHILOX) {
+        if (mode == 0) {
+            GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 0, 0>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
+        } else if (mode == 1) {
+            GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 0, 1>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
+        } else {
+            GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 0, 2>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
+        }
+    } else {
+        if (mode == 0) {
+            GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 1, 0>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
+        } else if (mode == 1) {
+            GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 1, 1>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
+        } else {
+            GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 1, 2>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
+        }
+    }
+    return launch_status("gc_qsgd_encode");
+}
+
+int gc_qsgd_decode(const uint32_t *words, const int64_t *idx, uint64_t n, const float *norm, uint32_t bits,
+                   const gc_lanes *lanes, float alpha, float *out, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_bits(bits, "gc_qsgd_decode")) || (rc = check_lanes(lanes, n, "gc_qsgd_decode")))
+        return rc;
+    const uint32_t s = (1u << bits) - 1u;
+    GC_REQUIRE(lanes->offset == s && lanes->range == 2ull * s, "gc_qsgd_decode: lanes not made by gc_qsgd_layout");
+    GC_REQUIRE(norm && words && (n == 0 || out), "gc_qsgd_decode: null pointer");
+    GC_REQUIRE(aligned16(words), "gc_qsgd_decode: words must be 16-byte aligned");
+    if (lanes->plane_words == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const int mode = idx ? 2 : (aligned16(out) ? 0 : 1);
+    const int32_t sub = (int32_t)(lanes->world * s);
+    const unsigned grid = grid_for(lanes->plane_words >> 2);
+    const float sf = (float)s;
+#define GC_DEC(MODE_)                                                                                         \
+    GC_DISPATCH_L(lanes->per_word, hipLaunchKernelGGL((k_qsgd_decode<LL, MODE_>), dim3(grid), dim3(kBlock), 0, \
+                                                      st, words, idx, n, norm, sf, sub, lanes->bits,          \
+                                                      lanes->plane_words, alpha, out))
+    if (mode == 0) {
+        GC_DEC(0);
+    } else if (mode == 1) {
+        GC_DEC(1);
+    } else {
+        GC_DEC(2);
+    }
+#undef GC_DEC
+    return launch_status("gc_qsgd_decode");
+}
+
+int gc_qsgd_quantize(const float *x, uint64_t n, const float *norm, uint32_t bits, const gc_rng *rng,
+                     uint32_t level, void *q, uint32_t q_dtype, gc_stream_t stream)
+{
+    return gc_qsgd_quantize_le(x, n, norm, bits, rng, level, q, q_dtype, nullptr, 0, stream);
+}
+
+int gc_qsgd_quantize_le(const float *x, uint64_t n, const float *norm, uint32_t bits, const gc_rng *rng,
+                        uint32_t level, void *q, uint32_t q_dtype, int8_t *le_mask, uint32_t le_bits,
+                        gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_bits(bits, "gc_qsgd_quantize")) || (rc = check_rng(rng, "gc_qsgd_quantize")))
+        return rc;
+    GC_REQUIRE(q_dtype == GC_I8 || q_dtype == GC_I32, "gc_qsgd_quantize: q_dtype must be GC_I8 or GC_I32");
+    GC_REQUIRE(level < 65536, "gc_qsgd_quantize: level too large");
+    GC_REQUIRE(!le_mask || (le_bits >= 1 && le_bits <= 24), "gc_qsgd_quantize: bad le_bits");
+    GC_REQUIRE(n == 0 || (x && q && norm), "gc_qsgd_quantize: null pointer");
+    if (n == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const RngArgs ra = rng_args(rng, n);
+    const float sf = (float)((1u << bits) - 1u);
+    const int32_t le_max = le_mask ? (int32_t)((1u << le_bits) - 1u) : 0;
+    const unsigned grid = grid_for((n + 3) >> 2);
+    const bool vec = aligned16(x);
+#define GC_Q(KIND_, MODE_, QT_)                                                                                  \
+    hipLaunchKernelGGL((k_qsgd_quantize<KIND_, MODE_, QT_>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, sf, level, \
+                       ra, reinterpret_cast<QT_ *>(q), le_mask, le_max)
+    if (rng->kind == GC_RNG_PHILOX) {
+        if (q_dtype == GC_I8) {
+            if (vec) GC_Q(0, 0, int8_t); else GC_Q(0, 1, int8_t);
+        } else {
+            if (vec) GC_Q(0, 0, int32_t); else GC_Q(0, 1, int32_t);
+        }
+    } else {
+        if (q_dtype == GC_I8) {
+            if (vec) GC_Q(1, 0, int8_t); else GC_Q(1, 1, int8_t);
+        } else {
+            if (vec) GC_Q(1, 0, int32_t); else GC_Q(1, 1, int32_t);
+        }
+    }
+#undef GC_Q
+    return launch_status("gc_qsgd_quantize");
+}
+
+int gc_qsgd_dequantize(const void *q, uint32_t q_dtype, uint64_t n, const float *norm, uint32_t bits, float alpha,
+                       float *out, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_bits(bits, "gc_qsgd_dequantize")))
+        return rc;
+    GC_REQUIRE(q_dtype == GC_I8 || q_dtype == GC_I32, "gc_qsgd_dequantize: q_dtype must be GC_I8 or GC_I32");
+    GC_REQUIRE(n == 0 || (q && out && norm), "gc_qsgd_dequantize: null pointer");
+    if (n == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const float sf = (float)((1u << bits) - 1u);
+    if (q_dtype == GC_I8)
+        hipLaunchKernelGGL((k_qsgd_dequantize<int8_t>), dim3(grid_for(n)), dim3(kBlock), 0, st,
+                           reinterpret_cast<const int8_t *>(q), n, norm, sf, alpha, out);
+    else
+        hipLaunchKernelGGL((k_qsgd_dequantize<int32_t>), dim3(grid_for(n)), dim3(kBlock), 0, st,
+                           reinterpret_cast<const int32_t *>(q), n, norm, sf, alpha, out);
+    return launch_status("gc_qsgd_dequantize");
+}
+
+int gc_lane_pack(const void *q, uint32_t q_dtype, const gc_lanes *lanes, uint32_t *words, gc_stream_t stream)
+{
+    int rc;
+    GC_REQUIRE(lanes, "gc_lane_pack: null lanes");
+    if ((rc = check_lanes(lanes, lanes->n, "gc_lane_pack")))
+        return rc;
+    GC_REQUIRE(q_dtype == GC_I8 || q_dtype == GC_I32, "gc_lane_pack: q_dtype must be GC_I8 or GC_I32");
+    GC_REQUIRE(words && (lanes->n == 0 || q), "gc_lane_pack: null pointer");
+    if (lanes->plane_words == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = grid_for(lanes->plane_words);
+    const int32_t off = (int32_t)lanes->offset;
+    if (q_dtype == GC_I8) {
+        GC_DISPATCH_L(lanes->per_word,
+                      hipLaunchKernelGGL((k_lane_pack<LL, int8_t>), dim3(grid), dim3(kBlock), 0, st,
+                                         reinterpret_cast<const int8_t *>(q), lanes->n, off, lanes->bits,
+                                         lanes->plane_words, words));
+    } else {
+        GC_DISPATCH_L(lanes->per_word,
+                      hipLaunchKernelGGL((k_lane_pack<LL, int32_t>), dim3(grid), dim3(kBlock), 0, st,
+                                         reinterpret_cast<const int32_t *>(q), lanes->n, off, lanes->bits,
+                                         lanes->plane_words, words));
+    }
+    return launch_status("gc_lane_pack");
+}
+
+int gc_lane_unpack(const uint32_t *words, const gc_lanes *lanes, int32_t *q, gc_stream_t stream)
+{
+    int rc;
+    GC_REQUIRE(lanes, "gc_lane_unpack: null lanes");
+    if ((rc = check_lanes(lanes, lanes->n, "gc_lane_unpack")))
+        return rc;
+    GC_REQUIRE(words && (lanes->n == 0 || q), "gc_lane_unpack: null pointer");
+    if (lanes->plane_words == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const int32_t sub = (int32_t)(lanes->world * lanes->offset);
+    GC_DISPATCH_L(lanes->per_word,
+                  hipLaunchKernelGGL((k_lane_unpack<LL>), dim3(grid_for(lanes->plane_words)), dim3(kBlock), 0, st,
+                                     words, lanes->n, sub, lanes->bits, lanes->plane_words, q));
+    return launch_status("gc_lane_unpack");
+}
+
+}  // extern "C"

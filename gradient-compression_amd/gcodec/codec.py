@@ -1,0 +1,370 @@
+"""Tensor-level API over libgcodec (the HIP backend).
+
+Every function takes/returns torch tensors on a gfx950 device, enqueues on
+the current HIP stream and never synchronises (except the torch-mode RNG
+hand-off).  Packed streams are int32 tensors (torch/RCCL have no uint32
+SUM); the bits are the uint32 lane words of include/gcodec.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+DTYPE_CODE = {torch.int8: _lib.GC_I8, torch.int32: _lib.GC_I32, torch.int64: _lib.GC_I64}
+
+
+def _dev(t: torch.Tensor) -> torch.device:
+    if not t.is_cuda:
+        raise _lib.GCodecError(_lib.GC_ENODEV, "gcodec runs on the GPU only: tensor is on "
+                               f"{t.device}; there is no CPU fallback")
+    _lib.require_device(t.device.index if t.device.index is not None else torch.cuda.current_device())
+    return t.device
+
+
+def _stream(device) -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _p(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _f32(x: torch.Tensor, what: str) -> torch.Tensor:
+    if x.dtype != torch.float32:
+        raise _lib.GCodecError(_lib.GC_EINVAL, f"{what}: expected float32, got {x.dtype}")
+    if not x.is_contiguous():
+        x = x.contiguous()
+    return x.view(-1)
+
+
+def _idx(idx, device):
+    if idx is None:
+        return None
+    if not isinstance(idx, torch.Tensor):
+        idx = torch.as_tensor(np.asarray(idx), dtype=torch.int64)
+    if idx.dtype != torch.int64:
+        idx = idx.to(torch.int64)
+    if idx.device != device:
+        idx = idx.to(device, non_blocking=True)
+    return idx.contiguous().view(-1)
+
+
+def norm_tensor(norm, device) -> torch.Tensor:
+    """The max-norm as a device float32 scalar tensor (no host sync)."""
+    if isinstance(norm, torch.Tensor):
+        t = norm.detach()
+        if t.dtype != torch.float32:
+            t = t.float()
+        if t.device != device:
+            t = t.to(device)
+        return t.reshape(1) if t.dim() == 0 else t.view(-1)[:1]
+    return torch.tensor([float(norm)], dtype=torch.float32, device=device)
+
+
+# ---------------------------------------------------------------------------
+# layouts
+# ---------------------------------------------------------------------------
+def qsgd_layout(n: int, bits: int, world: int = 1) -> _lib.gc_lanes:
+    ln = _lib.gc_lanes()
+    check(_lib.load().gc_qsgd_layout(n, bits, world, C.byref(ln)), "gc_qsgd_layout")
+    return ln
+
+
+def lane_layout(n: int, value_range: int, world: int = 1, offset: int = 0) -> _lib.gc_lanes:
+    ln = _lib.gc_lanes()
+    check(_lib.load().gc_lane_layout(n, value_range, world, offset, C.byref(ln)), "gc_lane_layout")
+    return ln
+
+
+def levels_struct(levels) -> _lib.gc_levels:
+    lv = sorted(int(b) for b in levels)
+    if not 1 <= len(lv) <= _lib.GC_MAX_LEVELS:
+        raise _lib.GCodecError(_lib.GC_EINVAL, f"1..{_lib.GC_MAX_LEVELS} levels supported")
+    s = _lib.gc_levels()
+    s.count = len(lv)
+    for i, b in enumerate(lv):
+        s.bits[i] = b
+    return s
+
+
+def ms_layouts(n: int, levels, world: int = 1):
+    lv = levels_struct(levels)
+    ql, ml = _lib.gc_lanes(), _lib.gc_lanes()
+    check(_lib.load().gc_ms_layout(n, C.byref(lv), world, C.byref(ql)), "gc_ms_layout")
+    check(_lib.load().gc_ms_mask_layout(n, C.byref(lv), world, C.byref(ml)), "gc_ms_mask_layout")
+    return ql, ml
+
+
+def mask_words_total(ml: _lib.gc_lanes, levels) -> int:
+    return (len(levels) - 1) * ml.plane_words
+
+
+# ---------------------------------------------------------------------------
+# max-norm
+# ---------------------------------------------------------------------------
+def absmax(x: torch.Tensor, idx=None, out: torch.Tensor | None = None) -> torch.Tensor:
+    dev = _dev(x)
+    x = _f32(x, "absmax")
+    idx = _idx(idx, dev)
+    n = idx.numel() if idx is not None else x.numel()
+    if out is None:
+        out = torch.empty(1, dtype=torch.float32, device=dev)
+    check(_lib.load().gc_absmax_f32(_p(x), _p(idx), n, _p(out), _stream(dev)), "gc_absmax_f32")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# QSGD-MaxNorm packed
+# ---------------------------------------------------------------------------
+def qsgd_encode(x, norm, bits, rng, world=1, idx=None, out=None, lanes=None) -> torch.Tensor:
+    dev = _dev(x)
+    x = _f32(x, "qsgd_encode")
+    idx = _idx(idx, dev)
+    n = idx.numel() if idx is not None else x.numel()
+    lanes = lanes or qsgd_layout(n, bits, world)
+    nt = norm_tensor(norm, dev)
+    if out is None:
+        out = torch.empty(lanes.plane_words, dtype=torch.int32, device=dev)
+    r = rng.struct()
+    check(_lib.load().gc_qsgd_encode(_p(x), _p(idx), n, _p(nt), bits, C.byref(lanes), C.byref(r), _p(out),
+                                     _stream(dev)), "gc_qsgd_encode")
+    return out
+
+
+def qsgd_decode(words, n, norm, bits, world=1, alpha=1.0, idx=None, out=None, lanes=None) -> torch.Tensor:
+    dev = _dev(words)
+    idx = _idx(idx, dev)
+    lanes = lanes or qsgd_layout(n, bits, world)
+    nt = norm_tensor(norm, dev)
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+    check(_lib.load().gc_qsgd_decode(_p(words), _p(idx), n, _p(nt), bits, C.byref(lanes), float(alpha), _p(out),
+                                     _stream(dev)), "gc_qsgd_decode")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# QSGD-MaxNorm unpacked (compressors.py compress/decompress semantics)
+# ---------------------------------------------------------------------------
+def qsgd_quantize(x, norm, bits, rng, level=0, dtype=torch.int8, le_bits=None):
+    dev = _dev(x)
+    x = _f32(x, "qsgd_quantize")
+    nt = norm_tensor(norm, dev)
+    q = torch.empty(x.numel(), dtype=dtype, device=dev)
+    le = torch.empty(x.numel(), dtype=torch.int8, device=dev) if le_bits else None
+    r = rng.struct()
+    check(_lib.load().gc_qsgd_quantize_le(_p(x), x.numel(), _p(nt), bits, C.byref(r), level, _p(q),
+                                          DTYPE_CODE[dtype], _p(le), int(le_bits or 0), _stream(dev)),
+          "gc_qsgd_quantize")
+    return (q, le) if le_bits else q
+
+
+def qsgd_dequantize(q, norm, bits, alpha=1.0, out=None):
+    dev = _dev(q)
+    q = q.contiguous().view(-1)
+    if q.dtype not in (torch.int8, torch.int32):
+        q = q.to(torch.int32)
+    nt = norm_tensor(norm, dev)
+    if out is None:
+        out = torch.empty(q.numel(), dtype=torch.float32, device=dev)
+    check(_lib.load().gc_qsgd_dequantize(_p(q), DTYPE_CODE[q.dtype], q.numel(), _p(nt), bits, float(alpha),
+                                         _p(out), _stream(dev)), "gc_qsgd_dequantize")
+    return out
+
+
+def lane_pack(q, lanes, out=None):
+    dev = _dev(q)
+    q = q.contiguous().view(-1)
+    if q.dtype not in (torch.int8, torch.int32):
+        q = q.to(torch.int32)
+    if out is None:
+        out = torch.empty(lanes.plane_words, dtype=torch.int32, device=dev)
+    check(_lib.load().gc_lane_pack(_p(q), DTYPE_CODE[q.dtype], C.byref(lanes), _p(out), _stream(dev)),
+          "gc_lane_pack")
+    return out
+
+
+def lane_unpack(words, lanes, out=None):
+    dev = _dev(words)
+    if out is None:
+        out = torch.empty(lanes.n, dtype=torch.int32, device=dev)
+    check(_lib.load().gc_lane_unpack(_p(words), C.byref(lanes), _p(out), _stream(dev)), "gc_lane_unpack")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# multi-scale packed
+# ---------------------------------------------------------------------------
+def ms_mask_encode(x, norm, levels, rng, world=1, idx=None, out=None):
+    dev = _dev(x)
+    x = _f32(x, "ms_mask_encode")
+    idx = _idx(idx, dev)
+    n = idx.numel() if idx is not None else x.numel()
+    _, ml = ms_layouts(n, levels, world)
+    lv = levels_struct(levels)
+    nt = norm_tensor(norm, dev)
+    if out is None:
+        out = torch.empty(mask_words_total(ml, levels), dtype=torch.int32, device=dev)
+    r = rng.struct()
+    check(_lib.load().gc_ms_mask_encode(_p(x), _p(idx), n, _p(nt), C.byref(lv), C.byref(r), C.byref(ml), _p(out),
+                                        _stream(dev)), "gc_ms_mask_encode")
+    return out
+
+
+def ms_select_encode(x, norm, levels, rng, mask_words, world=1, idx=None, out=None):
+    dev = _dev(x)
+    x = _f32(x, "ms_select_encode")
+    idx = _idx(idx, dev)
+    n = idx.numel() if idx is not None else x.numel()
+    ql, ml = ms_layouts(n, levels, world)
+    lv = levels_struct(levels)
+    nt = norm_tensor(norm, dev)
+    if out is None:
+        out = torch.empty(ql.plane_words, dtype=torch.int32, device=dev)
+    r = rng.struct()
+    check(_lib.load().gc_ms_select_encode(_p(x), _p(idx), n, _p(nt), C.byref(lv), C.byref(r), _p(mask_words),
+                                          C.byref(ml), C.byref(ql), _p(out), _stream(dev)), "gc_ms_select_encode")
+    return out
+
+
+def ms_decode(words, mask_words, n, norm, levels, world=1, order=0, alpha=1.0, idx=None, out=None):
+    dev = _dev(words)
+    idx = _idx(idx, dev)
+    ql, ml = ms_layouts(n, levels, world)
+    lv = levels_struct(levels)
+    nt = norm_tensor(norm, dev)
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+    check(_lib.load().gc_ms_decode(_p(words), _p(mask_words), _p(idx), n, _p(nt), C.byref(lv), C.byref(ml),
+                                   C.byref(ql), int(order), float(alpha), _p(out), _stream(dev)), "gc_ms_decode")
+    return out
+
+
+def ms_mask_unpack(mask_words, n, levels, world=1):
+    dev = _dev(mask_words)
+    _, ml = ms_layouts(n, levels, world)
+    out = torch.empty(n, dtype=torch.int8, device=dev)
+    check(_lib.load().gc_ms_mask_unpack(_p(mask_words), C.byref(ml), len(levels), _p(out), _stream(dev)),
+          "gc_ms_mask_unpack")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# multi-scale unpacked
+# ---------------------------------------------------------------------------
+def ms_quantize_mask(x, norm, levels, rng):
+    dev = _dev(x)
+    x = _f32(x, "ms_quantize_mask")
+    lv = levels_struct(levels)
+    nt = norm_tensor(norm, dev)
+    mask = torch.empty(x.numel(), dtype=torch.int8, device=dev)
+    r = rng.struct()
+    check(_lib.load().gc_ms_quantize_mask(_p(x), x.numel(), _p(nt), C.byref(lv), C.byref(r), _p(mask),
+                                          _stream(dev)), "gc_ms_quantize_mask")
+    return mask
+
+
+def ms_select_quantize(x, norm, levels, rng, mask, dtype=torch.int8):
+    dev = _dev(x)
+    x = _f32(x, "ms_select_quantize")
+    lv = levels_struct(levels)
+    nt = norm_tensor(norm, dev)
+    mask = mask.to(torch.int8).contiguous().view(-1)
+    q = torch.empty(x.numel(), dtype=dtype, device=dev)
+    r = rng.struct()
+    check(_lib.load().gc_ms_select_quantize(_p(x), x.numel(), _p(nt), C.byref(lv), C.byref(r), _p(mask), _p(q),
+                                            DTYPE_CODE[dtype], _stream(dev)), "gc_ms_select_quantize")
+    return q
+
+
+def ms_dequantize(q, mask, norm, levels, order=0, alpha=1.0):
+    dev = _dev(q)
+    q = q.contiguous().view(-1)
+    if q.dtype not in (torch.int8, torch.int32):
+        q = q.to(torch.int32)
+    mask = mask.to(torch.int8).contiguous().view(-1)
+    lv = levels_struct(levels)
+    nt = norm_tensor(norm, dev)
+    out = torch.empty(q.numel(), dtype=torch.float32, device=dev)
+    check(_lib.load().gc_ms_dequantize(_p(q), DTYPE_CODE[q.dtype], _p(mask), q.numel(), _p(nt), C.byref(lv),
+                                       int(order), float(alpha), _p(out), _stream(dev)), "gc_ms_dequantize")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# torch-generator stream on the GPU
+# ---------------------------------------------------------------------------
+def mt19937_seed_state(seed: int) -> np.ndarray:
+    st = np.empty(625, dtype=np.uint32)
+    check(_lib.load().gc_mt19937_seed(seed, st.ctypes.data_as(C.c_void_p)), "gc_mt19937_seed")
+    return st
+
+
+def mt19937_generate(state_dev: torch.Tensor, count: int, out=None) -> torch.Tensor:
+    dev = _dev(state_dev)
+    if out is None:
+        out = torch.empty(count, dtype=torch.int32, device=dev)
+    check(_lib.load().gc_mt19937_generate(_p(state_dev), _p(out), count, _stream(dev)), "gc_mt19937_generate")
+    return out
+
+
+def mt19937_draws(count: int, device) -> torch.Tensor:
+    """`count` draws of torch's CPU generator, produced on `device`; torch's
+    generator state advances exactly as torch.bernoulli would advance it."""
+    from .rng import set_torch_mt_state, torch_mt_state
+
+    device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    words, idx = torch_mt_state()
+    st = np.empty(625, dtype=np.uint32)
+    st[:624] = words
+    st[624] = idx
+    st_dev = torch.from_numpy(st.view(np.int32)).to(device)
+    out = mt19937_generate(st_dev, count)
+    new = st_dev.cpu().numpy().view(np.uint32)  # synchronises
+    set_torch_mt_state(new[:624], int(new[624]))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# reference-compatible packers
+# ---------------------------------------------------------------------------
+def bytepack8(src: torch.Tensor) -> torch.Tensor:
+    dev = _dev(src)
+    src = src.contiguous().view(-1)
+    if src.dtype not in DTYPE_CODE:
+        src = src.to(torch.int64)
+    out = torch.empty((src.numel() + 7) // 8, dtype=torch.int64, device=dev)
+    check(_lib.load().gc_bytepack8(_p(src), DTYPE_CODE[src.dtype], src.numel(), _p(out), _stream(dev)),
+          "gc_bytepack8")
+    return out
+
+
+def byteunpack8(words: torch.Tensor) -> torch.Tensor:
+    dev = _dev(words)
+    words = words.contiguous().view(-1).to(torch.int64)
+    out = torch.empty(8 * words.numel(), dtype=torch.int8, device=dev)
+    check(_lib.load().gc_byteunpack8(_p(words), words.numel(), _p(out), _stream(dev)), "gc_byteunpack8")
+    return out
+
+
+def greedy4_pack(src: torch.Tensor) -> torch.Tensor:
+    """Host implementation of the reference's sequential greedy format
+    (extensions/Extension CPU/bitpacking.cpp); device tensors are staged."""
+    a = np.ascontiguousarray(src.detach().cpu().numpy().astype(np.int32, copy=False)).reshape(-1)
+    out = np.empty(a.size + 1, dtype=np.int32)
+    nw = check(_lib.load().gc_greedy4_pack(a.ctypes.data_as(C.c_void_p), a.size, out.ctypes.data_as(C.c_void_p),
+                                           out.size), "gc_greedy4_pack")
+    return torch.from_numpy(out[:nw].copy()).to(src.device)
+
+
+def greedy4_unpack(words: torch.Tensor) -> torch.Tensor:
+    a = np.ascontiguousarray(words.detach().cpu().numpy().astype(np.int32, copy=False)).reshape(-1)
+    out = np.empty(15 * a.size + 1, dtype=np.int32)
+    cnt = check(_lib.load().gc_greedy4_unpack(a.ctypes.data_as(C.c_void_p), a.size, out.ctypes.data_as(C.c_void_p),
+                                              out.size), "gc_greedy4_unpack")
+    return torch.from_numpy(out[:cnt].copy()).to(words.device)

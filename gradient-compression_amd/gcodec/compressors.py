@@ -1,0 +1,165 @@
+"""Drop-in compressor classes with the reference's names, constructor
+arguments and method signatures (compressors.py), backed by the gfx950 HIP
+kernels of libgcodec.
+
+    reference (compressors.py)                       here
+    QSGDMaxNormCompressor            283-321         QSGDMaxNormCompressor
+    GlobalRandKMaxNormCompressor     419-456         GlobalRandKMaxNormCompressor
+    QSGDMaxNormTwoScaleCompressor    612-680         QSGDMaxNormTwoScaleCompressor
+    GlobalRandKMaxNormTwoScaleCompressor 683-751     GlobalRandKMaxNormTwoScaleCompressor
+    QSGDMaxNormMultiScaleCompressor  754-826         QSGDMaxNormMultiScaleCompressor
+
+compress()/decompress() return exactly what the reference returns (int8 for
+b < 8 else int32; float32), on the same device.  With the generator in
+"torch" mode (gcodec.manual_seed(seed, mode="torch") or
+gcodec.set_rng_mode("torch")) the draws are torch's CPU-generator stream, so
+`torch.manual_seed(s); c.compress(norm, x)` is bit-identical to the
+reference.  Each class also offers the packed, all-reduce-compatible
+encode()/decode() the reducers use.
+
+Divergences (documented in DESIGN.md): a zero / non-finite max-norm gives
+q = 0 where torch.bernoulli raises; the multi-scale constructor copies and
+sorts the caller's level list instead of sorting it in place (768).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import codec as _codec
+from .rng import default_generator
+
+
+def _qdtype(bits: int) -> torch.dtype:
+    # compressors.py:294-297
+    return torch.int8 if bits < 8 else torch.int32
+
+
+class _Base:
+    backend = _codec
+
+    def __init__(self, device, generator=None):
+        self._device = device
+        self._gen = generator or default_generator
+
+    def _reserve(self, n: int, levels: int, device):
+        return self._gen.reserve(n, levels, device=device, backend=self.backend)
+
+
+class QSGDMaxNormCompressor(_Base):
+    """compressors.py:283-321.  Code: sign array * xi array."""
+
+    def __init__(self, device, quantization_level=8, generator=None):
+        super().__init__(device, generator)
+        self._quantization_level = quantization_level
+        self._dtype = _qdtype(quantization_level)
+
+    def compress(self, norm, tensor):
+        rng = self._reserve(tensor.numel(), 1, tensor.device)
+        return self.backend.qsgd_quantize(tensor, norm, self._quantization_level, rng, 0, self._dtype)
+
+    def decompress(self, norm, sign_xi_array):
+        return self.backend.qsgd_dequantize(sign_xi_array, norm, self._quantization_level)
+
+    # packed, SUM-all-reduce-compatible stream (carry-free lanes for `world`)
+    def encode(self, norm, tensor, world=1, idx=None, out=None):
+        n = idx.numel() if idx is not None else tensor.numel()
+        rng = self._reserve(n, 1, tensor.device)
+        return self.backend.qsgd_encode(tensor, norm, self._quantization_level, rng, world, idx, out)
+
+    def decode(self, norm, words, n, world=1, alpha=1.0, idx=None, out=None):
+        return self.backend.qsgd_decode(words, n, norm, self._quantization_level, world, alpha, idx, out)
+
+
+class GlobalRandKMaxNormCompressor(QSGDMaxNormCompressor):
+    """compressors.py:419-456 — the same arithmetic applied to the K-subset."""
+
+
+class QSGDMaxNormTwoScaleCompressor(_Base):
+    """compressors.py:612-680.  compress_lower consumes draws [0, n) and
+    compress_higher [n, 2n) of one reservation (level 0 / level 1)."""
+
+    def __init__(self, device, lower_quantization_level=6, higher_quantization_level=10, generator=None):
+        super().__init__(device, generator)
+        self._lower_quantization_level = lower_quantization_level
+        self._higher_quantization_level = higher_quantization_level
+        self._dtype = _qdtype(lower_quantization_level)
+        self._rng = None
+
+    @property
+    def levels(self):
+        return [self._lower_quantization_level, self._higher_quantization_level]
+
+    def compress_lower(self, norm, tensor):
+        self._rng = self._reserve(tensor.numel(), 2, tensor.device)
+        return self.backend.qsgd_quantize(tensor, norm, self._lower_quantization_level, self._rng, 0, self._dtype)
+
+    def compress_higher(self, norm, tensor):
+        if self._rng is None or self._rng.n != tensor.numel():
+            self._rng = self._reserve(tensor.numel(), 2, tensor.device)
+        q, h = self.backend.qsgd_quantize(tensor, norm, self._higher_quantization_level, self._rng, 1, self._dtype,
+                                          le_bits=self._lower_quantization_level)
+        self._rng = None
+        return q, h
+
+    def decompress(self, norm, sign_xi_array, higher_resolution_mask):
+        return self.backend.ms_dequantize(sign_xi_array, higher_resolution_mask, norm, self.levels, order=1)
+
+    # packed: mask + select over the two levels (thermometer mask lanes)
+    def encode_mask(self, norm, tensor, world=1, idx=None):
+        n = idx.numel() if idx is not None else tensor.numel()
+        self._rng = self._reserve(n, 2, tensor.device)
+        return self.backend.ms_mask_encode(tensor, norm, self.levels, self._rng, world, idx)
+
+    def encode(self, norm, tensor, mask_words, world=1, idx=None):
+        return self.backend.ms_select_encode(tensor, norm, self.levels, self._rng, mask_words, world, idx)
+
+    def decode(self, norm, words, mask_words, n, world=1, alpha=1.0, idx=None, out=None):
+        return self.backend.ms_decode(words, mask_words, n, norm, self.levels, world, 1, alpha, idx, out)
+
+
+class GlobalRandKMaxNormTwoScaleCompressor(QSGDMaxNormTwoScaleCompressor):
+    """compressors.py:683-751 — identical arithmetic on the K-subset."""
+
+
+class QSGDMaxNormMultiScaleCompressor(_Base):
+    """compressors.py:754-826.  No L x n float cache: the select pass
+    recomputes the chosen level from the same reserved draws."""
+
+    def __init__(self, device, quantization_levels=None, generator=None):
+        super().__init__(device, generator)
+        if not quantization_levels:
+            quantization_levels = [6, 10]
+        self._quantization_levels = sorted(quantization_levels)
+        self._dtype = _qdtype(self._quantization_levels[0])
+        self._rng = None
+        self._x = None
+        self._norm = None
+
+    def compress_cache(self, norm, tensor):
+        self._rng = self._reserve(tensor.numel(), len(self._quantization_levels), tensor.device)
+        self._x, self._norm = tensor, norm
+
+    def compress_mask(self, norm, tensor):
+        self.compress_cache(norm, tensor)
+        return self.backend.ms_quantize_mask(tensor, norm, self._quantization_levels, self._rng)
+
+    def compress(self, resolution_mask):
+        return self.backend.ms_select_quantize(self._x, self._norm, self._quantization_levels, self._rng,
+                                               resolution_mask, self._dtype)
+
+    def decompress(self, norm, sign_xi_array, resolution_mask):
+        return self.backend.ms_dequantize(sign_xi_array, resolution_mask, norm, self._quantization_levels, order=0)
+
+    # packed
+    def encode_mask(self, norm, tensor, world=1, idx=None):
+        n = idx.numel() if idx is not None else tensor.numel()
+        self._rng = self._reserve(n, len(self._quantization_levels), tensor.device)
+        return self.backend.ms_mask_encode(tensor, norm, self._quantization_levels, self._rng, world, idx)
+
+    def encode(self, norm, tensor, mask_words, world=1, idx=None):
+        return self.backend.ms_select_encode(tensor, norm, self._quantization_levels, self._rng, mask_words, world,
+                                             idx)
+
+    def decode(self, norm, words, mask_words, n, world=1, alpha=1.0, idx=None, out=None):
+        return self.backend.ms_decode(words, mask_words, n, norm, self._quantization_levels, world, 0, alpha, idx,
+                                      out)

@@ -1,0 +1,271 @@
+"""Data-parallel reducers with the reference's names and phase structure
+(reducer.py), on the packed carry-free codec and RCCL.
+
+    reference (reducer.py)                              here
+    Reducer / TensorBuffer                 26-68        Reducer / TensorBuffer
+    QSGDMaxNormReducer                     498-554      QSGDMaxNormReducer
+    GlobalRandKMaxNormReducer              697-766      GlobalRandKMaxNormReducer
+    QSGDMaxNormTwoScaleReducer             1454-1531    QSGDMaxNormTwoScaleReducer
+    GlobalRandKMaxNormTwoScaleReducer      1534-1633    GlobalRandKMaxNormTwoScaleReducer
+    QSGDMaxNormMultiScaleReducer           1636-1715    QSGDMaxNormMultiScaleReducer
+
+Per step: flatten -> local max-norm (HIP) -> all_reduce MAX (4 B) ->
+[multi-scale: mask encode -> all_reduce SUM of thermometer lanes] -> encode
+(quantize + pack, HIP) -> ONE all_reduce SUM of the packed uint32 words ->
+decode (+ 1/W, HIP) -> setgrad.  The reference all-gathers the norm and
+all-reduces int8/int32 q (which overflows int8 once W*(2^b-1) > 127); the
+packed lanes are sized for W so the SUM never carries (SURVEY §7 hard part 4).
+Outputs equal the reference's (torch-mode RNG) for every W where the
+reference does not overflow.
+"""
+from __future__ import annotations
+
+import contextlib
+import random
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import codec as _hip_codec
+from . import compressors as C
+from .rng import default_generator
+
+
+class _NullTimer:
+    def __call__(self, label, epoch=-1.0, verbosity=1):
+        return contextlib.nullcontext()
+
+
+def set_seed(seed: int, generator=None):
+    """seed.py:6-11 plus the codec's own generator."""
+    np.random.seed(seed)
+    random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+    (generator or default_generator).manual_seed(seed)
+
+
+class Reducer:
+    """reducer.py:26-43."""
+
+    def __init__(self, device, timer=None, codec=None, generator=None, group=None):
+        if dist.is_available() and dist.is_initialized():
+            self.n_workers = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
+        else:
+            self.n_workers = 1
+            self.rank = 0
+        self._device = device
+        self._timer = timer or _NullTimer()
+        self._codec = codec or _hip_codec
+        self._gen = generator or default_generator
+        self._group = group
+
+    def reduce(self, grad_in, grad_out):
+        raise NotImplementedError()
+
+    # -- collectives (RCCL over xGMI when the group is "nccl") -------------
+    def _all_reduce(self, t, op=dist.ReduceOp.SUM):
+        if self.n_workers > 1:
+            dist.all_reduce(t, op=op, group=self._group)
+        return t
+
+    def _norm(self, buffer, idx=None):
+        norm = self._codec.absmax(buffer, idx=idx)
+        return self._all_reduce(norm, dist.ReduceOp.MAX)
+
+    def _compressor(self, cls, *args):
+        c = cls(self._device, *args, generator=self._gen)
+        c.backend = self._codec
+        return c
+
+    @staticmethod
+    def n_bits(tensor):
+        return 8 * tensor.nelement() * tensor.element_size()
+
+    def _setgrad(self, flat, grad_out):
+        """reducer.py:543-549 (the 1/W is already folded into `flat`)."""
+        for grad, out in zip(flat, grad_out):
+            out.copy_(grad)
+
+
+class TensorBuffer:
+    """reducer.py:46-68: flatten a list of tensors into one fp32 bucket."""
+
+    def __init__(self, tensors):
+        indices = [0]
+        for tensor in tensors:
+            indices.append(indices[-1] + tensor.nelement())
+        self._start_idx = indices[:-1]
+        self._end_idx = indices[1:]
+        self._len_tensors = len(tensors)
+        self._tensor_shapes = [tensor.size() for tensor in tensors]
+        self.buffer = torch.cat([tensor.reshape(-1) for tensor in tensors])
+
+    def __getitem__(self, index):
+        return self.buffer[self._start_idx[index]:self._end_idx[index]].view(self._tensor_shapes[index])
+
+    def __len__(self):
+        return self._len_tensors
+
+    def with_buffer(self, buffer):
+        self.buffer = buffer
+        return self
+
+
+class QSGDMaxNormReducer(Reducer):
+    """reducer.py:498-554."""
+
+    def __init__(self, device, timer=None, quantization_level=8, **kw):
+        super().__init__(device, timer, **kw)
+        self._quantization_level = quantization_level
+
+    def reduce(self, grad_in, grad_out):
+        W = self.n_workers
+        comp = self._compressor(C.QSGDMaxNormCompressor, self._quantization_level)
+        with self._timer("reduce.flat_pack"):
+            flat = TensorBuffer(grad_in)
+        n = flat.buffer.numel()
+        with self._timer("reduce.norm", verbosity=2):
+            norm = self._norm(flat.buffer)
+        with self._timer("reduce.compress", verbosity=2):
+            words = comp.encode(norm, flat.buffer, world=W)
+        with self._timer("reduce.reduce.vector", verbosity=2):
+            self._all_reduce(words)
+        bits = self.n_bits(norm) + self.n_bits(words)
+        with self._timer("reduce.decompress", verbosity=2):
+            flat.buffer = comp.decode(norm, words, n, world=W, alpha=1.0 / W)
+        with self._timer("reduce.setgrad", verbosity=2):
+            self._setgrad(flat, grad_out)
+        return bits
+
+
+class GlobalRandKMaxNormReducer(Reducer):
+    """reducer.py:697-766: K coordinates per step from a seeded permutation,
+    popped from the end; unselected coordinates keep the local gradient."""
+
+    def __init__(self, device, timer=None, seed=42, K=10000, quantization_level=8, **kw):
+        super().__init__(device, timer, **kw)
+        self._quantization_level = quantization_level
+        self._seed = seed
+        self._K = K
+        self._indices_queue = []
+
+    def _next_indices(self, n):
+        if not self._indices_queue:
+            set_seed(self._seed, self._gen)
+            self._indices_queue = list(torch.randperm(n).split(self._K))
+        return self._indices_queue.pop()
+
+    def _randk_compressor(self):
+        return self._compressor(C.GlobalRandKMaxNormCompressor, self._quantization_level)
+
+    def reduce(self, grad_in, grad_out):
+        W = self.n_workers
+        comp = self._randk_compressor()
+        with self._timer("reduce.flat_pack"):
+            flat = TensorBuffer(grad_in)
+        n = flat.buffer.numel()
+        idx = self._next_indices(n).to(flat.buffer.device, non_blocking=True)
+        k = idx.numel()
+        with self._timer("reduce.norm", verbosity=2):
+            norm = self._norm(flat.buffer, idx)
+        with self._timer("reduce.compress", verbosity=2):
+            words = comp.encode(norm, flat.buffer, world=W, idx=idx)
+        with self._timer("reduce.reduce.vector", verbosity=2):
+            self._all_reduce(words)
+        bits = self.n_bits(norm) + self.n_bits(words)
+        with self._timer("reduce.decompress", verbosity=2):
+            comp.decode(norm, words, k, world=W, alpha=1.0, idx=idx, out=flat.buffer)
+        with self._timer("reduce.setgrad", verbosity=2):
+            flat.buffer = flat.buffer * (1.0 / W) if W > 1 else flat.buffer
+            self._setgrad(flat, grad_out)
+        return bits
+
+
+class QSGDMaxNormTwoScaleReducer(Reducer):
+    """reducer.py:1454-1531: common high-resolution mask (AND over ranks),
+    blended two-scale integers, one integer all-reduce."""
+
+    _cls = C.QSGDMaxNormTwoScaleCompressor
+
+    def __init__(self, device, timer=None, lower_quantization_level=6, higher_quantization_level=10, **kw):
+        super().__init__(device, timer, **kw)
+        self._lower_quantization_level = lower_quantization_level
+        self._higher_quantization_level = higher_quantization_level
+
+    def _make(self):
+        return self._compressor(self._cls, self._lower_quantization_level, self._higher_quantization_level)
+
+    def _reduce_scales(self, comp, flat, idx, n):
+        W = self.n_workers
+        with self._timer("reduce.norm", verbosity=2):
+            norm = self._norm(flat.buffer, idx)
+        with self._timer("reduce.compress", verbosity=2):
+            mask = comp.encode_mask(norm, flat.buffer, world=W, idx=idx)
+            self._all_reduce(mask)
+            words = comp.encode(norm, flat.buffer, mask, world=W, idx=idx)
+        with self._timer("reduce.reduce.vector", verbosity=2):
+            self._all_reduce(words)
+        bits = self.n_bits(norm) + self.n_bits(mask) + self.n_bits(words)
+        return norm, mask, words, bits
+
+    def reduce(self, grad_in, grad_out):
+        W = self.n_workers
+        comp = self._make()
+        with self._timer("reduce.flat_pack"):
+            flat = TensorBuffer(grad_in)
+        n = flat.buffer.numel()
+        norm, mask, words, bits = self._reduce_scales(comp, flat, None, n)
+        with self._timer("reduce.decompress", verbosity=2):
+            flat.buffer = comp.decode(norm, words, mask, n, world=W, alpha=1.0 / W)
+        with self._timer("reduce.setgrad", verbosity=2):
+            self._setgrad(flat, grad_out)
+        return bits
+
+
+class GlobalRandKMaxNormTwoScaleReducer(QSGDMaxNormTwoScaleReducer):
+    """reducer.py:1534-1633."""
+
+    _cls = C.GlobalRandKMaxNormTwoScaleCompressor
+
+    def __init__(self, device, timer=None, seed=42, K=10000, lower_quantization_level=6,
+                 higher_quantization_level=10, **kw):
+        super().__init__(device, timer, lower_quantization_level, higher_quantization_level, **kw)
+        self._seed = seed
+        self._K = K
+        self._indices_queue = []
+
+    _next_indices = GlobalRandKMaxNormReducer._next_indices
+
+    def reduce(self, grad_in, grad_out):
+        W = self.n_workers
+        comp = self._make()
+        with self._timer("reduce.flat_pack"):
+            flat = TensorBuffer(grad_in)
+        n = flat.buffer.numel()
+        idx = self._next_indices(n).to(flat.buffer.device, non_blocking=True)
+        k = idx.numel()
+        norm, mask, words, bits = self._reduce_scales(comp, flat, idx, k)
+        with self._timer("reduce.decompress", verbosity=2):
+            comp.decode(norm, words, mask, k, world=W, alpha=1.0, idx=idx, out=flat.buffer)
+        with self._timer("reduce.setgrad", verbosity=2):
+            flat.buffer = flat.buffer * (1.0 / W) if W > 1 else flat.buffer
+            self._setgrad(flat, grad_out)
+        return bits
+
+
+class QSGDMaxNormMultiScaleReducer(QSGDMaxNormTwoScaleReducer):
+    """reducer.py:1636-1715: resolution mask MIN over ranks (thermometer lanes
+    + SUM), selected-level integers, one integer all-reduce."""
+
+    def __init__(self, device, timer=None, quantization_levels=None, **kw):
+        Reducer.__init__(self, device, timer, **kw)
+        if not quantization_levels:
+            quantization_levels = [6, 10]
+        self._quantization_levels = sorted(quantization_levels)
+
+    def _make(self):
+        return self._compressor(C.QSGDMaxNormMultiScaleCompressor, list(self._quantization_levels))

@@ -1,0 +1,187 @@
+/*
+ * gcodec.h — C ABI of libgcodec, the MI355X-native (gfx950) QSGD-MaxNorm
+ * gradient codec.
+ *
+ * Plain C: raw pointers, sizes and an opaque stream handle; no torch or HIP
+ * types.  Every device entry point takes caller-owned device buffers, never
+ * allocates, never synchronises the host, and enqueues on `stream` (a
+ * hipStream_t passed as void*; NULL = the legacy default stream), so a call
+ * sequence is hipGraph-capturable.  Status: 0 = GC_OK, negative = error;
+ * gc_last_error() returns a thread-local description of the last failure.
+ *
+ * Reference interfaces each entry point replaces (vineeths96/
+ * Gradient-Compression; file:line):
+ *   gc_absmax_f32 ............ reducer.py:516,726,1478,1577,1663  buffer.abs().max()
+ *   gc_qsgd_encode ........... compressors.py:299-316 QSGDMaxNormCompressor.compress
+ *                              (+ GlobalRandKMaxNormCompressor.compress 435-451 with idx)
+ *                              fused with the packing intent of compressors.py:357-358 /
+ *                              extensions/Extension CPU/bitpacking.cpp:5-61 (carry-free lanes)
+ *   gc_qsgd_decode ........... compressors.py:318-321 decompress (+ reducer.py:549 alpha=1/W,
+ *                              + reducer.py:754 scatter with idx)
+ *   gc_qsgd_quantize ......... compressors.py:299-316, unpacked int8/int32 output (literal drop-in)
+ *   gc_qsgd_dequantize ....... compressors.py:318-321, unpacked input
+ *   gc_lane_pack/_unpack ..... extensions/Extension GPU/gpu_bitpacking.cpp:5-125 intent
+ *                              (device packing of quantized ints), sum-compatible format
+ *   gc_ms_mask_encode ........ compressors.py:778-807 compress_cache + compress_mask
+ *                              (= TwoScale compress_lower/compress_higher 630-666 for 2 levels)
+ *   gc_ms_select_encode ...... compressors.py:809-817 compress(mask) (+ reducer.py:1503-1505 blend)
+ *   gc_ms_decode ............. compressors.py:819-826 (order 0) / 668-680 (order 1)
+ *   gc_mt19937_seed/_generate  seed.py:6-11 torch.manual_seed + torch CPU generator stream
+ *                              consumed by torch.bernoulli (compressors.py:310)
+ *   gc_greedy4_pack/_unpack .. extensions/Extension CPU/bitpacking.cpp:5-124 (host, same format)
+ *   gc_bytepack8/_unpack8 .... extensions/Extension CPU BP/bytepacking.cpp:6-64 (device)
+ */
+#ifndef GCODEC_H
+#define GCODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GC_ABI_VERSION 1
+
+/* status codes */
+#define GC_OK 0
+#define GC_EINVAL (-1)  /* bad argument (null pointer, bits, layout mismatch) */
+#define GC_EHIP (-2)    /* HIP runtime / launch error */
+#define GC_ERANGE (-3)  /* value outside the format's domain (greedy4: <0 or >255) */
+#define GC_ENOSPC (-4)  /* output capacity too small */
+#define GC_ENODEV (-5)  /* no gfx950 device */
+
+/* element dtypes for the unpacked-integer entry points */
+#define GC_I8 1u
+#define GC_I32 4u
+#define GC_I64 8u
+
+/* random streams for the stochastic rounding */
+#define GC_RNG_PHILOX 0u /* Philox4x32-10 keyed by seed, counter (element>>2, level, offset) */
+#define GC_RNG_STREAM 1u /* caller-supplied 32-bit draws, level-major: stream[level*n + i] */
+
+typedef void *gc_stream_t; /* hipStream_t */
+
+typedef struct gc_rng {
+    uint32_t kind;          /* GC_RNG_PHILOX | GC_RNG_STREAM */
+    uint32_t reserved;      /* 0 */
+    uint64_t seed;          /* PHILOX key */
+    uint64_t offset;        /* PHILOX: draws consumed before this call (counter high words) */
+    const uint32_t *stream; /* STREAM: device pointer to the draws */
+} gc_rng;
+
+/* Carry-free planar lane layout of a packed stream.
+ * Each element contributes a lane value in [0, range] (offset binary:
+ * lane = q + offset).  Lanes are `bits` wide with bits = bit_length(world*range),
+ * so a SUM all-reduce of the uint32 words over `world` ranks never carries
+ * between lanes.  per_word = floor(32/bits) lanes per word.  Planar: word j
+ * holds elements j, j+M, ..., j+(per_word-1)*M, M = plane_words =
+ * roundup(ceil(n/per_word), 64).  Elements >= n contribute 0 bits. */
+typedef struct gc_lanes {
+    uint64_t n;           /* elements */
+    uint64_t plane_words; /* M = words in the stream */
+    uint32_t bits;        /* lane width w */
+    uint32_t per_word;    /* L */
+    uint32_t offset;      /* lane = q + offset */
+    uint32_t world;       /* W the lanes were sized for */
+    uint64_t range;       /* per-rank lane value range [0, range] */
+} gc_lanes;
+
+/* ascending quantization levels (bits) of the multi-scale codec */
+#define GC_MAX_LEVELS 8
+typedef struct gc_levels {
+    uint32_t count;
+    uint32_t bits[GC_MAX_LEVELS];
+} gc_levels;
+
+/* ---- library ---------------------------------------------------------- */
+const char *gc_version(void);
+const char *gc_last_error(void);
+int gc_abi_version(void);
+int gc_device_check(int device); /* GC_OK if `device` is a gfx950 GPU */
+
+/* ---- layouts (host, pure) ---------------------------------------------- */
+int gc_lane_layout(uint64_t n, uint64_t range, uint32_t world, uint32_t offset, gc_lanes *out);
+/* QSGD lanes: range 2s, offset s, s = 2^bits-1 */
+int gc_qsgd_layout(uint64_t n, uint32_t bits, uint32_t world, gc_lanes *out);
+/* multi-scale q lanes: qmax = s_0 (2 levels) or s_0+1 (>=3 levels) */
+int gc_ms_layout(uint64_t n, const gc_levels *levels, uint32_t world, gc_lanes *out);
+/* multi-scale mask lanes: (count-1) thermometer fields of range 1, each its own
+ * stream of plane_words; total words = (count-1)*plane_words */
+int gc_ms_mask_layout(uint64_t n, const gc_levels *levels, uint32_t world, gc_lanes *out);
+
+/* ---- max-norm ----------------------------------------------------------- */
+/* *norm = max_i |x[idx ? idx[i] : i]| over i < n (NaN-propagating); norm is a
+ * device float overwritten by the call. */
+int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, gc_stream_t stream);
+
+/* ---- QSGD-MaxNorm ------------------------------------------------------- */
+/* words[lanes->plane_words] = pack(q + s), q = stochastic_round(x[idx?idx[i]:i], *norm, bits) */
+int gc_qsgd_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, uint32_t bits,
+                   const gc_lanes *lanes, const gc_rng *rng, uint32_t *words, gc_stream_t stream);
+/* out[idx?idx[i]:i] = RN(RN(RN(*norm/s) * (lane_sum - W*s)) * alpha) */
+int gc_qsgd_decode(const uint32_t *words, const int64_t *idx, uint64_t n, const float *norm, uint32_t bits,
+                   const gc_lanes *lanes, float alpha, float *out, gc_stream_t stream);
+/* unpacked: q[i] (GC_I8 | GC_I32, wraps like torch .to()) for draw block `level` */
+int gc_qsgd_quantize(const float *x, uint64_t n, const float *norm, uint32_t bits, const gc_rng *rng,
+                     uint32_t level, void *q, uint32_t q_dtype, gc_stream_t stream);
+/* as gc_qsgd_quantize; also le_mask[i] = (|q[i]| <= 2^le_bits - 1) computed on the
+ * unwrapped magnitude — compressors.py:660 higher_resolution_mask of compress_higher */
+int gc_qsgd_quantize_le(const float *x, uint64_t n, const float *norm, uint32_t bits, const gc_rng *rng,
+                        uint32_t level, void *q, uint32_t q_dtype, int8_t *le_mask, uint32_t le_bits,
+                        gc_stream_t stream);
+/* out[i] = RN(RN(RN(*norm/s) * q[i]) * alpha) */
+int gc_qsgd_dequantize(const void *q, uint32_t q_dtype, uint64_t n, const float *norm, uint32_t bits,
+                       float alpha, float *out, gc_stream_t stream);
+
+/* ---- lane packing of already-quantized integers -------------------------- */
+int gc_lane_pack(const void *q, uint32_t q_dtype, const gc_lanes *lanes, uint32_t *words, gc_stream_t stream);
+/* q[i] = lane - world*offset (the W-way sum) */
+int gc_lane_unpack(const uint32_t *words, const gc_lanes *lanes, int32_t *q, gc_stream_t stream);
+
+/* ---- multi-scale / two-scale --------------------------------------------- */
+int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, const gc_levels *levels,
+                      const gc_rng *rng, const gc_lanes *mask_lanes, uint32_t *mask_words, gc_stream_t stream);
+/* mask_words: the (W-summed) thermometer stream; selected level m = #fields with sum == W */
+int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm,
+                        const gc_levels *levels, const gc_rng *rng, const uint32_t *mask_words,
+                        const gc_lanes *mask_lanes, const gc_lanes *q_lanes, uint32_t *words,
+                        gc_stream_t stream);
+/* order 0: RN(RN(Q*norm)/s_m) (multi-scale); order 1: RN(RN(norm/s_m)*Q) (two-scale); then *alpha */
+int gc_ms_decode(const uint32_t *words, const uint32_t *mask_words, const int64_t *idx, uint64_t n,
+                 const float *norm, const gc_levels *levels, const gc_lanes *mask_lanes,
+                 const gc_lanes *q_lanes, int order, float alpha, float *out, gc_stream_t stream);
+/* unpacked selected level per element (int8), from a thermometer stream */
+int gc_ms_mask_unpack(const uint32_t *mask_words, const gc_lanes *mask_lanes, uint32_t levels_count,
+                      int8_t *mask, gc_stream_t stream);
+/* unpacked forms (the literal compressor drop-ins): int8 resolution mask
+ * (compressors.py:799-807), select (809-817), decompress (819-826 / 668-680) */
+int gc_ms_quantize_mask(const float *x, uint64_t n, const float *norm, const gc_levels *levels, const gc_rng *rng,
+                        int8_t *mask, gc_stream_t stream);
+int gc_ms_select_quantize(const float *x, uint64_t n, const float *norm, const gc_levels *levels,
+                          const gc_rng *rng, const int8_t *mask, void *q, uint32_t q_dtype, gc_stream_t stream);
+int gc_ms_dequantize(const void *q, uint32_t q_dtype, const int8_t *mask, uint64_t n, const float *norm,
+                     const gc_levels *levels, int order, float alpha, float *out, gc_stream_t stream);
+
+/* ---- torch CPU generator stream (MT19937) -------------------------------- */
+/* state = 624 words + next index (625 uint32); index 624 = block exhausted */
+int gc_mt19937_seed(uint64_t seed, uint32_t *state_host);
+/* out[count] = next `count` draws; state_dev (625 words, device) advances */
+int gc_mt19937_generate(uint32_t *state_dev, uint32_t *out, uint64_t count, gc_stream_t stream);
+
+/* ---- reference-compatible packers ----------------------------------------- */
+/* greedy 4-mode format of extensions/Extension CPU/bitpacking.cpp (host
+ * buffers); returns words / elements written or a negative status */
+int64_t gc_greedy4_pack(const int32_t *src, uint64_t n, int32_t *out, uint64_t cap);
+int64_t gc_greedy4_unpack(const int32_t *src, uint64_t nwords, int32_t *out, uint64_t cap);
+/* 8 x (v & 0xFF) per int64, MSB-first (extensions/Extension CPU BP), device */
+int gc_bytepack8(const void *src, uint32_t src_dtype, uint64_t n, int64_t *out, gc_stream_t stream);
+int gc_byteunpack8(const int64_t *src, uint64_t nwords, int8_t *out, gc_stream_t stream);
+/* host-buffer forms (the reference's byte packer is a CPU extension) */
+int gc_bytepack8_host(const int64_t *src, uint64_t n, int64_t *out);
+int gc_byteunpack8_host(const int64_t *src, uint64_t nwords, int8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GCODEC_H */

@@ -1,0 +1,150 @@
+"""CPU-side checks of the C ABI: the library loads, exports every symbol
+include/gcodec.h declares, and its pure host functions (layouts, error
+reporting, greedy-4 / byte packers) behave — no device calls."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gcodec.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(gc_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_the_entry_points():
+    syms = declared_symbols()
+    for s in ("gc_absmax_f32", "gc_qsgd_encode", "gc_qsgd_decode", "gc_ms_mask_encode", "gc_ms_select_encode",
+              "gc_ms_decode", "gc_mt19937_generate", "gc_greedy4_pack", "gc_bytepack8", "gc_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from gcodec import _lib
+
+    lib = _lib.load()
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    # the ctypes table covers the header exactly
+    assert set(_lib.SIGNATURES) == set(declared_symbols())
+
+
+def test_version_and_abi():
+    from gcodec import _lib
+
+    assert _lib.load().gc_abi_version() == 1
+    assert b"gfx950" in _lib.load().gc_version()
+
+
+def test_layouts_match_oracle():
+    from gcodec import codec
+    from oracle import oracle as O
+
+    for n in (0, 1, 5, 64, 1000, 23_520_842, 100_000_000):
+        for bits in (1, 2, 4, 8, 12):
+            for world in (1, 2, 3, 8):
+                ln = codec.qsgd_layout(n, bits, world)
+                s = (1 << bits) - 1
+                assert (ln.bits, ln.per_word, ln.plane_words) == O.lane_layout(n, 2 * s, world)
+                assert ln.per_word * ln.plane_words >= n and ln.plane_words % 64 == 0
+                assert world * 2 * s < (1 << ln.bits)
+
+
+def test_ms_layouts():
+    from gcodec import codec
+
+    ql, ml = codec.ms_layouts(23_520_842, [4, 2], 1)
+    assert (ql.offset, ql.bits, ql.per_word) == (3, 3, 10)
+    assert (ml.bits, ml.per_word) == (1, 32)
+    ql3, _ = codec.ms_layouts(1000, [2, 4, 6], 1)
+    assert ql3.offset == 4  # |q| <= s0 + 1 with >= 3 levels
+    ql8, ml8 = codec.ms_layouts(1000, [2, 4], 8)
+    assert ml8.bits == 4 and ql8.bits == 6
+
+
+def test_errors_are_reported_not_raised():
+    from gcodec import _lib, codec
+
+    with pytest.raises(_lib.GCodecError) as e:
+        codec.qsgd_layout(10, 0, 1)
+    assert e.value.code == _lib.GC_EINVAL and "bits" in str(e.value)
+    with pytest.raises(_lib.GCodecError):
+        codec.lane_layout(10, 1 << 31, 4)
+
+
+def test_device_calls_refuse_cpu_tensors():
+    torch = pytest.importorskip("torch")
+    from gcodec import _lib, codec
+
+    with pytest.raises(_lib.GCodecError) as e:
+        codec.absmax(torch.zeros(10))
+    assert "no CPU fallback" in str(e.value)
+
+
+def test_greedy4_host_matches_reference_vectors():
+    torch = pytest.importorskip("torch")
+    from gcodec.packing import bitpacking
+
+    p = os.path.join(ROOT, "tests", "golden", "packers.npz")
+    if not os.path.exists(p):
+        pytest.skip("no packer fixtures")
+    z = np.load(p, allow_pickle=False)
+    for nm in sorted({k.split("/")[1] for k in z.files if k.startswith("g4/")}):
+        src = torch.from_numpy(z[f"g4/{nm}/src"])
+        packed = bitpacking.packing(src)
+        assert np.array_equal(packed.numpy(), z[f"g4/{nm}/packed"]), nm
+        assert np.array_equal(bitpacking.unpacking(packed).numpy(), z[f"g4/{nm}/unpacked"]), nm
+
+
+def test_greedy4_rejects_out_of_domain():
+    torch = pytest.importorskip("torch")
+    from gcodec import _lib
+    from gcodec.packing import bitpacking
+
+    for bad in ([0, 256], [3, -1]):
+        with pytest.raises(_lib.GCodecError) as e:
+            bitpacking.packing(torch.tensor(bad, dtype=torch.int32))
+        assert e.value.code == _lib.GC_ERANGE
+
+
+def test_bytepack_host_matches_reference_vectors():
+    torch = pytest.importorskip("torch")
+    from gcodec.packing import bytepacking
+
+    p = os.path.join(ROOT, "tests", "golden", "packers.npz")
+    if not os.path.exists(p):
+        pytest.skip("no packer fixtures")
+    z = np.load(p, allow_pickle=False)
+    for nm in sorted({k.split("/")[1] for k in z.files if k.startswith("bp/")}):
+        src = torch.from_numpy(z[f"bp/{nm}/src"])
+        packed = bytepacking.packing(src)
+        assert np.array_equal(packed.numpy(), z[f"bp/{nm}/packed"])
+        assert np.array_equal(bytepacking.unpacking(packed).numpy(), z[f"bp/{nm}/unpacked"])
+
+
+def test_reference_extension_oracle_agrees_with_host_packers():
+    """oracle/_ref (the reference's own C++ built from its sources) vs ours on fresh inputs."""
+    torch = pytest.importorskip("torch")
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import build_ref
+
+    if not build_ref.available():
+        pytest.skip("oracle/_ref not built")
+    from gcodec.packing import bitpacking, bytepacking
+
+    ref_bit, ref_byte = build_ref.load()
+    rng = np.random.default_rng(11)
+    for _ in range(20):
+        n = int(rng.integers(1, 400))
+        hi = int(rng.choice([4, 16, 128, 256]))
+        src = torch.from_numpy(rng.integers(0, hi, n).astype(np.int32))
+        assert torch.equal(bitpacking.packing(src), ref_bit.packing(src))
+        b = torch.from_numpy(rng.integers(-500, 500, n).astype(np.int32))
+        assert torch.equal(bytepacking.packing(b), ref_byte.packing(b))

@@ -1,0 +1,323 @@
+"""HIP kernels (through the C ABI) vs the CPU oracle and the reference's
+golden vectors.  Integers and packed words: bit-exact.  Floats: bit-exact
+(the kernels use the reference's operation order; the north-star tolerance
+is 1 ULP, the tests demand 0)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # collected on CPU, skipped there
+    pytest.skip("no GPU", allow_module_level=True)
+
+import gcodec  # noqa: E402
+from gcodec import codec  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def gz(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+def u32(t):
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+def bits_eq(a, b):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+SIZES = [1, 3, 4, 5, 63, 64, 65, 127, 1000, 4099, 65536 + 3, 1_000_003]
+
+
+# --------------------------------------------------------------------------- absmax
+@pytest.mark.parametrize("n", SIZES + [10_000_019])
+def test_absmax(n):
+    x = O.gen_input(n, seed=n, kind=1)
+    assert codec.absmax(dev(x)).item() == float(O.absmax(x))
+
+
+def test_absmax_unaligned_gather_nan():
+    x = O.gen_input(100_001, seed=3)
+    xd = dev(x)
+    assert codec.absmax(xd[1:]).item() == float(O.absmax(x[1:]))  # scalar path
+    idx = np.random.default_rng(0).choice(x.size, 997, replace=False).astype(np.int64)
+    assert codec.absmax(xd, idx=dev(idx)).item() == float(O.absmax(x[idx]))
+    x2 = x.copy()
+    x2[5000] = np.nan
+    assert np.isnan(codec.absmax(dev(x2)).item())
+    assert codec.absmax(dev(np.zeros(10, np.float32))).item() == 0.0
+
+
+# --------------------------------------------------------------------------- QSGD packed, Philox
+@pytest.mark.parametrize("bits", [2, 4, 8])
+@pytest.mark.parametrize("world", [1, 2, 8])
+@pytest.mark.parametrize("n", [1, 5, 64, 65, 4099, 1_000_003])
+def test_encode_decode_philox_vs_oracle(bits, world, n):
+    x = O.gen_input(n, seed=7 * n + bits, kind=n % 2)
+    norm = O.absmax(x)
+    seed, off = 1234 + bits, 77 * n
+    r = gcodec.rng.Reservation(gcodec._lib.GC_RNG_PHILOX, seed, off, None, n, 1)
+    words = codec.qsgd_encode(dev(x), float(norm), bits, r, world)
+    ref = O.qsgd_encode(x, norm, bits, world, O.philox_rng(seed, off))
+    assert bits_eq(u32(words), ref)
+    alpha = np.float32(1.0 / world)
+    dec = codec.qsgd_decode(words, n, float(norm), bits, world, float(alpha))
+    assert bits_eq(u32(dec), O.qsgd_decode(ref, n, norm, bits, world, alpha).view(np.uint32))
+
+
+def test_encode_unaligned_and_gather():
+    n, bits = 50_001, 4
+    x = O.gen_input(n + 1, seed=9)
+    xd = dev(x)
+    norm = O.absmax(x[1:])
+    r = gcodec.rng.Reservation(0, 5, 0, None, n, 1)
+    words = codec.qsgd_encode(xd[1:], float(norm), bits, r, 1)  # misaligned x -> scalar path
+    assert bits_eq(u32(words), O.qsgd_encode(x[1:], norm, bits, 1, O.philox_rng(5, 0)))
+    idx = np.random.default_rng(1).permutation(n + 1)[:10_000].astype(np.int64)
+    normk = O.absmax(x[idx])
+    rk = gcodec.rng.Reservation(0, 5, 3, None, idx.size, 1)
+    wk = codec.qsgd_encode(xd, float(normk), bits, rk, 2, idx=dev(idx))
+    refk = O.qsgd_encode(x[idx], normk, bits, 2, O.philox_rng(5, 3))
+    assert bits_eq(u32(wk), refk)
+    out = torch.zeros(n + 1, dtype=torch.float32, device=DEV)
+    codec.qsgd_decode(wk, idx.size, float(normk), bits, 2, 1.0, idx=dev(idx), out=out)
+    exp = np.zeros(n + 1, np.float32)
+    exp[idx] = O.qsgd_decode(refk, idx.size, normk, bits, 2, 1.0)
+    assert bits_eq(u32(out), exp.view(np.uint32))
+
+
+def test_zero_bucket_gives_zero():
+    n, bits = 1000, 4
+    x = np.zeros(n, np.float32)
+    r = gcodec.rng.Reservation(0, 1, 0, None, n, 1)
+    words = codec.qsgd_encode(dev(x), 0.0, bits, r, 1)
+    dec = codec.qsgd_decode(words, n, 0.0, bits, 1)
+    assert bits_eq(u32(words), O.qsgd_encode(x, np.float32(0), bits, 1, O.philox_rng(1, 0)))
+    assert torch.all(dec == 0)
+
+
+# --------------------------------------------------------------------------- torch-mode = reference
+@pytest.mark.parametrize("case", ["b2", "b4", "b8", "n1", "n3", "n65", "n1000"])
+def test_facade_compress_matches_reference(case):
+    z = gz("qsgd.npz")
+    x, norm, q, dec, bits = (z[f"{case}/{k}"] for k in ("x", "norm", "q", "dec", "bits"))
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(int(z[f"{case}/seed"]))
+        c = gcodec.QSGDMaxNormCompressor(DEV, int(bits))
+        qg = c.compress(torch.tensor(norm, device=DEV), dev(x))
+        assert qg.dtype == torch.from_numpy(q).dtype
+        assert bits_eq(qg.cpu().numpy(), q)
+        dg = c.decompress(torch.tensor(norm, device=DEV), qg)
+        assert bits_eq(u32(dg), dec.view(np.uint32))
+        # the packed stream in torch mode is the reference's q, lane-packed
+        torch.manual_seed(int(z[f"{case}/seed"]))
+        words = c.encode(torch.tensor(norm, device=DEV), dev(x))
+        s = (1 << int(bits)) - 1
+        w, L, M = O.lane_layout(x.size, 2 * s, 1)
+        assert bits_eq(u32(words), O.lane_pack(q.astype(np.int32), s, w, L, M))
+    finally:
+        gcodec.set_rng_mode("philox")
+
+
+def test_torch_generator_state_advances_like_reference():
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(5)
+        x = dev(O.gen_input(3001, seed=1))
+        gcodec.QSGDMaxNormCompressor(DEV, 4).compress(codec.absmax(x), x)
+        after = torch.rand(5)
+        torch.manual_seed(5)
+        torch.bernoulli(torch.full((3001,), 0.5))
+        assert torch.equal(after, torch.rand(5))
+    finally:
+        gcodec.set_rng_mode("philox")
+
+
+def test_mt19937_kernel_matches_oracle():
+    st = codec.mt19937_seed_state(42)
+    sd = torch.from_numpy(st.view(np.int32)).to(DEV)
+    a = codec.mt19937_generate(sd, 1000)
+    b = codec.mt19937_generate(sd, 123_457)
+    mt = O.MT19937(42)
+    assert bits_eq(u32(a), mt.draws(1000))
+    assert bits_eq(u32(b), mt.draws(123_457))
+
+
+@pytest.mark.parametrize("name", ["qsgd_b4_1e6_k0", "qsgd_b8_1e6_k1"])
+def test_large_digest_torch_mode(name):
+    import hashlib
+
+    meta = json.load(open(os.path.join(GOLD, "golden.json")))["digests"][name]
+    x = O.gen_input(meta["n"], seed=42, kind=meta["kind"])
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(42)
+        xd = dev(x)
+        norm = codec.absmax(xd)
+        c = gcodec.QSGDMaxNormCompressor(DEV, meta["bits"])
+        q = c.compress(norm, xd)
+        assert hashlib.sha256(q.cpu().numpy().tobytes()).hexdigest() == meta["q"]
+        d = c.decompress(norm, q)
+        assert hashlib.sha256(d.cpu().numpy().tobytes()).hexdigest() == meta["dec"]
+    finally:
+        gcodec.set_rng_mode("philox")
+
+
+# --------------------------------------------------------------------------- two-/multi-scale
+@pytest.mark.parametrize("lohi", [(2, 4), (4, 8), (2, 6), (6, 10)])
+def test_two_scale_facade_matches_reference(lohi):
+    lo, hi = lohi
+    z = gz("multiscale.npz")
+    c = f"ts{lo}_{hi}"
+    x, norm = z[f"{c}/x"], z[f"{c}/norm"]
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(int(z[f"{c}/seed"]))
+        comp = gcodec.QSGDMaxNormTwoScaleCompressor(DEV, lo, hi)
+        nt = torch.tensor(norm, device=DEV)
+        q_lo = comp.compress_lower(nt, dev(x))
+        q_hi, h = comp.compress_higher(nt, dev(x))
+        assert bits_eq(q_lo.cpu().numpy(), z[f"{c}/q_lo"])
+        assert bits_eq(q_hi.cpu().numpy(), z[f"{c}/q_hi"])
+        assert bits_eq(h.cpu().numpy(), z[f"{c}/h"])
+        q = h * q_hi + (1 - h) * q_lo
+        assert bits_eq(q.cpu().numpy(), z[f"{c}/q"])
+        d = comp.decompress(nt, q, h)
+        assert bits_eq(u32(d), z[f"{c}/dec"].view(np.uint32))
+    finally:
+        gcodec.set_rng_mode("philox")
+
+
+@pytest.mark.parametrize("levels", [(2, 4), (4, 8), (2, 4, 6), (3, 5, 7, 9), (6, 10)])
+def test_multi_scale_facade_matches_reference(levels):
+    z = gz("multiscale.npz")
+    c = "ms" + "_".join(map(str, levels))
+    x, norm = z[f"{c}/x"], z[f"{c}/norm"]
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(int(z[f"{c}/seed"]))
+        comp = gcodec.QSGDMaxNormMultiScaleCompressor(DEV, list(levels))
+        nt = torch.tensor(norm, device=DEV)
+        mask = comp.compress_mask(nt, dev(x))
+        assert bits_eq(mask.cpu().numpy(), z[f"{c}/mask"])
+        q = comp.compress(mask)
+        assert bits_eq(q.cpu().numpy(), z[f"{c}/q"])
+        d = comp.decompress(nt, q, mask)
+        assert bits_eq(u32(d), z[f"{c}/dec"].view(np.uint32))
+    finally:
+        gcodec.set_rng_mode("philox")
+
+
+@pytest.mark.parametrize("levels", [(2, 4), (4, 8), (2, 4, 6), (3, 5, 7, 9)])
+@pytest.mark.parametrize("world", [1, 3, 8])
+@pytest.mark.parametrize("n", [5, 4099, 300_001])
+def test_ms_packed_vs_oracle(levels, world, n):
+    """mask thermometer lanes + select + decode, Philox, vs the oracle."""
+    x = O.gen_input(n, seed=n + world, kind=1)
+    norm = O.absmax(x)
+    L = len(levels)
+    r = gcodec.rng.Reservation(0, 99, 11, None, n, L)
+    xd = dev(x)
+    mw = codec.ms_mask_encode(xd, float(norm), levels, r, world)
+    m_ref = O.ms_mask(x, norm, levels, O.philox_rng(99, 11))
+    # W identical ranks: the summed thermometer lanes decode to the same mask
+    mw_sum = (mw.to(torch.int64) * world).to(torch.int32)
+    got_mask = codec.ms_mask_unpack(mw_sum, n, levels, world)
+    assert bits_eq(got_mask.cpu().numpy().astype(np.uint8), m_ref)
+    words = codec.ms_select_encode(xd, float(norm), levels, r, mw_sum, world)
+    q_ref = O.ms_select(x, norm, levels, O.philox_rng(99, 11), m_ref)
+    ql, _ = codec.ms_layouts(n, levels, world)
+    assert bits_eq(u32(words), O.lane_pack(q_ref, ql.offset, ql.bits, ql.per_word, ql.plane_words))
+    wsum = (words.to(torch.int64) * world).to(torch.int32)
+    for order in (0, 1):
+        d = codec.ms_decode(wsum, mw_sum, n, float(norm), levels, world, order, 1.0)
+        ref = O.ms_dequantize(q_ref * world, norm, levels, m_ref, order)
+        assert bits_eq(u32(d), ref.view(np.uint32))
+
+
+# --------------------------------------------------------------------------- GRandK
+@pytest.mark.parametrize("case", ["n20011_k1000", "n5000_k5000", "n3001_k1000"])
+def test_grandk_torch_mode_matches_reference(case):
+    z = gz("randk.npz")
+    buf, idx, norm, q = (z[f"{case}/{k}"] for k in ("buf", "idx", "norm", "q"))
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(int(z[f"{case}/seed"]))
+        perm = torch.randperm(buf.size)  # consumes n-1 draws, like the reducer
+        assert np.array_equal(list(perm.split(int(z[f"{case}/K"])))[-1].numpy(), idx)
+        bd = dev(buf)
+        nk = codec.absmax(bd, idx=dev(idx))
+        assert nk.item() == float(norm)
+        c = gcodec.GlobalRandKMaxNormCompressor(DEV, int(z[f"{case}/bits"]))
+        qk = c.compress(nk, bd[dev(idx)])
+        assert bits_eq(qk.cpu().numpy(), q)
+    finally:
+        gcodec.set_rng_mode("philox")
+
+
+# --------------------------------------------------------------------------- packers
+def test_lane_pack_unpack_kernels():
+    rng = np.random.default_rng(3)
+    for world in (1, 2, 8):
+        n, s = 70_001, 15
+        q = rng.integers(-s, s + 1, n).astype(np.int32)
+        ln = codec.qsgd_layout(n, 4, world)
+        for dt in (torch.int8, torch.int32):
+            words = codec.lane_pack(dev(q).to(dt), ln)
+            assert bits_eq(u32(words), O.lane_pack(q, s, ln.bits, ln.per_word, ln.plane_words))
+        back = codec.lane_unpack((words.to(torch.int64) * world).to(torch.int32), ln)
+        assert np.array_equal(back.cpu().numpy(), q * world)
+
+
+def test_bytepack_kernels_match_reference_vectors():
+    p = os.path.join(GOLD, "packers.npz")
+    if not os.path.exists(p):
+        pytest.skip("no packer fixtures")
+    z = gz("packers.npz")
+    for nm in sorted({k.split("/")[1] for k in z.files if k.startswith("bp/")}):
+        src = z[f"bp/{nm}/src"]
+        w = codec.bytepack8(dev(src))
+        assert bits_eq(w.cpu().numpy(), z[f"bp/{nm}/packed"])
+        assert bits_eq(codec.byteunpack8(w).cpu().numpy(), z[f"bp/{nm}/unpacked"])
+
+
+# --------------------------------------------------------------------------- full-size properties
+def test_full_size_properties_100m():
+    """BASELINE config 2 size: no oracle run at 1e8; size-independent checks —
+    |decode - x| <= norm/s, lanes within range, unbiasedness, determinism."""
+    n, bits = 100_000_000, 4
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(n, device=DEV, generator=g).mul_(0.01)
+    norm = codec.absmax(x)
+    assert norm.item() == x.abs().max().item()
+    r = gcodec.rng.Reservation(0, 42, 0, None, n, 1)
+    w1 = codec.qsgd_encode(x, norm, bits, r, 1)
+    w2 = codec.qsgd_encode(x, norm, bits, r, 1)
+    assert torch.equal(w1, w2)  # launch-invariant counter RNG
+    d = codec.qsgd_decode(w1, n, norm, bits, 1)
+    step = norm.item() / 15
+    err = (d - x).abs().max().item()
+    assert err <= step * (1 + 1e-6)
+    bias = (d - x).double().mean().item()
+    assert abs(bias) < 5 * step / np.sqrt(n)
+    lanes = codec.lane_unpack(w1, codec.qsgd_layout(n, bits, 1))
+    assert lanes.min().item() >= -15 and lanes.max().item() <= 15
+    # chunk of the full bucket against the oracle (same counters)
+    k0 = 64 * 1000
+    xs = x[:k0].cpu().numpy()
+    q_ref = O.qsgd_quantize(xs, np.float32(norm.item()), bits, O.philox_rng(42, 0))
+    assert np.array_equal(lanes[:k0].cpu().numpy(), q_ref)
