@@ -115,7 +115,7 @@ int gc_lane_layout(uint64_t n, uint64_t range, uint32_t world, uint32_t offset, 
         ++w;
     uint32_t L = 32u / w;
     uint64_t m = (n + L - 1) / L;
-    m = (m + 63) & ~(uint64_t)63;
+    m = (m + 3) & ~(uint64_t)3;
     out->n = n;
     out->plane_words = m;
     out->bits = w;

@@ -92,8 +92,9 @@ __device__ __forceinline__ float pickf(const float4 &v, int j)
 // One element of the stochastic quantizer (compressors.py:299-316):
 //   l = RN(RN(|x| / norm) * s); fl = trunc(l); p = l - fl (exact, in [0,1));
 //   xi = fl + (u < p), u = (r & 0xFFFFFF) * 2^-24; q = sign(x) * xi.
-// Returns xi (>= 0) and the sign separately; NaN/inf quotient -> 0
-// (the reference raises there; documented divergence).
+// Returns xi (>= 0) and the sign separately.  A NaN quotient (0/0 for a
+// zero bucket, NaN inputs) gives 0 where the reference raises (documented
+// divergence); l is clamped to 2^30 (no-op when |x| <= norm).
 // ---------------------------------------------------------------------------
 struct QElem {
     int32_t xi;
@@ -104,7 +105,7 @@ __device__ __forceinline__ QElem q_elem(float x, float norm, float s, uint32_t r
 {
     const float a = fabsf(x);
     const float ql = a / norm;  // IEEE division, as torch's div
-    const bool ok = ql <= 3.0e38f;
+    const bool ok = ql == ql;
     const float l = fminf(ql * s, 1073741824.0f);
     const int32_t fl = (int32_t)l;
     const float p = l - (float)fl;

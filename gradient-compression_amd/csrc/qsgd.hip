@@ -14,6 +14,7 @@
 // The element group i0..i0+3 of each float4 is also one Philox block.
 #include "gc_device.h"
 #include "gc_host.h"
+#include "qsgd_encode.h"
 
 namespace gc {
 
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(kBlock) void k_absmax(const float *__restrict__ x, 
 }
 
 // ---------------------------------------------------------------------------
-// encode: lane(k) of word j = clamp(q(x[kM + j]), -qmax, qmax) + qmax
+// encode: see qsgd_encode.h (lane(k) of word j = qmax + q(x[kM + j]))
 // ---------------------------------------------------------------------------
 template <int MODE>
 __device__ __forceinline__ float4 load4(const float *__restrict__ x, const int64_t *__restrict__ idx, uint64_t i0,
@@ -77,42 +78,6 @@ __device__ __forceinline__ float4 load4(const float *__restrict__ x, const int64
     v.z = i0 + 2 < n ? (MODE == 2 ? x[idx[i0 + 2]] : x[i0 + 2]) : 0.0f;
     v.w = i0 + 3 < n ? (MODE == 2 ? x[idx[i0 + 3]] : x[i0 + 3]) : 0.0f;
     return v;
-}
-
-__device__ __forceinline__ uint32_t lane_of(float x, float norm, float s, uint32_t r, int32_t qmax, bool valid)
-{
-    int32_t q = q_signed(x, norm, s, r);
-    q = min(max(q, -qmax), qmax);
-    return valid ? (uint32_t)(q + qmax) : 0u;
-}
-
-template <int L, int KIND, int MODE>
-__global__ __launch_bounds__(kBlock) void k_qsgd_encode(const float *__restrict__ x, const int64_t *__restrict__ idx,
-                                                        uint64_t n, const float *__restrict__ normp, float s,
-                                                        int32_t qmax, uint32_t w, uint64_t M, RngArgs rng,
-                                                        uint32_t *__restrict__ words)
-{
-    const float norm = *normp;
-    const uint64_t quads = M >> 2;
-    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
-        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
-        // fully unrolled for L <= 16: the compiler hoists the L independent
-        // float4 loads ahead of the arithmetic (L x 16 B in flight per lane)
-#pragma unroll
-        for (int k = 0; k < L; ++k) {
-            const uint64_t i0 = (uint64_t)k * M + 4 * t;
-            if (i0 < n) {
-                const float4 xv = load4<MODE>(x, idx, i0, n);
-                const uint4 r = draws4<KIND>(rng, 0, i0);
-                const uint32_t sh = (uint32_t)k * w;
-                acc.x |= lane_of(xv.x, norm, s, r.x, qmax, true) << sh;
-                acc.y |= lane_of(xv.y, norm, s, r.y, qmax, i0 + 1 < n) << sh;
-                acc.z |= lane_of(xv.z, norm, s, r.z, qmax, i0 + 2 < n) << sh;
-                acc.w |= lane_of(xv.w, norm, s, r.w, qmax, i0 + 3 < n) << sh;
-            }
-        }
-        *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -285,7 +250,7 @@ static void launch_encode(const float *x, const int64_t *idx, uint64_t n, const 
                           const gc_lanes *ln, RngArgs ra, uint32_t *words, hipStream_t st)
 {
     const uint64_t quads = ln->plane_words >> 2;
-    hipLaunchKernelGGL((k_qsgd_encode<L, KIND, MODE>), dim3(grid_for(quads)), dim3(kBlock), 0, st, x, idx, n, norm,
+    hipLaunchKernelGGL((k_qsgd_encode<L, KIND, MODE, 0>), dim3(grid_for(quads)), dim3(kBlock), 0, st, x, idx, n, norm,
                        s, qmax, ln->bits, ln->plane_words, ra, words);
 }
 

@@ -1,0 +1,191 @@
+// qsgd_encode.h — the fused QSGD-MaxNorm encode kernel (quantize + stochastic
+// round + carry-free planar pack), compressors.py:299-316.
+//
+// Shared by qsgd.hip (the product instantiation, ABL = 0) and
+// tools/encode_lab.hip (ablation variants for measurement only).
+//
+// Per element, the reference's arithmetic in its own order:
+//   ql = RN(|x| / norm)        IEEE division (see div_norm below)
+//   l  = RN(ql * s)            then min(l, s) (lane safety; no-op in contract)
+//   fl = trunc(l), p = l - fl  (v_cvt_i32_f32, v_fract_f32: exact for l >= 0)
+//   xi = fl + [ (r & 0xFFFFFF) * 2^-24 < p ]
+//   lane = qmax + sign(x) * xi
+// A NaN quotient gives xi = 0 (the oracle's q = 0); over-range values saturate.
+#pragma once
+
+#include "gc_device.h"
+
+namespace gc {
+
+enum : int {
+    ENC_ABL_NORNG = 1,  // measurement only: draws = element index (no Philox)
+    ENC_ABL_NODIV = 2,  // measurement only: ql = |x| * (1/norm) (not exact)
+};
+
+// Division by the bucket-constant norm.  hipcc lowers a / b (IEEE, denormals
+// on) to: D = div_scale(b), N = div_scale(a), r = rcp(D), r += r*(1 - D*r),
+// q = N*r, q += r*(N - D*q), q = div_fmas(r*(N - D*q) + q), div_fixup.  With
+// b normal, 1/b normal and a >= 2^-100 (or a == 0) div_scale is the identity
+// and div_fmas a plain fma, so hoisting the reciprocal out of the loop gives
+// bit-identical quotients for 1 mul + 4 fma.  Anything else takes the
+// compiler's full division.
+struct DivNorm {
+    float norm;
+    float r;
+    uint32_t thr_bits;  // |x| bit patterns in (0, thr) take the full division
+    bool fast;          // uniform: norm in [2^-100, 2^100]
+};
+
+__device__ __forceinline__ DivNorm make_div(float norm)
+{
+    DivNorm d;
+    d.norm = norm;
+    d.fast = norm >= 0x1p-100f && norm <= 0x1p100f;
+    float r = __builtin_amdgcn_rcpf(norm);
+    const float e = fmaf(-norm, r, 1.0f);
+    d.r = fmaf(e, r, r);
+    d.thr_bits = __float_as_uint(0x1p-100f);
+    return d;
+}
+
+__device__ __forceinline__ float div_fast(float a, const DivNorm &d)
+{
+    float q = a * d.r;
+    float e = fmaf(-d.norm, q, a);
+    q = fmaf(e, d.r, q);
+    e = fmaf(-d.norm, q, a);
+    return fmaf(e, d.r, q);
+}
+
+// lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
+// input) gives xi = 0 (fmaxf(NaN, 0) = 0); an infinite one saturates at s.
+__device__ __forceinline__ uint32_t enc_lane(float x, float ql, float s, int32_t qmax, uint32_t r)
+{
+    const float l = fminf(fmaxf(ql * s, 0.0f), s);
+    const int32_t fl = (int32_t)l;
+    const float p = __builtin_amdgcn_fractf(l);
+    const float u = (float)(r & 0xFFFFFFu) * 0x1p-24f;
+    const int32_t xi = fl + (u < p ? 1 : 0);
+    const int32_t m = (__float_as_int(x) >> 30) | 1;  // -1 if the sign bit is set, else +1
+    return (uint32_t)(m * xi + qmax);
+}
+
+template <int ABL>
+__device__ __forceinline__ float4 quot4(const float4 &v, const DivNorm &d)
+{
+    float4 q;
+    if constexpr ((ABL & ENC_ABL_NODIV) != 0) {
+        q.x = fabsf(v.x) * d.r;
+        q.y = fabsf(v.y) * d.r;
+        q.z = fabsf(v.z) * d.r;
+        q.w = fabsf(v.w) * d.r;
+    } else {
+        const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z), aw = fabsf(v.w);
+        q.x = div_fast(ax, d);
+        q.y = div_fast(ay, d);
+        q.z = div_fast(az, d);
+        q.w = div_fast(aw, d);
+        // 0 < |x| < 2^-100: the full division (rare; one branch per float4)
+        const uint32_t t1 = d.thr_bits - 1u;
+        const int slow = (int)(__float_as_uint(ax) - 1u < t1) | (int)(__float_as_uint(ay) - 1u < t1) |
+                         (int)(__float_as_uint(az) - 1u < t1) | (int)(__float_as_uint(aw) - 1u < t1);
+        if (__builtin_expect(slow, 0)) {
+            q.x = ax / d.norm;
+            q.y = ay / d.norm;
+            q.z = az / d.norm;
+            q.w = aw / d.norm;
+        }
+    }
+    return q;
+}
+
+template <int KIND, int ABL>
+__device__ __forceinline__ uint4 draws4_abl(const RngArgs &rng, uint32_t level, uint64_t i0)
+{
+    if constexpr ((ABL & ENC_ABL_NORNG) != 0) {
+        const uint32_t b = (uint32_t)i0 * 2654435761u;
+        return make_uint4(b, b + 1u, b + 2u, b + 3u);
+    } else {
+        return draws4<KIND>(rng, level, i0);
+    }
+}
+
+// Full tiles: every one of the L planes of words 4t..4t+3 is in range, so
+// no per-element bounds, 32-bit element indices, L float4 loads in flight.
+// Tail quads, gathers, unaligned x and the non-fast-division case go through
+// the generic body.
+template <int L, int KIND, int MODE, int ABL>
+__global__ __launch_bounds__(kBlock) void k_qsgd_encode(const float *__restrict__ x, const int64_t *__restrict__ idx,
+                                                        uint64_t n, const float *__restrict__ normp, float s,
+                                                        int32_t qmax, uint32_t w, uint64_t M, RngArgs rng,
+                                                        uint32_t *__restrict__ words)
+{
+    const float norm = *normp;
+    const DivNorm dv = make_div(norm);
+    const bool fast = dv.fast || (ABL & ENC_ABL_NODIV) != 0;
+    const uint64_t quads = M >> 2;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+
+    // quads whose last plane is full: (L-1)*M + 4t + 3 < n
+    const uint64_t last = (uint64_t)(L - 1) * M;
+    const uint64_t full = (MODE == 0 && fast && n >= last + 4 && n < (1ull << 32)) ? (n - last) >> 2 : 0;
+    const uint32_t M32 = (uint32_t)M;
+    for (; t < full; t += stride) {
+        const uint32_t t4 = (uint32_t)t * 4u;
+        float4 xv[L];
+#pragma unroll
+        for (int k = 0; k < L; ++k)
+            xv[k] = *reinterpret_cast<const float4 *>(x + (k * M32 + t4));
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            const uint32_t i0 = k * M32 + t4;
+            const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
+            const float4 q = quot4<ABL>(xv[k], dv);
+            const uint32_t sh = (uint32_t)k * w;
+            acc.x |= enc_lane(xv[k].x, q.x, s, qmax, r.x) << sh;
+            acc.y |= enc_lane(xv[k].y, q.y, s, qmax, r.y) << sh;
+            acc.z |= enc_lane(xv[k].z, q.z, s, qmax, r.z) << sh;
+            acc.w |= enc_lane(xv[k].w, q.w, s, qmax, r.w) << sh;
+        }
+        *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
+    }
+    // generic body: tail quads (partial planes), gathers, unaligned x, odd norms
+    for (; t < quads; t += stride) {
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            const uint64_t i0 = (uint64_t)k * M + 4 * t;
+            if (i0 < n) {
+                float4 v;
+                if (MODE == 0 && i0 + 4 <= n) {
+                    v = *reinterpret_cast<const float4 *>(x + i0);
+                } else {
+                    v.x = MODE == 2 ? x[idx[i0]] : x[i0];
+                    v.y = i0 + 1 < n ? (MODE == 2 ? x[idx[i0 + 1]] : x[i0 + 1]) : 0.0f;
+                    v.z = i0 + 2 < n ? (MODE == 2 ? x[idx[i0 + 2]] : x[i0 + 2]) : 0.0f;
+                    v.w = i0 + 3 < n ? (MODE == 2 ? x[idx[i0 + 3]] : x[i0 + 3]) : 0.0f;
+                }
+                const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
+                float4 q;
+                if (fast) {
+                    q = quot4<ABL>(v, dv);
+                } else {
+                    q.x = fabsf(v.x) / norm;
+                    q.y = fabsf(v.y) / norm;
+                    q.z = fabsf(v.z) / norm;
+                    q.w = fabsf(v.w) / norm;
+                }
+                const uint32_t sh = (uint32_t)k * w;
+                acc.x |= enc_lane(v.x, q.x, s, qmax, r.x) << sh;
+                acc.y |= (i0 + 1 < n ? enc_lane(v.y, q.y, s, qmax, r.y) : 0u) << sh;
+                acc.z |= (i0 + 2 < n ? enc_lane(v.z, q.z, s, qmax, r.z) : 0u) << sh;
+                acc.w |= (i0 + 3 < n ? enc_lane(v.w, q.w, s, qmax, r.w) : 0u) << sh;
+            }
+        }
+        *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
+    }
+}
+
+}  // namespace gc

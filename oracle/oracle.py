@@ -34,7 +34,11 @@ class _MT(C.Structure):
 
 
 def build() -> str:
-    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    import fcntl
+
+    with open(os.path.join(HERE, ".build.lock"), "w") as lk:  # concurrent test workers
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
 

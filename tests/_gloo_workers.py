@@ -1,0 +1,64 @@
+"""Worker bodies for the multi-process (gloo, CPU) reducer tests."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "gradient-compression_amd"), HERE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+SEED = 42
+REDUCERS = ["qsgd", "ts", "ms", "ms3", "randk", "randk_ts"]
+
+
+def make_reducer(name, **kw):
+    from gcodec import reducer as R
+
+    dev = torch.device("cpu")
+    if name == "qsgd":
+        return R.QSGDMaxNormReducer(dev, None, quantization_level=4, **kw)
+    if name == "ts":
+        return R.QSGDMaxNormTwoScaleReducer(dev, None, 2, 4, **kw)
+    if name == "ms":
+        return R.QSGDMaxNormMultiScaleReducer(dev, None, [2, 4], **kw)
+    if name == "ms3":
+        return R.QSGDMaxNormMultiScaleReducer(dev, None, [2, 4, 6], **kw)
+    if name == "randk":
+        return R.GlobalRandKMaxNormReducer(dev, None, SEED, K=100, quantization_level=4, **kw)
+    if name == "randk_ts":
+        return R.GlobalRandKMaxNormTwoScaleReducer(dev, None, SEED, K=100, lower_quantization_level=2,
+                                                   higher_quantization_level=4, **kw)
+    raise KeyError(name)
+
+
+def reducer_vs_reference(rank, world, init_file, fixture, out_dir):
+    """Run our reducers (oracle codec, torch-mode RNG) on the golden grads."""
+    import gcodec
+    import oracle_codec
+
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    z = np.load(fixture, allow_pickle=False)
+    gen = gcodec.Generator(0, "torch")
+    res = {}
+    for name in REDUCERS:
+        red = make_reducer(name, codec=oracle_codec, generator=gen)
+        torch.manual_seed(SEED + rank)
+        for step in range(2):
+            gin = []
+            i = 0
+            while f"r{rank}/{name}/s{step}/in{i}" in z.files:
+                gin.append(torch.from_numpy(z[f"r{rank}/{name}/s{step}/in{i}"].copy()))
+                i += 1
+            gout = [torch.empty_like(g) for g in gin]
+            bits = red.reduce(gin, gout)
+            for i, g in enumerate(gout):
+                res[f"{name}/s{step}/out{i}"] = g.numpy()
+            res[f"{name}/s{step}/bits"] = np.int64(bits)
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -1,0 +1,174 @@
+// encode_lab.hip — measurement harness for the QSGD encode path (not product
+// code).  Times, with HIP events, on a 100M-fp32 bucket:
+//   * memory rooflines with the encode's exact access pattern (read-only,
+//     read L planes + write packed words),
+//   * the product entry points through the C ABI (gc_absmax_f32,
+//     gc_qsgd_encode, gc_qsgd_decode),
+//   * ablations of the encode kernel (no Philox / no exact division) and
+//     grid sizes, to locate the bound.
+// Build: make -C tools encode_lab ; run: tools/encode_lab [n]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "gcodec.h"
+#include "qsgd_encode.h"
+
+using namespace gc;
+
+#define CK(x)                                                                               \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) {                                                             \
+            fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            exit(2);                                                                        \
+        }                                                                                   \
+    } while (0)
+
+__global__ void k_fill(float *x, uint64_t n, uint32_t seed)
+{
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+        h ^= h >> 15;
+        h *= 2246822519u;
+        h ^= h >> 13;
+        float u = (float)(int32_t)h * 0x1p-31f;
+        x[i] = u * u * u * 0.05f;
+    }
+}
+
+// read-only stream (absmax-like roofline)
+__global__ __launch_bounds__(256) void k_read(const float4 *x, uint64_t n4, uint32_t *out)
+{
+    uint32_t m = 0;
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < n4; t += gridDim.x * 256ull) {
+        float4 v = x[t];
+        m = max(m, max(max(__float_as_uint(v.x), __float_as_uint(v.y)), max(__float_as_uint(v.z), __float_as_uint(v.w))));
+    }
+    if (m == 0x7fffffffu)
+        out[0] = m;
+}
+
+// the encode's exact memory pattern with no arithmetic: L float4 planes -> uint4
+template <int L>
+__global__ __launch_bounds__(256) void k_copy_planar(const float *x, uint32_t M, uint32_t *words)
+{
+    const uint32_t quads = M >> 2;
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < quads; t += gridDim.x * 256u) {
+        uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            float4 v = *reinterpret_cast<const float4 *>(x + k * M + 4 * t);
+            acc.x ^= __float_as_uint(v.x);
+            acc.y ^= __float_as_uint(v.y);
+            acc.z ^= __float_as_uint(v.z);
+            acc.w ^= __float_as_uint(v.w);
+        }
+        *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
+    }
+}
+
+struct Timer {
+    hipEvent_t a, b;
+    Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
+    template <class F>
+    float run(F f, int reps = 20)
+    {
+        f();
+        f();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a, 0));
+        for (int i = 0; i < reps; ++i)
+            f();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        return ms / reps;
+    }
+};
+
+static void row(const char *name, float ms, double bytes)
+{
+    double gbs = bytes / (ms * 1e-3) / 1e9;
+    printf("%-44s %9.1f us  %8.1f GB/s  %5.1f%% of 8 TB/s\n", name, ms * 1e3, gbs, 100.0 * gbs / 8000.0);
+}
+
+int main(int argc, char **argv)
+{
+    uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 100000000ull;
+    const uint32_t bits = 4;
+    gc_lanes ln;
+    if (gc_qsgd_layout(n, bits, 1, &ln) != GC_OK) {
+        fprintf(stderr, "layout: %s\n", gc_last_error());
+        return 1;
+    }
+    const uint32_t M = (uint32_t)ln.plane_words;
+    float *x, *norm, *dec;
+    uint32_t *words, *words2, *scratch;
+    CK(hipMalloc(&x, n * 4 + 64));
+    CK(hipMalloc(&dec, n * 4 + 64));
+    CK(hipMalloc(&norm, 64));
+    CK(hipMalloc(&words, (size_t)M * 4 + 64));
+    CK(hipMalloc(&words2, (size_t)M * 4 + 64));
+    CK(hipMalloc(&scratch, 64));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, x, n, 7u);
+    CK(hipDeviceSynchronize());
+    printf("n=%llu  M=%u words  lanes w=%u L=%u\n", (unsigned long long)n, M, ln.bits, ln.per_word);
+    const double enc_bytes = 4.0 * n + 4.0 * M, rd_bytes = 4.0 * n;
+    Timer T;
+
+    row("roofline: read-only stream (n fp32)", T.run([&] {
+            hipLaunchKernelGGL(k_read, dim3(2048), dim3(256), 0, 0, (const float4 *)x, n / 4, scratch);
+        }), rd_bytes);
+    for (unsigned g : {1024u, 2048u, 4096u, 8192u}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "roofline: planar read + packed write g=%u", g);
+        row(nm, T.run([&] { hipLaunchKernelGGL(k_copy_planar<6>, dim3(g), dim3(256), 0, 0, x, M, words2); }),
+            enc_bytes);
+    }
+    row("product gc_absmax_f32 (memset + kernel)", T.run([&] { gc_absmax_f32(x, nullptr, n, norm, nullptr); }),
+        rd_bytes);
+    gc_rng rng = {GC_RNG_PHILOX, 0, 42, 0, nullptr};
+    row("product gc_qsgd_encode", T.run([&] { gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr); }),
+        enc_bytes);
+    row("product absmax + encode (one step)", T.run([&] {
+            gc_absmax_f32(x, nullptr, n, norm, nullptr);
+            gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr);
+        }), 8.0 * n + 4.0 * M);
+    row("product gc_qsgd_decode", T.run([&] { gc_qsgd_decode(words, nullptr, n, norm, bits, &ln, 1.0f, dec, nullptr); }),
+        4.0 * n + 4.0 * M);
+
+    RngArgs ra{42, 0, nullptr, n};
+    const float s = 15.0f;
+    const int32_t qmax = 15;
+    auto enc = [&](auto kern, unsigned g) {
+        return [=] {
+            hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, 0, x, (const int64_t *)nullptr, n, norm, s, qmax, ln.bits,
+                               (uint64_t)M, ra, words2);
+        };
+    };
+    for (unsigned g : {1024u, 2048u, 4096u, 8192u, 16384u}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "encode ABL=0 (exact) g=%u", g);
+        row(nm, T.run(enc(k_qsgd_encode<6, 0, 0, 0>, g)), enc_bytes);
+    }
+    row("encode ABL=NORNG g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG>, 2048)), enc_bytes);
+    row("encode ABL=NODIV g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NODIV>, 2048)), enc_bytes);
+    row("encode ABL=NORNG|NODIV g=2048",
+        T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 2048)), enc_bytes);
+
+    // the lab's ABL=0 instantiation must equal the product's words
+    hipLaunchKernelGGL((k_qsgd_encode<6, 0, 0, 0>), dim3(2048), dim3(256), 0, 0, x, (const int64_t *)nullptr, n, norm,
+                       s, qmax, ln.bits, (uint64_t)M, ra, words2);
+    gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr);
+    CK(hipDeviceSynchronize());
+    std::vector<uint32_t> a(M), b(M);
+    CK(hipMemcpy(a.data(), words, (size_t)M * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), words2, (size_t)M * 4, hipMemcpyDeviceToHost));
+    printf("lab ABL=0 == product: %s\n", memcmp(a.data(), b.data(), (size_t)M * 4) == 0 ? "yes" : "NO");
+    return 0;
+}
