@@ -24,17 +24,48 @@ struct RngArgs {
     uint64_t n;  // elements per level in the stream
 };
 
+// Philox4x32-10 round function; IMPL selects the instruction mix only (the
+// outputs are identical): 0 = 64-bit products + 2-input XORs, 1 = 64-bit
+// products (v_mad_u64_u32) + 3-input XOR (v_bitop3_b32 0x96), 2 = 32-bit
+// mul_hi / mul_lo + v_bitop3_b32.
+#ifndef GC_PHILOX_IMPL
+#define GC_PHILOX_IMPL 1
+#endif
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+template <int IMPL = GC_PHILOX_IMPL>
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1)
 {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
-        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        uint32_t hi0, lo0, hi1, lo1;
+        if constexpr (IMPL == 2) {
+            hi0 = __umulhi(0xD2511F53u, c.x);
+            lo0 = 0xD2511F53u * c.x;
+            hi1 = __umulhi(0xCD9E8D57u, c.z);
+            lo1 = 0xCD9E8D57u * c.z;
+        } else {
+            const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+            const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+            hi0 = (uint32_t)(p0 >> 32);
+            lo0 = (uint32_t)p0;
+            hi1 = (uint32_t)(p1 >> 32);
+            lo1 = (uint32_t)p1;
+        }
         uint4 o;
-        o.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
-        o.y = (uint32_t)p1;
-        o.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
-        o.w = (uint32_t)p0;
+        if constexpr (IMPL == 0) {
+            o.x = hi1 ^ c.y ^ k0;
+            o.z = hi0 ^ c.w ^ k1;
+        } else {
+            o.x = xor3(hi1, c.y, k0);
+            o.z = xor3(hi0, c.w, k1);
+        }
+        o.y = lo1;
+        o.w = lo0;
         c = o;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -43,7 +74,7 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
 }
 
 // Four draws for elements i0..i0+3 (i0 % 4 == 0) at scale `level`.
-template <int KIND>
+template <int KIND, int IMPL = GC_PHILOX_IMPL>
 __device__ __forceinline__ uint4 draws4(const RngArgs &r, uint32_t level, uint64_t i0)
 {
     if constexpr (KIND == 0) {
@@ -53,7 +84,7 @@ __device__ __forceinline__ uint4 draws4(const RngArgs &r, uint32_t level, uint64
         c.y = ((uint32_t)(g >> 32) & 0xffffu) | (level << 16);
         c.z = (uint32_t)r.offset;
         c.w = (uint32_t)(r.offset >> 32);
-        return philox4x32_10(c, (uint32_t)r.seed, (uint32_t)(r.seed >> 32));
+        return philox4x32_10<IMPL>(c, (uint32_t)r.seed, (uint32_t)(r.seed >> 32));
     } else {
         const uint32_t *p = r.stream + (uint64_t)level * r.n + i0;
         const uint64_t left = i0 < r.n ? r.n - i0 : 0;

@@ -20,6 +20,9 @@ namespace gc {
 enum : int {
     ENC_ABL_NORNG = 1,  // measurement only: draws = element index (no Philox)
     ENC_ABL_NODIV = 2,  // measurement only: ql = |x| * (1/norm) (not exact)
+    ENC_PHX0 = 4,       // Philox instruction mix 0 (same outputs)
+    ENC_PHX2 = 8,       // Philox instruction mix 2 (same outputs)
+    ENC_MED3 = 16,      // clamp with v_med3_f32
 };
 
 // Division by the bucket-constant norm.  hipcc lowers a / b (IEEE, denormals
@@ -59,9 +62,10 @@ __device__ __forceinline__ float div_fast(float a, const DivNorm &d)
 
 // lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
 // input) gives xi = 0 (fmaxf(NaN, 0) = 0); an infinite one saturates at s.
+template <int ABL = 0>
 __device__ __forceinline__ uint32_t enc_lane(float x, float ql, float s, int32_t qmax, uint32_t r)
 {
-    const float l = fminf(fmaxf(ql * s, 0.0f), s);
+    const float l = (ABL & ENC_MED3) ? __builtin_amdgcn_fmed3f(ql * s, 0.0f, s) : fminf(fmaxf(ql * s, 0.0f), s);
     const int32_t fl = (int32_t)l;
     const float p = __builtin_amdgcn_fractf(l);
     const float u = (float)(r & 0xFFFFFFu) * 0x1p-24f;
@@ -105,6 +109,10 @@ __device__ __forceinline__ uint4 draws4_abl(const RngArgs &rng, uint32_t level, 
     if constexpr ((ABL & ENC_ABL_NORNG) != 0) {
         const uint32_t b = (uint32_t)i0 * 2654435761u;
         return make_uint4(b, b + 1u, b + 2u, b + 3u);
+    } else if constexpr ((ABL & ENC_PHX0) != 0) {
+        return draws4<KIND, 0>(rng, level, i0);
+    } else if constexpr ((ABL & ENC_PHX2) != 0) {
+        return draws4<KIND, 2>(rng, level, i0);
     } else {
         return draws4<KIND>(rng, level, i0);
     }
@@ -144,10 +152,10 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_encode(const float *__restrict_
             const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
             const float4 q = quot4<ABL>(xv[k], dv);
             const uint32_t sh = (uint32_t)k * w;
-            acc.x |= enc_lane(xv[k].x, q.x, s, qmax, r.x) << sh;
-            acc.y |= enc_lane(xv[k].y, q.y, s, qmax, r.y) << sh;
-            acc.z |= enc_lane(xv[k].z, q.z, s, qmax, r.z) << sh;
-            acc.w |= enc_lane(xv[k].w, q.w, s, qmax, r.w) << sh;
+            acc.x |= enc_lane<ABL>(xv[k].x, q.x, s, qmax, r.x) << sh;
+            acc.y |= enc_lane<ABL>(xv[k].y, q.y, s, qmax, r.y) << sh;
+            acc.z |= enc_lane<ABL>(xv[k].z, q.z, s, qmax, r.z) << sh;
+            acc.w |= enc_lane<ABL>(xv[k].w, q.w, s, qmax, r.w) << sh;
         }
         *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
     }
@@ -178,10 +186,10 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_encode(const float *__restrict_
                     q.w = fabsf(v.w) / norm;
                 }
                 const uint32_t sh = (uint32_t)k * w;
-                acc.x |= enc_lane(v.x, q.x, s, qmax, r.x) << sh;
-                acc.y |= (i0 + 1 < n ? enc_lane(v.y, q.y, s, qmax, r.y) : 0u) << sh;
-                acc.z |= (i0 + 2 < n ? enc_lane(v.z, q.z, s, qmax, r.z) : 0u) << sh;
-                acc.w |= (i0 + 3 < n ? enc_lane(v.w, q.w, s, qmax, r.w) : 0u) << sh;
+                acc.x |= enc_lane<ABL>(v.x, q.x, s, qmax, r.x) << sh;
+                acc.y |= (i0 + 1 < n ? enc_lane<ABL>(v.y, q.y, s, qmax, r.y) : 0u) << sh;
+                acc.z |= (i0 + 2 < n ? enc_lane<ABL>(v.z, q.z, s, qmax, r.z) : 0u) << sh;
+                acc.w |= (i0 + 3 < n ? enc_lane<ABL>(v.w, q.w, s, qmax, r.w) : 0u) << sh;
             }
         }
         *reinterpret_cast<uint4 *>(words + 4 * t) = acc;

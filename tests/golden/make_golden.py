@@ -211,9 +211,8 @@ def reducer_fixtures(world: int):
 
 
 def packer_fixtures():
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
-        import build_ref
+        from oracle import build_ref
 
         bitpacking, bytepacking = build_ref.load()
     except Exception as e:  # unbuildable here -> skip, recorded in digests.json

@@ -130,10 +130,7 @@ def test_bytepack_host_matches_reference_vectors():
 def test_reference_extension_oracle_agrees_with_host_packers():
     """oracle/_ref (the reference's own C++ built from its sources) vs ours on fresh inputs."""
     torch = pytest.importorskip("torch")
-    import sys
-
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import build_ref
+    from oracle import build_ref
 
     if not build_ref.available():
         pytest.skip("oracle/_ref not built")

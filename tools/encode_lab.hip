@@ -156,6 +156,10 @@ int main(int argc, char **argv)
         snprintf(nm, sizeof nm, "encode ABL=0 (exact) g=%u", g);
         row(nm, T.run(enc(k_qsgd_encode<6, 0, 0, 0>, g)), enc_bytes);
     }
+    row("encode philox impl 0 (64b mad, xor2)", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PHX0>, 2048)), enc_bytes);
+    row("encode philox impl 2 (mul_hi/lo, xor3)", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PHX2>, 2048)), enc_bytes);
+    row("encode med3 clamp", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 2048)), enc_bytes);
+    row("encode med3 clamp + impl 2", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3 | ENC_PHX2>, 2048)), enc_bytes);
     row("encode ABL=NORNG g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG>, 2048)), enc_bytes);
     row("encode ABL=NODIV g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NODIV>, 2048)), enc_bytes);
     row("encode ABL=NORNG|NODIV g=2048",
@@ -170,5 +174,16 @@ int main(int argc, char **argv)
     CK(hipMemcpy(a.data(), words, (size_t)M * 4, hipMemcpyDeviceToHost));
     CK(hipMemcpy(b.data(), words2, (size_t)M * 4, hipMemcpyDeviceToHost));
     printf("lab ABL=0 == product: %s\n", memcmp(a.data(), b.data(), (size_t)M * 4) == 0 ? "yes" : "NO");
+    // exact variants (same outputs by construction) must agree bit for bit
+    auto same = [&](const char *nm, auto kern) {
+        CK(hipMemset(words2, 0, (size_t)M * 4));
+        enc(kern, 2048)();
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(b.data(), words2, (size_t)M * 4, hipMemcpyDeviceToHost));
+        printf("%-28s == product: %s\n", nm, memcmp(a.data(), b.data(), (size_t)M * 4) == 0 ? "yes" : "NO");
+    };
+    same("philox impl 0", k_qsgd_encode<6, 0, 0, ENC_PHX0>);
+    same("philox impl 2", k_qsgd_encode<6, 0, 0, ENC_PHX2>);
+    same("med3 clamp", k_qsgd_encode<6, 0, 0, ENC_MED3>);
     return 0;
 }
