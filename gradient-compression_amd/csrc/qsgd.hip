@@ -24,9 +24,17 @@ __device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v)
 // max-norm: uint max over |x| bit patterns (exact, order-free, NaN wins like
 // torch.max), wave64 shuffle tree, 4 wave partials in LDS, one atomic/block.
 // ---------------------------------------------------------------------------
-template <int MODE>  // 0: float4 dense, 1: scalar dense, 2: gather
+// Without a workspace: one atomicMax per block into *norm (zeroed by a
+// preceding hipMemsetAsync).  With a workspace: no memset launch — every block
+// stores its partial, releases it (agent scope) and takes a ticket; the block
+// that draws the last ticket acquires, reduces the partials, writes *norm and
+// re-arms the ticket for the next call (MI355X_MICROARCH.md, inter-workgroup
+// visibility; cdna_hip_programming.md Guideline 16).
+constexpr unsigned kAbsmaxMaxBlocks = 2048;
+
+template <int MODE, bool WS>  // MODE 0: float4 dense, 1: scalar dense, 2: gather
 __global__ __launch_bounds__(kBlock) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
-                                                   uint64_t n, uint32_t *__restrict__ out)
+                                                   uint64_t n, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)
 {
     uint32_t m = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
@@ -53,13 +61,45 @@ __global__ __launch_bounds__(kBlock) void k_absmax(const float *__restrict__ x, 
     }
     m = wave_max_u32(m);
     __shared__ uint32_t part[kBlock / 64];
+    __shared__ int last;
     if ((threadIdx.x & 63) == 0)
         part[threadIdx.x >> 6] = m;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        m = max(max(part[0], part[1]), max(part[2], part[3]));
-        if (m)
-            atomicMax(out, m);
+    if constexpr (!WS) {
+        if (threadIdx.x == 0) {
+            m = max(max(part[0], part[1]), max(part[2], part[3]));
+            if (m)
+                atomicMax(out, m);
+        }
+        return;
+    } else {
+        uint32_t *ticket = ws;
+        uint32_t *partials = ws + 16;  // own cache line
+        if (threadIdx.x == 0) {
+            m = max(max(part[0], part[1]), max(part[2], part[3]));
+            __hip_atomic_store(&partials[blockIdx.x], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t tk = atomicAdd(ticket, 1u);
+            last = tk == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (!last)
+            return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        uint32_t v = 0;
+        for (uint32_t i = threadIdx.x; i < gridDim.x; i += kBlock)
+            v = max(v, __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        v = wave_max_u32(v);
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0)
+            part[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            *out = max(max(part[0], part[1]), max(part[2], part[3]));
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -260,22 +300,31 @@ using namespace gc;
 
 extern "C" {
 
-int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, gc_stream_t stream)
+size_t gc_absmax_workspace_size(void) { return 64 + 4 * kAbsmaxMaxBlocks; }
+
+int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, void *workspace, gc_stream_t stream)
 {
     GC_REQUIRE(norm, "gc_absmax_f32: null norm");
     GC_REQUIRE(n == 0 || x, "gc_absmax_f32: null x");
     hipStream_t st = as_stream(stream);
-    if (hipMemsetAsync(norm, 0, sizeof(float), st) != hipSuccess)
-        return launch_status("gc_absmax_f32 memset");
-    if (n == 0)
-        return GC_OK;
     uint32_t *o = reinterpret_cast<uint32_t *>(norm);
-    if (idx)
-        hipLaunchKernelGGL((k_absmax<2>), dim3(grid_for(n)), dim3(kBlock), 0, st, x, idx, n, o);
-    else if (aligned16(x))
-        hipLaunchKernelGGL((k_absmax<0>), dim3(grid_for(n >> 2)), dim3(kBlock), 0, st, x, idx, n, o);
-    else
-        hipLaunchKernelGGL((k_absmax<1>), dim3(grid_for(n)), dim3(kBlock), 0, st, x, idx, n, o);
+    uint32_t *ws = reinterpret_cast<uint32_t *>(workspace);
+    if (n == 0 || !ws) {
+        if (hipMemsetAsync(norm, 0, sizeof(float), st) != hipSuccess)
+            return launch_status("gc_absmax_f32 memset");
+        if (n == 0)
+            return GC_OK;
+    }
+    const int mode = idx ? 2 : (aligned16(x) ? 0 : 1);
+    const unsigned grid = grid_for(mode == 0 ? (n >> 2) : n, kAbsmaxMaxBlocks);
+#define GC_AM(MODE_, WS_) \
+    hipLaunchKernelGGL((k_absmax<MODE_, WS_>), dim3(grid), dim3(kBlock), 0, st, x, idx, n, o, ws)
+    if (ws) {
+        if (mode == 0) GC_AM(0, true); else if (mode == 1) GC_AM(1, true); else GC_AM(2, true);
+    } else {
+        if (mode == 0) GC_AM(0, false); else if (mode == 1) GC_AM(1, false); else GC_AM(2, false);
+    }
+#undef GC_AM
     return launch_status("gc_absmax_f32");
 }
 

@@ -22,7 +22,7 @@ enum : int {
     ENC_ABL_NODIV = 2,  // measurement only: ql = |x| * (1/norm) (not exact)
     ENC_PHX0 = 4,       // Philox instruction mix 0 (same outputs)
     ENC_PHX2 = 8,       // Philox instruction mix 2 (same outputs)
-    ENC_MED3 = 16,      // clamp with v_med3_f32
+    ENC_MED3 = 16,      // clamp with v_max + v_min instead of v_med3_f32
 };
 
 // Division by the bucket-constant norm.  hipcc lowers a / b (IEEE, denormals
@@ -35,8 +35,9 @@ enum : int {
 struct DivNorm {
     float norm;
     float r;
-    uint32_t thr_bits;  // |x| bit patterns in (0, thr) take the full division
-    bool fast;          // uniform: norm in [2^-100, 2^100]
+    uint32_t lo1;  // bits(thr_lo) - 1: |x| in (0, thr_lo) takes the full division
+    uint32_t hi;   // bits(thr_hi): |x| above (and inf / NaN) takes the full division
+    bool fast;     // uniform: norm in [2^-100, 2^100]
 };
 
 __device__ __forceinline__ DivNorm make_div(float norm)
@@ -47,7 +48,10 @@ __device__ __forceinline__ DivNorm make_div(float norm)
     float r = __builtin_amdgcn_rcpf(norm);
     const float e = fmaf(-norm, r, 1.0f);
     d.r = fmaf(e, r, r);
-    d.thr_bits = __float_as_uint(0x1p-100f);
+    // thr_lo keeps |x| >= 2^-100 (no numerator scaling) and |x|/norm >= 2^-120
+    // (normal quotient); thr_hi keeps |x|/norm <= 2^64 (no overflow scaling)
+    d.lo1 = __float_as_uint(fmaxf(0x1p-100f, norm * 0x1p-120f)) - 1u;
+    d.hi = __float_as_uint(fminf(norm * 0x1p64f, 3.4028234e38f));
     return d;
 }
 
@@ -60,12 +64,28 @@ __device__ __forceinline__ float div_fast(float a, const DivNorm &d)
     return fmaf(e, d.r, q);
 }
 
+// running range of |x| bit patterns for the fast-division check:
+// mn = min(bits - 1) (zero wraps to 0xFFFFFFFF and never triggers), mx = max(bits)
+struct Range {
+    uint32_t mn = 0xffffffffu, mx = 0u;
+    __device__ __forceinline__ void add4(const float4 &v)
+    {
+        const uint32_t a = __float_as_uint(v.x) & 0x7fffffffu, b = __float_as_uint(v.y) & 0x7fffffffu;
+        const uint32_t c = __float_as_uint(v.z) & 0x7fffffffu, e = __float_as_uint(v.w) & 0x7fffffffu;
+        mn = min(min(mn, a - 1u), min(min(b - 1u, c - 1u), e - 1u));
+        mx = max(max(mx, a), max(max(b, c), e));
+    }
+    __device__ __forceinline__ bool slow(const DivNorm &d) const { return (mn < d.lo1) | (mx > d.hi); }
+};
+
 // lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
 // input) gives xi = 0 (fmaxf(NaN, 0) = 0); an infinite one saturates at s.
 template <int ABL = 0>
 __device__ __forceinline__ uint32_t enc_lane(float x, float ql, float s, int32_t qmax, uint32_t r)
 {
-    const float l = (ABL & ENC_MED3) ? __builtin_amdgcn_fmed3f(ql * s, 0.0f, s) : fminf(fmaxf(ql * s, 0.0f), s);
+    // v_med3_f32(l, 0, s): clamps to [0, s]; a NaN l yields 0 (checked against
+    // the oracle by tests/test_gpu_parity.py::test_encode_non_finite_and_tiny_inputs)
+    const float l = (ABL & ENC_MED3) ? fminf(fmaxf(ql * s, 0.0f), s) : __builtin_amdgcn_fmed3f(ql * s, 0.0f, s);
     const int32_t fl = (int32_t)l;
     const float p = __builtin_amdgcn_fractf(l);
     const float u = (float)(r & 0xFFFFFFu) * 0x1p-24f;
@@ -75,7 +95,7 @@ __device__ __forceinline__ uint32_t enc_lane(float x, float ql, float s, int32_t
 }
 
 template <int ABL>
-__device__ __forceinline__ float4 quot4(const float4 &v, const DivNorm &d)
+__device__ __forceinline__ float4 quot4_fast(const float4 &v, const DivNorm &d)
 {
     float4 q;
     if constexpr ((ABL & ENC_ABL_NODIV) != 0) {
@@ -84,22 +104,21 @@ __device__ __forceinline__ float4 quot4(const float4 &v, const DivNorm &d)
         q.z = fabsf(v.z) * d.r;
         q.w = fabsf(v.w) * d.r;
     } else {
-        const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z), aw = fabsf(v.w);
-        q.x = div_fast(ax, d);
-        q.y = div_fast(ay, d);
-        q.z = div_fast(az, d);
-        q.w = div_fast(aw, d);
-        // 0 < |x| < 2^-100: the full division (rare; one branch per float4)
-        const uint32_t t1 = d.thr_bits - 1u;
-        const int slow = (int)(__float_as_uint(ax) - 1u < t1) | (int)(__float_as_uint(ay) - 1u < t1) |
-                         (int)(__float_as_uint(az) - 1u < t1) | (int)(__float_as_uint(aw) - 1u < t1);
-        if (__builtin_expect(slow, 0)) {
-            q.x = ax / d.norm;
-            q.y = ay / d.norm;
-            q.z = az / d.norm;
-            q.w = aw / d.norm;
-        }
+        q.x = div_fast(fabsf(v.x), d);
+        q.y = div_fast(fabsf(v.y), d);
+        q.z = div_fast(fabsf(v.z), d);
+        q.w = div_fast(fabsf(v.w), d);
     }
+    return q;
+}
+
+__device__ __forceinline__ float4 quot4_ieee(const float4 &v, float norm)
+{
+    float4 q;
+    q.x = fabsf(v.x) / norm;
+    q.y = fabsf(v.y) / norm;
+    q.z = fabsf(v.z) / norm;
+    q.w = fabsf(v.w) / norm;
     return q;
 }
 
@@ -145,17 +164,28 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_encode(const float *__restrict_
 #pragma unroll
         for (int k = 0; k < L; ++k)
             xv[k] = *reinterpret_cast<const float4 *>(x + (k * M32 + t4));
+        float4 q[L];
+        Range rg;
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            q[k] = quot4_fast<ABL>(xv[k], dv);
+            rg.add4(xv[k]);
+        }
+        if ((ABL & ENC_ABL_NODIV) == 0 && __builtin_expect(rg.slow(dv), 0)) {
+#pragma unroll
+            for (int k = 0; k < L; ++k)
+                q[k] = quot4_ieee(xv[k], norm);
+        }
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (int k = 0; k < L; ++k) {
             const uint32_t i0 = k * M32 + t4;
             const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
-            const float4 q = quot4<ABL>(xv[k], dv);
             const uint32_t sh = (uint32_t)k * w;
-            acc.x |= enc_lane<ABL>(xv[k].x, q.x, s, qmax, r.x) << sh;
-            acc.y |= enc_lane<ABL>(xv[k].y, q.y, s, qmax, r.y) << sh;
-            acc.z |= enc_lane<ABL>(xv[k].z, q.z, s, qmax, r.z) << sh;
-            acc.w |= enc_lane<ABL>(xv[k].w, q.w, s, qmax, r.w) << sh;
+            acc.x |= enc_lane<ABL>(xv[k].x, q[k].x, s, qmax, r.x) << sh;
+            acc.y |= enc_lane<ABL>(xv[k].y, q[k].y, s, qmax, r.y) << sh;
+            acc.z |= enc_lane<ABL>(xv[k].z, q[k].z, s, qmax, r.z) << sh;
+            acc.w |= enc_lane<ABL>(xv[k].w, q[k].w, s, qmax, r.w) << sh;
         }
         *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
     }
@@ -177,14 +207,12 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_encode(const float *__restrict_
                 }
                 const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
                 float4 q;
-                if (fast) {
-                    q = quot4<ABL>(v, dv);
-                } else {
-                    q.x = fabsf(v.x) / norm;
-                    q.y = fabsf(v.y) / norm;
-                    q.z = fabsf(v.z) / norm;
-                    q.w = fabsf(v.w) / norm;
-                }
+                Range rg;
+                rg.add4(v);
+                if (fast && ((ABL & ENC_ABL_NODIV) != 0 || !rg.slow(dv)))
+                    q = quot4_fast<ABL>(v, dv);
+                else
+                    q = quot4_ieee(v, norm);
                 const uint32_t sh = (uint32_t)k * w;
                 acc.x |= enc_lane<ABL>(v.x, q.x, s, qmax, r.x) << sh;
                 acc.y |= (i0 + 1 < n ? enc_lane<ABL>(v.y, q.y, s, qmax, r.y) : 0u) << sh;

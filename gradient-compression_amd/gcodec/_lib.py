@@ -75,7 +75,8 @@ SIGNATURES = {
     "gc_qsgd_layout": (C.c_int, [u64, u32, u32, LANESP]),
     "gc_ms_layout": (C.c_int, [u64, LEVP, u32, LANESP]),
     "gc_ms_mask_layout": (C.c_int, [u64, LEVP, u32, LANESP]),
-    "gc_absmax_f32": (C.c_int, [P, P, u64, P, P]),
+    "gc_absmax_workspace_size": (C.c_size_t, []),
+    "gc_absmax_f32": (C.c_int, [P, P, u64, P, P, P]),
     "gc_qsgd_encode": (C.c_int, [P, P, u64, P, u32, LANESP, RNGP, P, P]),
     "gc_qsgd_decode": (C.c_int, [P, P, u64, P, u32, LANESP, f32, P, P]),
     "gc_qsgd_quantize": (C.c_int, [P, u64, P, u32, RNGP, u32, P, u32, P]),

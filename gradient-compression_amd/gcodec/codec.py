@@ -107,6 +107,19 @@ def mask_words_total(ml: _lib.gc_lanes, levels) -> int:
 # ---------------------------------------------------------------------------
 # max-norm
 # ---------------------------------------------------------------------------
+_WS = {}
+
+
+def _absmax_ws(dev, stream) -> torch.Tensor:
+    """Self-resetting last-block workspace, one per (device, stream)."""
+    key = (dev.index, stream.value)
+    ws = _WS.get(key)
+    if ws is None:
+        ws = torch.zeros(int(_lib.load().gc_absmax_workspace_size()), dtype=torch.uint8, device=dev)
+        _WS[key] = ws
+    return ws
+
+
 def absmax(x: torch.Tensor, idx=None, out: torch.Tensor | None = None) -> torch.Tensor:
     dev = _dev(x)
     x = _f32(x, "absmax")
@@ -114,7 +127,8 @@ def absmax(x: torch.Tensor, idx=None, out: torch.Tensor | None = None) -> torch.
     n = idx.numel() if idx is not None else x.numel()
     if out is None:
         out = torch.empty(1, dtype=torch.float32, device=dev)
-    check(_lib.load().gc_absmax_f32(_p(x), _p(idx), n, _p(out), _stream(dev)), "gc_absmax_f32")
+    st = _stream(dev)
+    check(_lib.load().gc_absmax_f32(_p(x), _p(idx), n, _p(out), _p(_absmax_ws(dev, st)), st), "gc_absmax_f32")
     return out
 
 

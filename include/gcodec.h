@@ -112,8 +112,12 @@ int gc_ms_mask_layout(uint64_t n, const gc_levels *levels, uint32_t world, gc_la
 
 /* ---- max-norm ----------------------------------------------------------- */
 /* *norm = max_i |x[idx ? idx[i] : i]| over i < n (NaN-propagating); norm is a
- * device float overwritten by the call. */
-int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, gc_stream_t stream);
+ * device float overwritten by the call.  workspace: NULL (a memset of *norm
+ * is enqueued first) or gc_absmax_workspace_size() device bytes, zeroed ONCE
+ * by the caller and then reused (self-resetting; one workspace per stream). */
+size_t gc_absmax_workspace_size(void);
+int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, void *workspace,
+                  gc_stream_t stream);
 
 /* ---- QSGD-MaxNorm ------------------------------------------------------- */
 /* words[lanes->plane_words] = pack(q + s), q = stochastic_round(x[idx?idx[i]:i], *norm, bits) */

@@ -99,6 +99,30 @@ def test_encode_unaligned_and_gather():
     assert bits_eq(u32(out), exp.view(np.uint32))
 
 
+@pytest.mark.parametrize("world", [1, 4])
+def test_encode_non_finite_and_tiny_inputs(world):
+    """NaN -> 0, +/-inf and |x| > norm saturate at +/-s, subnormal and
+    below-2^-100 magnitudes take the exact-division branch — all vs the oracle."""
+    n, bits = 4 * 6 * 997, 4
+    x = O.gen_input(n, seed=5)
+    x[::97] = np.nan
+    x[5::101] = np.inf
+    x[7::103] = -np.inf
+    x[11::89] = np.float32(3e-41)      # subnormal
+    x[13::83] = np.float32(-1e-35)     # normal, below 2^-100 * norm? (norm ~1e-2)
+    x[17::79] = np.float32(7e-31)
+    x[19::73] = 0.25                   # |x| > norm
+    x[23::71] = -0.0
+    norm = np.float32(np.nanmax(np.abs(x[np.isfinite(x)])) / 8)  # finite, smaller than some |x|
+    r = gcodec.rng.Reservation(0, 77, 1, None, n, 1)
+    words = codec.qsgd_encode(dev(x), float(norm), bits, r, world)
+    assert bits_eq(u32(words), O.qsgd_encode(x, norm, bits, world, O.philox_rng(77, 1)))
+    # tiny norms take the generic exact-division path for every element
+    for tiny in (np.float32(1e-38), np.float32(2e-45), np.float32(3e33)):
+        words = codec.qsgd_encode(dev(x), float(tiny), bits, r, world)
+        assert bits_eq(u32(words), O.qsgd_encode(x, tiny, bits, world, O.philox_rng(77, 1))), tiny
+
+
 def test_zero_bucket_gives_zero():
     n, bits = 1000, 4
     x = np.zeros(n, np.float32)

@@ -71,6 +71,59 @@ __global__ __launch_bounds__(256) void k_copy_planar(const float *x, uint32_t M,
     }
 }
 
+// tiled-planar pattern: one wave owns a tile of 256 words = 6 x 256-float
+// chunks that are ADJACENT in memory (6 KB contiguous per wave)
+template <int L>
+__global__ __launch_bounds__(256) void k_copy_tiled(const float *x, uint32_t tiles, uint32_t *words)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t tile = (blockIdx.x * 256u + threadIdx.x) >> 6; tile < tiles; tile += gridDim.x * 4u) {
+        const float *base = x + (size_t)tile * (L * 256u) + 4u * lane;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            float4 v = *reinterpret_cast<const float4 *>(base + k * 256);
+            acc.x ^= __float_as_uint(v.x);
+            acc.y ^= __float_as_uint(v.y);
+            acc.z ^= __float_as_uint(v.z);
+            acc.w ^= __float_as_uint(v.w);
+        }
+        *reinterpret_cast<uint4 *>(words + (size_t)tile * 256u + 4u * lane) = acc;
+    }
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void k_read_planar(const float *x, uint32_t M, uint32_t *out)
+{
+    uint32_t m = 0;
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < (M >> 2); t += gridDim.x * 256u) {
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            float4 v = *reinterpret_cast<const float4 *>(x + k * M + 4 * t);
+            m = max(m, max(max(__float_as_uint(v.x), __float_as_uint(v.y)), max(__float_as_uint(v.z), __float_as_uint(v.w))));
+        }
+    }
+    if (m == 0x7fffffffu)
+        out[0] = m;
+}
+
+__global__ __launch_bounds__(256) void k_write(uint4 *o, uint64_t n4)
+{
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < n4; t += gridDim.x * 256ull)
+        o[t] = make_uint4((uint32_t)t, 1, 2, 3);
+}
+
+__global__ __launch_bounds__(256) void k_write_nt(uint4 *o, uint64_t n4)
+{
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < n4; t += gridDim.x * 256ull) {
+        uint4 v = make_uint4((uint32_t)t, 1, 2, 3);
+        __builtin_nontemporal_store(v.x, &o[t].x);
+        __builtin_nontemporal_store(v.y, &o[t].y);
+        __builtin_nontemporal_store(v.z, &o[t].z);
+        __builtin_nontemporal_store(v.w, &o[t].w);
+    }
+}
+
 struct Timer {
     hipEvent_t a, b;
     Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
@@ -130,13 +183,37 @@ int main(int argc, char **argv)
         row(nm, T.run([&] { hipLaunchKernelGGL(k_copy_planar<6>, dim3(g), dim3(256), 0, 0, x, M, words2); }),
             enc_bytes);
     }
-    row("product gc_absmax_f32 (memset + kernel)", T.run([&] { gc_absmax_f32(x, nullptr, n, norm, nullptr); }),
+    for (unsigned g : {2048u, 8192u, 16384u}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "roofline: TILED read + packed write g=%u", g);
+        const uint32_t tiles = (uint32_t)(n / (6 * 256));
+        row(nm, T.run([&] { hipLaunchKernelGGL(k_copy_tiled<6>, dim3(g), dim3(256), 0, 0, x, tiles, words2); }),
+            (double)tiles * 6 * 256 * 4 + (double)tiles * 256 * 4);
+    }
+    row("roofline: planar read only g=2048", T.run([&] {
+            hipLaunchKernelGGL(k_read_planar<6>, dim3(2048), dim3(256), 0, 0, x, M, scratch);
+        }), rd_bytes);
+    row("roofline: planar read only g=16384", T.run([&] {
+            hipLaunchKernelGGL(k_read_planar<6>, dim3(16384), dim3(256), 0, 0, x, M, scratch);
+        }), rd_bytes);
+    row("roofline: write-only 400 MB", T.run([&] {
+            hipLaunchKernelGGL(k_write, dim3(8192), dim3(256), 0, 0, (uint4 *)dec, n / 4);
+        }), rd_bytes);
+    row("roofline: write-only 400 MB nontemporal", T.run([&] {
+            hipLaunchKernelGGL(k_write_nt, dim3(8192), dim3(256), 0, 0, (uint4 *)dec, n / 4);
+        }), rd_bytes);
+    row("product gc_absmax_f32 (memset + kernel)", T.run([&] { gc_absmax_f32(x, nullptr, n, norm, nullptr, nullptr); }),
+        rd_bytes);
+    void *ws;
+    CK(hipMalloc(&ws, gc_absmax_workspace_size()));
+    CK(hipMemset(ws, 0, gc_absmax_workspace_size()));
+    row("product gc_absmax_f32 (workspace, 1 launch)", T.run([&] { gc_absmax_f32(x, nullptr, n, norm, ws, nullptr); }),
         rd_bytes);
     gc_rng rng = {GC_RNG_PHILOX, 0, 42, 0, nullptr};
     row("product gc_qsgd_encode", T.run([&] { gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr); }),
         enc_bytes);
     row("product absmax + encode (one step)", T.run([&] {
-            gc_absmax_f32(x, nullptr, n, norm, nullptr);
+            gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
             gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr);
         }), 8.0 * n + 4.0 * M);
     row("product gc_qsgd_decode", T.run([&] { gc_qsgd_decode(words, nullptr, n, norm, bits, &ln, 1.0f, dec, nullptr); }),
@@ -151,15 +228,16 @@ int main(int argc, char **argv)
                                (uint64_t)M, ra, words2);
         };
     };
-    for (unsigned g : {1024u, 2048u, 4096u, 8192u, 16384u}) {
+    for (unsigned g : {2048u, 8192u, 16384u, 32768u}) {
         char nm[96];
         snprintf(nm, sizeof nm, "encode ABL=0 (exact) g=%u", g);
         row(nm, T.run(enc(k_qsgd_encode<6, 0, 0, 0>, g)), enc_bytes);
     }
     row("encode philox impl 0 (64b mad, xor2)", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PHX0>, 2048)), enc_bytes);
     row("encode philox impl 2 (mul_hi/lo, xor3)", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PHX2>, 2048)), enc_bytes);
-    row("encode med3 clamp", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 2048)), enc_bytes);
-    row("encode med3 clamp + impl 2", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3 | ENC_PHX2>, 2048)), enc_bytes);
+    row("encode max+min clamp", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 2048)), enc_bytes);
+    row("encode max+min clamp g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 16384)), enc_bytes);
+    row("encode NORNG|NODIV g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 16384)), enc_bytes);
     row("encode ABL=NORNG g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG>, 2048)), enc_bytes);
     row("encode ABL=NODIV g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NODIV>, 2048)), enc_bytes);
     row("encode ABL=NORNG|NODIV g=2048",
@@ -184,6 +262,6 @@ int main(int argc, char **argv)
     };
     same("philox impl 0", k_qsgd_encode<6, 0, 0, ENC_PHX0>);
     same("philox impl 2", k_qsgd_encode<6, 0, 0, ENC_PHX2>);
-    same("med3 clamp", k_qsgd_encode<6, 0, 0, ENC_MED3>);
+    same("max+min clamp", k_qsgd_encode<6, 0, 0, ENC_MED3>);
     return 0;
 }
