@@ -153,6 +153,7 @@ static void row(const char *name, float ms, double bytes)
 int main(int argc, char **argv)
 {
     uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 100000000ull;
+    const bool quick = argc > 2;  // small-n run: rooflines + product + ablations only
     const uint32_t bits = 4;
     gc_lanes ln;
     if (gc_qsgd_layout(n, bits, 1, &ln) != GC_OK) {
