@@ -16,6 +16,8 @@
 #include "gc_host.h"
 #include "qsgd_encode.h"
 
+#include <algorithm>
+
 namespace gc {
 
 __device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
@@ -30,15 +32,19 @@ __device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v)
 // block that draws the last ticket reduces the partials (sc1 loads), writes
 // *norm and re-arms the ticket for the next call.  Fence-free: a per-block
 // release fence (buffer_wbl2) measured 2x slower than the memset it removes.
-constexpr unsigned kAbsmaxMaxBlocks = 2048;
+// One 1024-thread block per CU: 16 waves x 4 float4 loads in flight = 64 KB
+// per CU (HBM-saturating), and at most 256 same-address atomics (one word
+// takes ~88 atomics/us, MI355X_MICROARCH.md 'dequeue': 2048 blocks cost ~20 us).
+constexpr unsigned kAbsmaxThreads = 1024;
+constexpr unsigned kAbsmaxMaxBlocks = 256;
 
 template <int MODE, bool WS>  // MODE 0: float4 dense, 1: scalar dense, 2: gather
-__global__ __launch_bounds__(kBlock) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
+__global__ __launch_bounds__(kAbsmaxThreads) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
                                                    uint64_t n, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)
 {
     uint32_t m = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * kAbsmaxThreads;
+    uint64_t t = (uint64_t)blockIdx.x * kAbsmaxThreads + threadIdx.x;
     if constexpr (MODE == 0) {
         const float4 *x4 = reinterpret_cast<const float4 *>(x);
         const uint64_t n4 = n >> 2;
@@ -60,14 +66,15 @@ __global__ __launch_bounds__(kBlock) void k_absmax(const float *__restrict__ x, 
             m = max(m, absbits(MODE == 2 ? x[idx[t]] : x[t]));
     }
     m = wave_max_u32(m);
-    __shared__ uint32_t part[kBlock / 64];
+    __shared__ uint32_t part[kAbsmaxThreads / 64];
     __shared__ int last;
     if ((threadIdx.x & 63) == 0)
         part[threadIdx.x >> 6] = m;
     __syncthreads();
     if constexpr (!WS) {
         if (threadIdx.x == 0) {
-            m = max(max(part[0], part[1]), max(part[2], part[3]));
+            for (unsigned w = 1; w < kAbsmaxThreads / 64; ++w)
+                m = max(m, part[w]);
             if (m)
                 atomicMax(out, m);
         }
@@ -89,7 +96,7 @@ __global__ __launch_bounds__(kBlock) void k_absmax(const float *__restrict__ x, 
         if (!last)
             return;
         uint32_t v = 0;
-        for (uint32_t i = threadIdx.x; i < gridDim.x; i += kBlock)
+        for (uint32_t i = threadIdx.x; i < gridDim.x; i += kAbsmaxThreads)
             v = max(v, __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         v = wave_max_u32(v);
         __syncthreads();
@@ -97,7 +104,10 @@ __global__ __launch_bounds__(kBlock) void k_absmax(const float *__restrict__ x, 
             part[threadIdx.x >> 6] = v;
         __syncthreads();
         if (threadIdx.x == 0) {
-            *out = max(max(part[0], part[1]), max(part[2], part[3]));
+            uint32_t r = part[0];
+            for (unsigned w = 1; w < kAbsmaxThreads / 64; ++w)
+                r = max(r, part[w]);
+            *out = r;
             __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -316,9 +326,11 @@ int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, v
             return GC_OK;
     }
     const int mode = idx ? 2 : (aligned16(x) ? 0 : 1);
-    const unsigned grid = grid_for(mode == 0 ? (n >> 2) : n, kAbsmaxMaxBlocks);
+    const uint64_t items = mode == 0 ? (n >> 2) : n;
+    const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((items + kAbsmaxThreads - 1) / kAbsmaxThreads, 1),
+                                                       kAbsmaxMaxBlocks);
 #define GC_AM(MODE_, WS_) \
-    hipLaunchKernelGGL((k_absmax<MODE_, WS_>), dim3(grid), dim3(kBlock), 0, st, x, idx, n, o, ws)
+    hipLaunchKernelGGL((k_absmax<MODE_, WS_>), dim3(grid), dim3(kAbsmaxThreads), 0, st, x, idx, n, o, ws)
     if (ws) {
         if (mode == 0) GC_AM(0, true); else if (mode == 1) GC_AM(1, true); else GC_AM(2, true);
     } else {

@@ -23,6 +23,7 @@ enum : int {
     ENC_PHX0 = 4,       // Philox instruction mix 0 (same outputs)
     ENC_PHX2 = 8,       // Philox instruction mix 2 (same outputs)
     ENC_MED3 = 16,      // clamp with v_max + v_min instead of v_med3_f32
+    ENC_ABL_L2 = 32,    // measurement only: loads from a 16 KB window (compute floor)
 };
 
 // Division by the bucket-constant norm.  hipcc lowers a / b (IEEE, denormals
@@ -163,7 +164,8 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_encode(const float *__restrict_
         float4 xv[L];
 #pragma unroll
         for (int k = 0; k < L; ++k)
-            xv[k] = *reinterpret_cast<const float4 *>(x + (k * M32 + t4));
+            xv[k] = *reinterpret_cast<const float4 *>(x + ((ABL & ENC_ABL_L2) ? ((k * M32 + t4) & 4095u)
+                                                                                : (k * M32 + t4)));
         float4 q[L];
         Range rg;
 #pragma unroll

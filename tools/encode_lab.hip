@@ -239,6 +239,10 @@ int main(int argc, char **argv)
     row("encode max+min clamp", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 2048)), enc_bytes);
     row("encode max+min clamp g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 16384)), enc_bytes);
     row("encode NORNG|NODIV g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 16384)), enc_bytes);
+    row("encode COMPUTE ONLY (16KB window) g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 2048)), enc_bytes);
+    row("encode COMPUTE ONLY g=8192", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 8192)), enc_bytes);
+    row("encode COMPUTE ONLY, no Philox", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2 | ENC_ABL_NORNG>, 2048)), enc_bytes);
+    row("encode COMPUTE ONLY, no div", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2 | ENC_ABL_NODIV>, 2048)), enc_bytes);
     row("encode ABL=NORNG g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG>, 2048)), enc_bytes);
     row("encode ABL=NODIV g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NODIV>, 2048)), enc_bytes);
     row("encode ABL=NORNG|NODIV g=2048",
