@@ -226,6 +226,34 @@ def main():
                               "steps": "absmax, all_reduce MAX, encode, all_reduce SUM (RCCL), decode + 1/W"}
         del dec
 
+        # PCIe-inclusive: the reference's path starts and ends in host memory;
+        # pinned buffers, hipMemcpyAsync (torch non_blocking copies) on the same stream
+        xh = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        xh.copy_(x)
+        wh = torch.empty(M, dtype=torch.int32, pin_memory=True)
+        dh = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        xd = torch.empty_like(x)
+
+        def pcie_encode():
+            xd.copy_(xh, non_blocking=True)
+            codec.absmax(xd, out=norm)
+            codec.qsgd_encode(xd, norm, bits, gen.reserve(n), world, out=words, lanes=lanes)
+            wh.copy_(words, non_blocking=True)
+
+        def pcie_decode():
+            words.copy_(wh, non_blocking=True)
+            codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
+            dh.copy_(dec, non_blocking=True)
+
+        pk = max(3, K // 4)
+        ms_pe = _events(torch, pcie_encode, pk)
+        ms_pd = _events(torch, pcie_decode, pk)
+        out["pcie_inclusive"] = {
+            "encode_grad_floats_per_s": n / (ms_pe * 1e-3), "encode_ms": ms_pe,
+            "decode_grad_floats_per_s": n / (ms_pd * 1e-3), "decode_ms": ms_pd,
+            "note": "pinned host x -> H2D -> absmax+encode -> D2H packed words; and H2D words -> decode -> D2H floats"}
+        del xh, wh, dh, xd
+
         # reference-parity mode: torch CPU-generator (MT19937) stream, generated on the GPU
         n_mt = min(n, 10_000_000)
         pgen = gcodec.Generator(0, "torch")

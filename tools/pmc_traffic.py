@@ -1,0 +1,62 @@
+"""Summarise a tools/profile.sh run into profiles/:
+  profiles/<tag>_kernel_stats.csv   (rocprofv3 --stats, copied)
+  profiles/<tag>_pmc.json           (per-kernel HBM bytes per launch)
+  profiles/pmc_traffic.json         (latest, read by bench.py for roofline.traffic)
+HBM bytes per launch = 2 * FETCH_SIZE (gfx950 reports half of a wide streaming
+read, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, both in KiB from rocprofv3."""
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _rows(pattern):
+    for p in glob.glob(pattern, recursive=True):
+        with open(p) as f:
+            yield from csv.DictReader(f)
+
+
+def _short(name):
+    for k in ("k_qsgd_encode", "k_absmax", "k_qsgd_decode"):
+        if k in name:
+            return k
+    return name[:60]
+
+
+def counter(tag, which, cname):
+    vals = {}
+    for r in _rows(os.path.join(ROOT, "gpurun_out", f"prof_{tag}", which, "**", "*counter_collection.csv")):
+        if r.get("Counter_Name") != cname:
+            continue
+        vals.setdefault(_short(r.get("Kernel_Name", "")), []).append(float(r["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in vals.items()}
+
+
+def main(tag, n=100_000_000, bits=4):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+    fetch = counter(tag, "fetch", "FETCH_SIZE")
+    write = counter(tag, "write", "WRITE_SIZE")
+    out = {"tag": tag, "n": n, "bits": bits, "units": "bytes per launch",
+           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024",
+           "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(k), write.get(k)
+        out["kernels"][k] = {"fetch_size_kib_raw": f, "write_size_kib": w,
+                             "hbm_bytes_per_launch": None if f is None or w is None else (2 * f + w) * 1024}
+    for name in (f"{tag}_pmc.json", "pmc_traffic.json"):
+        with open(os.path.join(ROOT, "profiles", name), "w") as fh:
+            json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
