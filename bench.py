@@ -224,7 +224,6 @@ def main():
         out["reduce_path"] = {"grad_floats_per_s": world * n * K / pel, "ms_per_step": pel / K * 1e3,
                               "packed_bytes_per_rank": 4 * M,
                               "steps": "absmax, all_reduce MAX, encode, all_reduce SUM (RCCL), decode + 1/W"}
-        del dec
 
         # PCIe-inclusive: the reference's path starts and ends in host memory;
         # pinned buffers, hipMemcpyAsync (torch non_blocking copies) on the same stream
@@ -252,7 +251,7 @@ def main():
             "encode_grad_floats_per_s": n / (ms_pe * 1e-3), "encode_ms": ms_pe,
             "decode_grad_floats_per_s": n / (ms_pd * 1e-3), "decode_ms": ms_pd,
             "note": "pinned host x -> H2D -> absmax+encode -> D2H packed words; and H2D words -> decode -> D2H floats"}
-        del xh, wh, dh, xd
+        del xh, wh, dh, xd, dec
 
         # reference-parity mode: torch CPU-generator (MT19937) stream, generated on the GPU
         n_mt = min(n, 10_000_000)

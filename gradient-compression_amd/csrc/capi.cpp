@@ -115,7 +115,10 @@ int gc_lane_layout(uint64_t n, uint64_t range, uint32_t world, uint32_t offset, 
         ++w;
     uint32_t L = 32u / w;
     uint64_t m = (n + L - 1) / L;
-    m = (m + 3) & ~(uint64_t)3;
+    // planes start on 256-B boundaries for large streams (a wave's 1 KiB
+    // float4 access never straddles a line shared with another XCD's L2);
+    // 16 B (all the kernels need) for small ones (GRandK K ~ 1e4)
+    m = m >= 65536 ? (m + 63) & ~(uint64_t)63 : (m + 3) & ~(uint64_t)3;
     out->n = n;
     out->plane_words = m;
     out->bits = w;

@@ -45,42 +45,40 @@ __device__ __forceinline__ float4 load4m(const float *__restrict__ x, const int6
     return v;
 }
 
-// resolution level of 4 elements: last level whose |q| <= maxv (level 0 always)
+// resolution level of 4 elements: last level whose |q| <= maxv (level 0 always
+// qualifies, so its draws are not needed here; level l uses draw block l)
 template <int KIND>
-__device__ __forceinline__ uint4 ms_levels4(const float4 &v, float norm, const LevelsArg &lv, const RngArgs &rng,
-                                            uint64_t i0)
+__device__ __forceinline__ uint4 ms_levels4(const float4 &q, const LevelsArg &lv, const RngArgs &rng, uint64_t i0)
 {
     uint4 m = make_uint4(0u, 0u, 0u, 0u);
     for (uint32_t l = 1; l < lv.count; ++l) {
         const uint4 r = draws4<KIND>(rng, l, i0);
         const float s = lv.s[l];
-        if (q_elem(v.x, norm, s, r.x).xi <= lv.maxv) m.x = l;
-        if (q_elem(v.y, norm, s, r.y).xi <= lv.maxv) m.y = l;
-        if (q_elem(v.z, norm, s, r.z).xi <= lv.maxv) m.z = l;
-        if (q_elem(v.w, norm, s, r.w).xi <= lv.maxv) m.w = l;
+        if (xi_from_q(q.x, s, r.x) <= lv.maxv) m.x = l;
+        if (xi_from_q(q.y, s, r.y) <= lv.maxv) m.y = l;
+        if (xi_from_q(q.z, s, r.z) <= lv.maxv) m.z = l;
+        if (xi_from_q(q.w, s, r.w) <= lv.maxv) m.w = l;
     }
     return m;
 }
-// Level 0 needs no draw for the mask: |q_0| <= s_0 = maxv always (its draws
-// are still "consumed" by the stream layout: level l uses block l).
 
 // q of 4 elements at their own levels m (same draws as the mask pass)
 template <int KIND>
-__device__ __forceinline__ int4 ms_select4(const float4 &v, float norm, const LevelsArg &lv, const RngArgs &rng,
+__device__ __forceinline__ int4 ms_select4(const float4 &v, const float4 &q, const LevelsArg &lv, const RngArgs &rng,
                                            uint64_t i0, uint4 m)
 {
-    int4 q = make_int4(0, 0, 0, 0);
+    int4 o = make_int4(0, 0, 0, 0);
     for (uint32_t l = 0; l < lv.count; ++l) {
         if (m.x != l && m.y != l && m.z != l && m.w != l)
             continue;
         const uint4 r = draws4<KIND>(rng, l, i0);
         const float s = lv.s[l];
-        if (m.x == l) q.x = q_signed(v.x, norm, s, r.x);
-        if (m.y == l) q.y = q_signed(v.y, norm, s, r.y);
-        if (m.z == l) q.z = q_signed(v.z, norm, s, r.z);
-        if (m.w == l) q.w = q_signed(v.w, norm, s, r.w);
+        if (m.x == l) o.x = sgn_of(v.x) * xi_from_q(q.x, s, r.x);
+        if (m.y == l) o.y = sgn_of(v.y) * xi_from_q(q.y, s, r.y);
+        if (m.z == l) o.z = sgn_of(v.z) * xi_from_q(q.z, s, r.z);
+        if (m.w == l) o.w = sgn_of(v.w) * xi_from_q(q.w, s, r.w);
     }
-    return q;
+    return o;
 }
 
 struct MaskArg {
@@ -115,6 +113,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_mask_encode(const float *__restri
                                                            uint32_t *__restrict__ mask_words)
 {
     const float norm = *normp;
+    const DivNorm dv = make_div(norm);
     const uint64_t quads = M >> 2;
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
         uint4 acc[GC_MAX_LEVELS - 1];
@@ -126,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_mask_encode(const float *__restri
             const uint64_t i0 = (uint64_t)j * M + 4 * t;
             if (i0 < n) {
                 const float4 v = load4m<MODE>(x, idx, i0, n);
-                const uint4 m = ms_levels4<KIND>(v, norm, lv, rng, i0);
+                const uint4 m = ms_levels4<KIND>(quot4_exact(v, dv), lv, rng, i0);
                 const uint32_t sh = (uint32_t)j * w;
 #pragma unroll
                 for (int f = 0; f < GC_MAX_LEVELS - 1; ++f) {
@@ -154,6 +153,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_encode(const float *__rest
                                                              int32_t qmax, uint32_t *__restrict__ words)
 {
     const float norm = *normp;
+    const DivNorm dv = make_div(norm);
     const uint64_t quads = Mq >> 2;
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_encode(const float *__rest
             if (i0 < n) {
                 const float4 v = load4m<MODE>(x, idx, i0, n);
                 const uint4 m = mask_levels4(mk, i0);
-                const int4 q = ms_select4<KIND>(v, norm, lv, rng, i0, m);
+                const int4 q = ms_select4<KIND>(v, quot4_exact(v, dv), lv, rng, i0, m);
                 const uint32_t sh = (uint32_t)k * wq;
                 acc.x |= (uint32_t)(min(max(q.x, -qmax), qmax) + qmax) << sh;
                 acc.y |= (i0 + 1 < n ? (uint32_t)(min(max(q.y, -qmax), qmax) + qmax) : 0u) << sh;
@@ -225,11 +225,12 @@ __global__ __launch_bounds__(kBlock) void k_ms_quantize_mask(const float *__rest
                                                              RngArgs rng, int8_t *__restrict__ mask)
 {
     const float norm = *normp;
+    const DivNorm dv = make_div(norm);
     const uint64_t groups = (n + 3) >> 2;
     for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * kBlock) {
         const uint64_t i0 = g << 2;
         const float4 v = load4m<MODE>(x, nullptr, i0, n);
-        const uint4 m = ms_levels4<KIND>(v, norm, lv, rng, i0);
+        const uint4 m = ms_levels4<KIND>(quot4_exact(v, dv), lv, rng, i0);
         for (int e = 0; e < 4; ++e)
             if (i0 + e < n)
                 mask[i0 + e] = (int8_t)pick(m, e);
@@ -243,6 +244,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_quantize(const float *__re
                                                                QT *__restrict__ q)
 {
     const float norm = *normp;
+    const DivNorm dv = make_div(norm);
     const uint64_t groups = (n + 3) >> 2;
     for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * kBlock) {
         const uint64_t i0 = g << 2;
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_quantize(const float *__re
         m.y = i0 + 1 < n ? (uint32_t)mask[i0 + 1] : 0u;
         m.z = i0 + 2 < n ? (uint32_t)mask[i0 + 2] : 0u;
         m.w = i0 + 3 < n ? (uint32_t)mask[i0 + 3] : 0u;
-        const int4 qq = ms_select4<KIND>(v, norm, lv, rng, i0, m);
+        const int4 qq = ms_select4<KIND>(v, quot4_exact(v, dv), lv, rng, i0, m);
         if (i0 + 0 < n) q[i0 + 0] = (QT)qq.x;
         if (i0 + 1 < n) q[i0 + 1] = (QT)qq.y;
         if (i0 + 2 < n) q[i0 + 2] = (QT)qq.z;

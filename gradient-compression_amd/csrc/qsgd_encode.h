@@ -26,59 +26,6 @@ enum : int {
     ENC_ABL_L2 = 32,    // measurement only: loads from a 16 KB window (compute floor)
 };
 
-// Division by the bucket-constant norm.  hipcc lowers a / b (IEEE, denormals
-// on) to: D = div_scale(b), N = div_scale(a), r = rcp(D), r += r*(1 - D*r),
-// q = N*r, q += r*(N - D*q), q = div_fmas(r*(N - D*q) + q), div_fixup.  With
-// b normal, 1/b normal and a >= 2^-100 (or a == 0) div_scale is the identity
-// and div_fmas a plain fma, so hoisting the reciprocal out of the loop gives
-// bit-identical quotients for 1 mul + 4 fma.  Anything else takes the
-// compiler's full division.
-struct DivNorm {
-    float norm;
-    float r;
-    uint32_t lo1;  // bits(thr_lo) - 1: |x| in (0, thr_lo) takes the full division
-    uint32_t hi;   // bits(thr_hi): |x| above (and inf / NaN) takes the full division
-    bool fast;     // uniform: norm in [2^-100, 2^100]
-};
-
-__device__ __forceinline__ DivNorm make_div(float norm)
-{
-    DivNorm d;
-    d.norm = norm;
-    d.fast = norm >= 0x1p-100f && norm <= 0x1p100f;
-    float r = __builtin_amdgcn_rcpf(norm);
-    const float e = fmaf(-norm, r, 1.0f);
-    d.r = fmaf(e, r, r);
-    // thr_lo keeps |x| >= 2^-100 (no numerator scaling) and |x|/norm >= 2^-120
-    // (normal quotient); thr_hi keeps |x|/norm <= 2^64 (no overflow scaling)
-    d.lo1 = __float_as_uint(fmaxf(0x1p-100f, norm * 0x1p-120f)) - 1u;
-    d.hi = __float_as_uint(fminf(norm * 0x1p64f, 3.4028234e38f));
-    return d;
-}
-
-__device__ __forceinline__ float div_fast(float a, const DivNorm &d)
-{
-    float q = a * d.r;
-    float e = fmaf(-d.norm, q, a);
-    q = fmaf(e, d.r, q);
-    e = fmaf(-d.norm, q, a);
-    return fmaf(e, d.r, q);
-}
-
-// running range of |x| bit patterns for the fast-division check:
-// mn = min(bits - 1) (zero wraps to 0xFFFFFFFF and never triggers), mx = max(bits)
-struct Range {
-    uint32_t mn = 0xffffffffu, mx = 0u;
-    __device__ __forceinline__ void add4(const float4 &v)
-    {
-        const uint32_t a = __float_as_uint(v.x) & 0x7fffffffu, b = __float_as_uint(v.y) & 0x7fffffffu;
-        const uint32_t c = __float_as_uint(v.z) & 0x7fffffffu, e = __float_as_uint(v.w) & 0x7fffffffu;
-        mn = min(min(mn, a - 1u), min(min(b - 1u, c - 1u), e - 1u));
-        mx = max(max(mx, a), max(max(b, c), e));
-    }
-    __device__ __forceinline__ bool slow(const DivNorm &d) const { return (mn < d.lo1) | (mx > d.hi); }
-};
-
 // lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
 // input) gives xi = 0 (fmaxf(NaN, 0) = 0); an infinite one saturates at s.
 template <int ABL = 0>
@@ -110,16 +57,6 @@ __device__ __forceinline__ float4 quot4_fast(const float4 &v, const DivNorm &d)
         q.z = div_fast(fabsf(v.z), d);
         q.w = div_fast(fabsf(v.w), d);
     }
-    return q;
-}
-
-__device__ __forceinline__ float4 quot4_ieee(const float4 &v, float norm)
-{
-    float4 q;
-    q.x = fabsf(v.x) / norm;
-    q.y = fabsf(v.y) / norm;
-    q.z = fabsf(v.z) / norm;
-    q.w = fabsf(v.w) / norm;
     return q;
 }
 

@@ -76,7 +76,8 @@ typedef struct gc_rng {
  * so a SUM all-reduce of the uint32 words over `world` ranks never carries
  * between lanes.  per_word = floor(32/bits) lanes per word.  Planar: word j
  * holds elements j, j+M, ..., j+(per_word-1)*M, M = plane_words =
- * roundup(ceil(n/per_word), 4).  Elements >= n contribute 0 bits. */
+ * roundup(ceil(n/per_word), A), A = 64 words if ceil(n/per_word) >= 65536 else 4.
+ * Elements >= n contribute 0 bits. */
 typedef struct gc_lanes {
     uint64_t n;           /* elements */
     uint64_t plane_words; /* M = words in the stream */
