@@ -34,12 +34,14 @@ __device__ __forceinline__ uint32_t enc_lane(float x, float ql, float s, int32_t
     // v_med3_f32(l, 0, s): clamps to [0, s]; a NaN l yields 0 (checked against
     // the oracle by tests/test_gpu_parity.py::test_encode_non_finite_and_tiny_inputs)
     const float l = (ABL & ENC_MED3) ? fminf(fmaxf(ql * s, 0.0f), s) : __builtin_amdgcn_fmed3f(ql * s, 0.0f, s);
-    const int32_t fl = (int32_t)l;
+    const uint32_t fl = (uint32_t)(int32_t)l;
     const float p = __builtin_amdgcn_fractf(l);
     const float u = (float)(r & 0xFFFFFFu) * 0x1p-24f;
-    const int32_t xi = fl + (u < p ? 1 : 0);
-    const int32_t m = (__float_as_int(x) >> 30) | 1;  // -1 if the sign bit is set, else +1
-    return (uint32_t)(m * xi + qmax);
+    const uint32_t xi = fl + (u < p ? 1u : 0u);
+    // qmax + sign(x)*xi without a multiply: sg = 0 or ~0 from the sign bit
+    // (-0.0 and signed NaN give xi = 0 anyway): (xi ^ sg) - sg + qmax
+    const uint32_t sg = (uint32_t)(__float_as_int(x) >> 31);
+    return (xi ^ sg) + ((uint32_t)qmax - sg);
 }
 
 template <int ABL>
