@@ -81,8 +81,8 @@ __device__ __forceinline__ uint4 draws4_abl(const RngArgs &rng, uint32_t level, 
 // no per-element bounds, 32-bit element indices, L float4 loads in flight.
 // Tail quads, gathers, unaligned x and the non-fast-division case go through
 // the generic body.
-template <int L, int KIND, int MODE, int ABL>
-__global__ __launch_bounds__(kBlock) void k_qsgd_encode(const float *__restrict__ x, const int64_t *__restrict__ idx,
+template <int L, int KIND, int MODE, int ABL, int MINW = 1>
+__global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__restrict__ x, const int64_t *__restrict__ idx,
                                                         uint64_t n, const float *__restrict__ normp, float s,
                                                         int32_t qmax, uint32_t w, uint64_t M, RngArgs rng,
                                                         uint32_t *__restrict__ words)

@@ -239,6 +239,12 @@ int main(int argc, char **argv)
     row("encode max+min clamp", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 2048)), enc_bytes);
     row("encode max+min clamp g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 16384)), enc_bytes);
     row("encode NORNG|NODIV g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 16384)), enc_bytes);
+    for (int rep = 0; rep < 3; ++rep) {
+        row("A/B: encode product (MINW=1) g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, 0>, 2048)), enc_bytes);
+        row("A/B: encode >=4 waves/SIMD", T.run(enc(k_qsgd_encode<6, 0, 0, 0, 4>, 2048)), enc_bytes);
+        row("A/B: encode >=6 waves/SIMD", T.run(enc(k_qsgd_encode<6, 0, 0, 0, 6>, 2048)), enc_bytes);
+        row("A/B: encode >=8 waves/SIMD", T.run(enc(k_qsgd_encode<6, 0, 0, 0, 8>, 2048)), enc_bytes);
+    }
     row("encode COMPUTE ONLY (16KB window) g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 2048)), enc_bytes);
     row("encode COMPUTE ONLY g=8192", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 8192)), enc_bytes);
     row("encode COMPUTE ONLY, no Philox", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2 | ENC_ABL_NORNG>, 2048)), enc_bytes);
@@ -268,5 +274,6 @@ int main(int argc, char **argv)
     same("philox impl 0", k_qsgd_encode<6, 0, 0, ENC_PHX0>);
     same("philox impl 2", k_qsgd_encode<6, 0, 0, ENC_PHX2>);
     same("max+min clamp", k_qsgd_encode<6, 0, 0, ENC_MED3>);
+    same(">=8 waves/SIMD", k_qsgd_encode<6, 0, 0, 0, 8>);
     return 0;
 }
