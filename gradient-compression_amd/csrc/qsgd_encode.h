@@ -24,6 +24,7 @@ enum : int {
     ENC_PHX2 = 8,       // Philox instruction mix 2 (same outputs)
     ENC_MED3 = 16,      // clamp with v_max + v_min instead of v_med3_f32
     ENC_ABL_L2 = 32,    // measurement only: loads from a 16 KB window (compute floor)
+    ENC_REV = 64,       // walk the full tiles from the top down (Infinity-Cache reuse after absmax)
 };
 
 // lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
     const uint64_t full = (MODE == 0 && fast && n >= last + 4 && n < (1ull << 32)) ? (n - last) >> 2 : 0;
     const uint32_t M32 = (uint32_t)M;
     for (; t < full; t += stride) {
-        const uint32_t t4 = (uint32_t)t * 4u;
+        const uint32_t t4 = (uint32_t)((ABL & ENC_REV) ? (full - 1 - t) : t) * 4u;
         float4 xv[L];
 #pragma unroll
         for (int k = 0; k < L; ++k)
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
             acc.z |= enc_lane<ABL>(xv[k].z, q[k].z, s, qmax, r.z) << sh;
             acc.w |= enc_lane<ABL>(xv[k].w, q[k].w, s, qmax, r.w) << sh;
         }
-        *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
+        *reinterpret_cast<uint4 *>(words + t4) = acc;
     }
     // generic body: tail quads (partial planes), gathers, unaligned x, odd norms
     for (; t < quads; t += stride) {

@@ -124,6 +124,28 @@ __global__ __launch_bounds__(256) void k_write_nt(uint4 *o, uint64_t n4)
     }
 }
 
+__global__ __launch_bounds__(256) void k_flush(uint4 *o, uint64_t n4)
+{
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < n4; t += gridDim.x * 256ull)
+        o[t] = make_uint4((uint32_t)t, 0, 0, 0);
+}
+
+// absmax walking the array downward (lab variant of the product's k_absmax)
+__global__ __launch_bounds__(1024) void k_absmax_rev(const float4 *x, uint64_t n4, uint32_t *out)
+{
+    uint32_t m = 0;
+    const uint64_t stride = gridDim.x * 1024ull;
+    for (uint64_t t = blockIdx.x * 1024ull + threadIdx.x; t < n4; t += stride) {
+        float4 v = x[n4 - 1 - t];
+        m = max(m, max(max(__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu),
+                       max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
+    }
+    for (int o = 32; o > 0; o >>= 1)
+        m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    if ((threadIdx.x & 63) == 0 && m)
+        atomicMax(out, m);
+}
+
 struct Timer {
     hipEvent_t a, b;
     Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
@@ -245,6 +267,44 @@ int main(int argc, char **argv)
         row("A/B: encode >=6 waves/SIMD", T.run(enc(k_qsgd_encode<6, 0, 0, 0, 6>, 2048)), enc_bytes);
         row("A/B: encode >=8 waves/SIMD", T.run(enc(k_qsgd_encode<6, 0, 0, 0, 8>, 2048)), enc_bytes);
     }
+    {
+        // Infinity-Cache reuse inside one step: flush 600 MB, then time absmax -> encode
+        uint4 *fl;
+        CK(hipMalloc(&fl, 600ull << 20));
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        auto pair = [&](const char *nm, auto am, auto en) {
+            float tot = 0;
+            for (int i = 0; i < 12; ++i) {
+                hipLaunchKernelGGL(k_flush, dim3(8192), dim3(256), 0, 0, fl, (600ull << 20) / 16);
+                CK(hipEventRecord(a, 0));
+                am();
+                en();
+                CK(hipEventRecord(b, 0));
+                CK(hipEventSynchronize(b));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a, b));
+                if (i >= 2)
+                    tot += ms;
+            }
+            row(nm, tot / 10, 8.0 * n + 4.0 * M);
+        };
+        auto am_fwd = [&] { gc_absmax_f32(x, nullptr, n, norm, ws, nullptr); };
+        auto am_rev = [&] {
+            CK(hipMemsetAsync(norm, 0, 4, 0));
+            hipLaunchKernelGGL(k_absmax_rev, dim3(256), dim3(1024), 0, 0, (const float4 *)x, n / 4, (uint32_t *)norm);
+        };
+        for (int rep = 0; rep < 2; ++rep) {
+            pair("COLD step: absmax fwd + encode fwd", am_fwd, enc(k_qsgd_encode<6, 0, 0, 0>, 2048));
+            pair("COLD step: absmax fwd + encode REV", am_fwd, enc(k_qsgd_encode<6, 0, 0, ENC_REV>, 2048));
+            pair("COLD step: absmax REV + encode fwd", am_rev, enc(k_qsgd_encode<6, 0, 0, 0>, 2048));
+            pair("COLD step: absmax REV + encode REV", am_rev, enc(k_qsgd_encode<6, 0, 0, ENC_REV>, 2048));
+        }
+        pair("COLD encode only (after flush)", [] {}, enc(k_qsgd_encode<6, 0, 0, 0>, 2048));
+        pair("COLD absmax only (after flush)", am_fwd, [] {});
+        CK(hipFree(fl));
+    }
     row("encode COMPUTE ONLY (16KB window) g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 2048)), enc_bytes);
     row("encode COMPUTE ONLY g=8192", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 8192)), enc_bytes);
     row("encode COMPUTE ONLY, no Philox", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2 | ENC_ABL_NORNG>, 2048)), enc_bytes);
@@ -275,5 +335,6 @@ int main(int argc, char **argv)
     same("philox impl 2", k_qsgd_encode<6, 0, 0, ENC_PHX2>);
     same("max+min clamp", k_qsgd_encode<6, 0, 0, ENC_MED3>);
     same(">=8 waves/SIMD", k_qsgd_encode<6, 0, 0, 0, 8>);
+    same("reverse tile order", k_qsgd_encode<6, 0, 0, ENC_REV>);
     return 0;
 }
