@@ -62,3 +62,36 @@ def reducer_vs_reference(rank, world, init_file, fixture, out_dir):
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def hip_reducer_vs_reference(rank, world, init_file, fixture, out_dir):
+    """Our reducers on the GPU (HIP codec, torch-mode RNG), gloo over CUDA tensors."""
+    import gcodec
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    z = np.load(fixture, allow_pickle=False)
+    gen = gcodec.Generator(0, "torch")
+    res = {}
+    from gcodec import reducer as R
+
+    for name in REDUCERS:
+        red = make_reducer(name, generator=gen)
+        red._device = dev
+        torch.manual_seed(SEED + rank)
+        for step in range(2):
+            gin = []
+            i = 0
+            while f"r{rank}/{name}/s{step}/in{i}" in z.files:
+                gin.append(torch.from_numpy(z[f"r{rank}/{name}/s{step}/in{i}"].copy()).to(dev))
+                i += 1
+            gout = [torch.empty_like(g) for g in gin]
+            bits = red.reduce(gin, gout)
+            torch.cuda.synchronize()
+            for i, g in enumerate(gout):
+                res[f"{name}/s{step}/out{i}"] = g.cpu().numpy()
+            res[f"{name}/s{step}/bits"] = np.int64(bits)
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
