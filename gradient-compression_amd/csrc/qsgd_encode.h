@@ -25,6 +25,9 @@ enum : int {
     ENC_MED3 = 16,      // clamp with v_max + v_min instead of v_med3_f32
     ENC_ABL_L2 = 32,    // measurement only: loads from a 16 KB window (compute floor)
     ENC_REV = 64,       // walk the full tiles from the top down (Infinity-Cache reuse after absmax)
+    ENC_GRP2 = 128,     // schedule the planes in pairs (fewer live Philox chains -> fewer VGPRs)
+    ENC_GRP3 = 256,     // schedule the planes in triples
+    ENC_SEQ = 512,      // one plane at a time: per-plane range check, sched barrier between planes
 };
 
 // lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
@@ -106,6 +109,26 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
         for (int k = 0; k < L; ++k)
             xv[k] = *reinterpret_cast<const float4 *>(x + ((ABL & ENC_ABL_L2) ? ((k * M32 + t4) & 4095u)
                                                                                 : (k * M32 + t4)));
+        if constexpr ((ABL & ENC_SEQ) != 0) {
+            uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                if (k)
+                    __builtin_amdgcn_sched_barrier(0);
+                const uint32_t i0 = k * M32 + t4;
+                const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
+                Range rg;
+                rg.add4(xv[k]);
+                const float4 q = __builtin_expect(rg.slow(dv), 0) ? quot4_ieee(xv[k], norm) : quot4_fast<ABL>(xv[k], dv);
+                const uint32_t sh = (uint32_t)k * w;
+                acc.x |= enc_lane<ABL>(xv[k].x, q.x, s, qmax, r.x) << sh;
+                acc.y |= enc_lane<ABL>(xv[k].y, q.y, s, qmax, r.y) << sh;
+                acc.z |= enc_lane<ABL>(xv[k].z, q.z, s, qmax, r.z) << sh;
+                acc.w |= enc_lane<ABL>(xv[k].w, q.w, s, qmax, r.w) << sh;
+            }
+            *reinterpret_cast<uint4 *>(words + t4) = acc;
+            continue;
+        }
         float4 q[L];
         Range rg;
 #pragma unroll
@@ -119,8 +142,11 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
                 q[k] = quot4_ieee(xv[k], norm);
         }
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+        constexpr int G = (ABL & ENC_GRP2) ? 2 : ((ABL & ENC_GRP3) ? 3 : L);
 #pragma unroll
         for (int k = 0; k < L; ++k) {
+            if (k && (k % G) == 0)
+                __builtin_amdgcn_sched_barrier(0);
             const uint32_t i0 = k * M32 + t4;
             const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
             const uint32_t sh = (uint32_t)k * w;

@@ -124,10 +124,14 @@ __global__ __launch_bounds__(256) void k_write_nt(uint4 *o, uint64_t n4)
     }
 }
 
+// read-only flush: fills the Infinity Cache with CLEAN lines of another buffer
 __global__ __launch_bounds__(256) void k_flush(uint4 *o, uint64_t n4)
 {
+    uint32_t acc = 0;
     for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < n4; t += gridDim.x * 256ull)
-        o[t] = make_uint4((uint32_t)t, 0, 0, 0);
+        acc ^= o[t].x;
+    if (acc == 0x12345678u)
+        o[0].y = acc;
 }
 
 // absmax walking the array downward (lab variant of the product's k_absmax)
@@ -263,14 +267,19 @@ int main(int argc, char **argv)
     row("encode NORNG|NODIV g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 16384)), enc_bytes);
     for (int rep = 0; rep < 3; ++rep) {
         row("A/B: encode product (MINW=1) g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, 0>, 2048)), enc_bytes);
-        row("A/B: encode >=4 waves/SIMD", T.run(enc(k_qsgd_encode<6, 0, 0, 0, 4>, 2048)), enc_bytes);
-        row("A/B: encode >=6 waves/SIMD", T.run(enc(k_qsgd_encode<6, 0, 0, 0, 6>, 2048)), enc_bytes);
-        row("A/B: encode >=8 waves/SIMD", T.run(enc(k_qsgd_encode<6, 0, 0, 0, 8>, 2048)), enc_bytes);
+        row("A/B: encode planes in pairs", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_GRP2>, 2048)), enc_bytes);
+        row("A/B: encode planes in triples", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_GRP3>, 2048)), enc_bytes);
+        row("A/B: encode SEQ planes", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_SEQ>, 2048)), enc_bytes);
+        row("A/B: encode SEQ planes >=6 waves", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_SEQ, 6>, 2048)), enc_bytes);
+        row("A/B: encode SEQ planes >=8 waves", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>, 2048)), enc_bytes);
+        row("A/B: encode SEQ planes >=8 waves g=4096", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>, 4096)), enc_bytes);
     }
     {
         // Infinity-Cache reuse inside one step: flush 600 MB, then time absmax -> encode
         uint4 *fl;
         CK(hipMalloc(&fl, 600ull << 20));
+        CK(hipMemset(fl, 0, 600ull << 20));
+        CK(hipDeviceSynchronize());
         hipEvent_t a, b;
         CK(hipEventCreate(&a));
         CK(hipEventCreate(&b));
@@ -336,5 +345,8 @@ int main(int argc, char **argv)
     same("max+min clamp", k_qsgd_encode<6, 0, 0, ENC_MED3>);
     same(">=8 waves/SIMD", k_qsgd_encode<6, 0, 0, 0, 8>);
     same("reverse tile order", k_qsgd_encode<6, 0, 0, ENC_REV>);
+    same("planes in pairs", k_qsgd_encode<6, 0, 0, ENC_GRP2>);
+    same("SEQ planes", k_qsgd_encode<6, 0, 0, ENC_SEQ>);
+    same("SEQ planes >=8 waves", k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>);
     return 0;
 }
