@@ -1,0 +1,70 @@
+"""Chunked, stream-overlapped QSGD-MaxNorm all-reduce.
+
+One bucket is cut into C contiguous chunks.  The max-norm is global over the
+whole bucket, so it is still computed once (absmax -> all_reduce MAX).  Then,
+per chunk:
+    encode(c)       on the compute stream                (HIP)
+    all_reduce(c)   on RCCL's stream, after encode(c)    (int32 SUM of packed lanes)
+    decode(c)       on a decode stream, after all_reduce(c)
+so encode(c+1) runs while chunk c is on the wire and chunk c-1 decodes.
+With the generator in torch mode the packed integers equal the unchunked
+encode's (draws are consumed chunk by chunk, in element order).
+
+The reference has no counterpart (it all-reduces one monolithic int8/int32
+vector after the whole compress, reducer.py:528-533).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import codec as _hip_codec
+from .rng import default_generator
+
+
+class ChunkedQSGDAllReduce:
+    def __init__(self, n: int, bits: int, device, chunks: int = 4, group=None, generator=None, codec=None):
+        self.n, self.bits, self.device = n, bits, torch.device(device)
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.world = dist.get_world_size(group)
+        else:
+            self.world = 1
+        self.codec = codec or _hip_codec
+        self.gen = generator or default_generator
+        chunks = max(1, min(chunks, n))
+        step = -(-n // chunks)
+        step = (step + 3) // 4 * 4  # chunk starts stay 16-byte aligned
+        self.bounds = [(s, min(s + step, n)) for s in range(0, n, step)]
+        self.lanes = [self.codec.qsgd_layout(e - s, bits, self.world) for s, e in self.bounds]
+        self.words = [torch.empty(ln.plane_words, dtype=torch.int32, device=self.device) for ln in self.lanes]
+        self.norm = torch.empty(1, dtype=torch.float32, device=self.device)
+        self.dec_stream = torch.cuda.Stream(self.device)
+
+    def bits_per_step(self) -> int:
+        return 32 + sum(32 * w.numel() for w in self.words)
+
+    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty_like(x)
+        W = self.world
+        compute = torch.cuda.current_stream(self.device)
+        self.codec.absmax(x, out=self.norm)
+        if W > 1:
+            dist.all_reduce(self.norm, op=dist.ReduceOp.MAX, group=self.group)
+        works = []
+        for (s, e), ln, wd in zip(self.bounds, self.lanes, self.words):
+            rng = self.gen.reserve(e - s, 1, device=self.device, backend=self.codec)
+            self.codec.qsgd_encode(x[s:e], self.norm, self.bits, rng, W, out=wd, lanes=ln)
+            works.append(dist.all_reduce(wd, group=self.group, async_op=True) if W > 1 else None)
+        # decode stream: starts after the norm is final, then each chunk after its all-reduce
+        self.dec_stream.wait_stream(compute)
+        with torch.cuda.stream(self.dec_stream):
+            for (s, e), ln, wd, wk in zip(self.bounds, self.lanes, self.words, works):
+                if wk is not None:
+                    wk.wait()  # the decode stream waits for RCCL, the host does not block
+                self.codec.qsgd_decode(wd, e - s, self.norm, self.bits, W, 1.0 / W, out=out[s:e], lanes=ln)
+        compute.wait_stream(self.dec_stream)
+        for t in [x, out, self.norm, *self.words]:
+            t.record_stream(self.dec_stream)
+        return out

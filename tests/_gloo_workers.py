@@ -95,3 +95,22 @@ def hip_reducer_vs_reference(rank, world, init_file, fixture, out_dir):
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def hip_pipeline_world(rank, world, init_file, out_dir, n, bits, chunks):
+    """ChunkedQSGDAllReduce on the GPU with a gloo group (CUDA tensors)."""
+    import gcodec
+    from oracle import oracle as O
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    x = O.gen_input(n, seed=100 + rank, kind=rank % 2)
+    gen = gcodec.Generator(7 + rank, "philox")
+    pipe = gcodec.ChunkedQSGDAllReduce(n, bits, dev, chunks=chunks, generator=gen)
+    out = pipe(torch.from_numpy(x).to(dev))
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"p{rank}.npz"), out=out.cpu().numpy(),
+             bounds=np.array(pipe.bounds, dtype=np.int64))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -39,3 +39,29 @@ def test_hip_reducers_match_reference(world):
                         assert a.tobytes() == b.tobytes(), f"rank {r} {name} step {step} tensor {i}"
                         i += 1
                     assert i > 0
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 3), (3, 1)])
+def test_chunked_pipeline_multirank(world, chunks):
+    """Every rank's result = oracle: per chunk, sum the ranks' packed words and decode."""
+    from oracle import oracle as O
+
+    n, bits = 300_007, 4
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(W.hip_pipeline_world, args=(world, os.path.join(td, "init"), td, n, bits, chunks), nprocs=world,
+                 join=True)
+        outs = [np.load(os.path.join(td, f"p{r}.npz"), allow_pickle=False) for r in range(world)]
+    xs = [O.gen_input(n, seed=100 + r, kind=r % 2) for r in range(world)]
+    norm = max(O.absmax(x) for x in xs)
+    bounds = outs[0]["bounds"]
+    exp = np.empty(n, np.float32)
+    off = 0
+    for s, e in bounds:
+        tot = None
+        for r in range(world):
+            w = O.qsgd_encode(xs[r][s:e], norm, bits, world, O.philox_rng(7 + r, off)).astype(np.uint64)
+            tot = w if tot is None else tot + w
+        exp[s:e] = O.qsgd_decode(tot.astype(np.uint32), e - s, norm, bits, world, np.float32(1.0 / world))
+        off += e - s
+    for r in range(world):
+        assert outs[r]["out"].tobytes() == exp.tobytes(), f"rank {r}"

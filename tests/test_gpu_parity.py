@@ -345,3 +345,35 @@ def test_full_size_properties_100m():
     xs = x[:k0].cpu().numpy()
     q_ref = O.qsgd_quantize(xs, np.float32(norm.item()), bits, O.philox_rng(42, 0))
     assert np.array_equal(lanes[:k0].cpu().numpy(), q_ref)
+
+
+# --------------------------------------------------------------------------- chunked pipeline
+@pytest.mark.parametrize("chunks", [1, 3, 7])
+def test_chunked_pipeline_world1(chunks):
+    """torch mode: chunked == unchunked bit for bit; Philox mode: every chunk
+    equals the oracle's encode/decode of that chunk."""
+    n, bits = 1_000_003, 4
+    x = O.gen_input(n, seed=21, kind=1)
+    xd = dev(x)
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(3)
+        c = gcodec.QSGDMaxNormCompressor(DEV, bits)
+        norm = codec.absmax(xd)
+        ref = c.decode(norm, c.encode(norm, xd), n)
+        torch.manual_seed(3)
+        pipe = gcodec.ChunkedQSGDAllReduce(n, bits, DEV, chunks=chunks)
+        got = pipe(xd)
+        torch.cuda.synchronize()
+        assert bits_eq(u32(got), u32(ref))
+    finally:
+        gcodec.set_rng_mode("philox")
+    gen = gcodec.Generator(99, "philox")
+    pipe = gcodec.ChunkedQSGDAllReduce(n, bits, DEV, chunks=chunks, generator=gen)
+    got = pipe(xd).cpu().numpy()
+    nh = O.absmax(x)
+    off = 0
+    for s, e in pipe.bounds:
+        w = O.qsgd_encode(x[s:e], nh, bits, 1, O.philox_rng(99, off))
+        assert bits_eq(got[s:e], O.qsgd_decode(w, e - s, nh, bits, 1))
+        off += e - s
