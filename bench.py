@@ -98,6 +98,99 @@ def cpu_baseline(n: int, bits: int, budget_s: float):
                       f"quantize + pack, {bits}-bit), {t_tot:.1f} s on 1 host thread"}
 
 
+def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
+    """BASELINE.json configs 3-5 (parity cases; not the headline `value`)."""
+    res = {}
+    reps = max(5, K // 2)
+
+    def sync_ms(fn, reps=reps):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+        return el / reps * 1e3
+
+    # config 3: two-scale "4+2" on a ResNet50-sized bucket (MultiScale levels [2, 4])
+    n3 = 23_520_842
+    g = torch.Generator(device=dev).manual_seed(11 + rank)
+    x3 = torch.randn(n3, device=dev, generator=g).mul_(0.01)
+    gen = gcodec.Generator(5 + rank, "philox")
+    for tag, ms in (("twoscale_2_4", gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen)),
+                    ("multiscale_2_4", gcodec.QSGDMaxNormMultiScaleCompressor(dev, [2, 4], generator=gen))):
+        nrm = torch.empty(1, device=dev)
+        holder = {}
+
+        def ms_step():
+            codec.absmax(x3, out=nrm)
+            if world > 1:
+                dist.all_reduce(nrm, op=dist.ReduceOp.MAX)
+            m = ms.encode_mask(nrm, x3, world)
+            if world > 1:
+                dist.all_reduce(m)
+            w = ms.encode(nrm, x3, m, world)
+            if world > 1:
+                dist.all_reduce(w)
+            holder["d"] = ms.decode(nrm, w, m, n3, world, 1.0 / world)
+
+        t = sync_ms(ms_step)
+        res[f"config3_{tag}"] = {
+            "n": n3, "ms_per_step": t, "grad_floats_per_s": world * n3 / (t * 1e-3),
+            "step": "absmax, MAX, mask encode, SUM(mask lanes), select encode, SUM(words), decode"}
+    del x3
+
+    # config 4: GRandK K=10000, 4-bit, VGG16-sized bucket: gather -> encode -> RCCL -> decode/scatter
+    n4, K4 = 14_728_266, 10_000
+    g = torch.Generator(device=dev).manual_seed(12 + rank)
+    x4 = torch.randn(n4, device=dev, generator=g).mul_(0.01)
+    idx = torch.randperm(n4, generator=torch.Generator().manual_seed(42))[:K4].to(dev)
+    comp = gcodec.GlobalRandKMaxNormCompressor(dev, 4, generator=gen)
+    nrm = torch.empty(1, device=dev)
+
+    def rk_step():
+        codec.absmax(x4, idx=idx, out=nrm)
+        if world > 1:
+            dist.all_reduce(nrm, op=dist.ReduceOp.MAX)
+        w = comp.encode(nrm, x4, world, idx=idx)
+        if world > 1:
+            dist.all_reduce(w)
+        comp.decode(nrm, w, K4, world, 1.0, idx=idx, out=x4)
+
+    t = sync_ms(rk_step, reps=max(20, reps))
+    res["config4_grandk_k10000"] = {"n": n4, "K": K4, "us_per_step": t * 1e3,
+                                    "step": "gather-absmax, MAX, gather-encode, SUM(words), decode-scatter"}
+    del x4
+
+    # config 5: 1B fp32, 8-bit, chunked encode | RCCL SUM | decode on separate streams
+    n5 = 1_000_000_000
+    try:
+        x5 = torch.empty(n5, device=dev).normal_(0, 0.01)
+        out5 = torch.empty_like(x5)
+        pipe = gcodec.ChunkedQSGDAllReduce(n5, 8, dev, chunks=8, generator=gen)
+        t = sync_ms(lambda: pipe(x5, out5), reps=3)
+        ln = codec.qsgd_layout(n5, 8, world)
+        res["config5_1b_8bit_chunked"] = {
+            "n": n5, "chunks": 8, "ms_per_step": t, "grad_floats_per_s": world * n5 / (t * 1e-3),
+            "lane_bits": ln.bits, "packed_bytes_per_rank": 4 * ln.plane_words,
+            "reference_wire_bytes_per_rank": 4 * n5}
+        del x5, out5, pipe
+    except torch.cuda.OutOfMemoryError:
+        res["config5_1b_8bit_chunked"] = {"skipped": "out of device memory"}
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     args = _args()
     import torch
@@ -266,6 +359,9 @@ def main():
         torch.cuda.synchronize()
         out["torch_parity_mode"] = {"n": n_mt, "grad_floats_per_s": n_mt / (time.perf_counter() - t0),
                                     "note": "MT19937 stream generated serially by one workgroup, then encode"}
+
+    if not args.no_extras:
+        out["configs"] = other_configs(torch, dist, gcodec, codec, dev, world, rank, K)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(n, bits, args.cpu_seconds)

@@ -255,6 +255,52 @@ int main(int argc, char **argv)
                                (uint64_t)M, ra, words2);
         };
     };
+    {
+        // placement: do the HBM addresses of the 6 plane read streams and the
+        // write stream (relative to each other) change the encode time?
+        float *xp;
+        uint32_t *wp;
+        const uint64_t padf = 1u << 20;
+        CK(hipMalloc(&xp, (n + padf) * 4));
+        CK(hipMalloc(&wp, ((size_t)M + padf) * 4));
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, xp, n + padf, 7u);
+        CK(hipDeviceSynchronize());
+        auto encp = [&](const float *xb, uint32_t *wb, uint64_t Mp) {
+            return [=] {
+                hipLaunchKernelGGL((k_qsgd_encode<6, 0, 0, 0>), dim3(2048), dim3(256), 0, 0, xb,
+                                   (const int64_t *)nullptr, n, norm, s, qmax, ln.bits, Mp, ra, wb);
+            };
+        };
+        for (int rep = 0; rep < 2; ++rep) {
+            row("place: product dst=words", T.run(encp(x, words, M)), enc_bytes);
+            row("place: product dst=words2", T.run(encp(x, words2, M)), enc_bytes);
+            row("place: product dst=wp", T.run(encp(x, wp, M)), enc_bytes);
+            row("place: xp dst=wp", T.run(encp(xp, wp, M)), enc_bytes);
+        }
+        for (uint64_t woff : {0ull, 64ull, 512ull, 1024ull, 4096ull, 65536ull}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "place: dst=wp+%llu words", (unsigned long long)woff);
+            row(nm, T.run(encp(xp, wp + woff, M)), enc_bytes);
+        }
+        for (uint64_t xoff : {64ull, 512ull, 1024ull, 4096ull, 65536ull}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "place: x=xp+%llu floats", (unsigned long long)xoff);
+            row(nm, T.run(encp(xp + xoff, wp, M)), enc_bytes);
+        }
+        for (uint64_t d : {64ull, 128ull, 256ull, 512ull, 1024ull, 2048ull, 4096ull, 8192ull, 16384ull}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "place: plane stride M+%llu", (unsigned long long)d);
+            row(nm, T.run(encp(xp, wp, M + d)), enc_bytes);
+        }
+        for (uint64_t d : {0ull, 64ull, 256ull, 1024ull, 4096ull}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "place: copy_planar stride M+%llu", (unsigned long long)d);
+            row(nm, T.run([&] { hipLaunchKernelGGL(k_copy_planar<6>, dim3(2048), dim3(256), 0, 0, xp, (uint32_t)(M + d), wp); }),
+                enc_bytes);
+        }
+        CK(hipFree(xp));
+        CK(hipFree(wp));
+    }
     for (unsigned g : {2048u, 8192u, 16384u, 32768u}) {
         char nm[96];
         snprintf(nm, sizeof nm, "encode ABL=0 (exact) g=%u", g);
