@@ -150,6 +150,37 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
             "step": "absmax, MAX, mask encode, SUM(mask lanes), select encode, SUM(words), decode"}
     del x3
 
+    # fused TensorBuffer / setgrad on the ResNet50 list (161 tensors)
+    from gcodec import shapes
+    sizes = shapes.resnet50_sizes()
+    base = torch.randn(sum(sizes) + 4 * len(sizes), device=dev, generator=g).mul_(0.01)
+    grads, pos = [], 0
+    for sz in sizes:
+        grads.append(base[pos:pos + sz])
+        pos += sz + (sz % 4 == 0) * 4  # keep most tensors 16-byte aligned like separate allocations
+    segs = codec.Segments(grads)
+    ln3 = codec.qsgd_layout(segs.n, 4, world)
+    nrm = torch.empty(1, device=dev)
+    flat = torch.empty(segs.n, device=dev)
+    w3 = torch.empty(ln3.plane_words, dtype=torch.int32, device=dev)
+    codec.qsgd_encode(torch.cat(grads), nrm, 4, gen.reserve(segs.n), world, out=w3, lanes=ln3)
+    ep = {"tensors": len(sizes), "n": segs.n}
+    ep["unfused_flatten_norm_ms"] = sync_ms(lambda: codec.absmax(torch.cat(grads), out=nrm))
+    ep["fused_flatten_norm_ms"] = sync_ms(lambda: codec.segments_flatten_absmax(segs, flat, nrm))
+
+    def unfused_setgrad():
+        d = codec.qsgd_decode(w3, segs.n, nrm, 4, world, 1.0 / world, out=flat, lanes=ln3)
+        torch._foreach_copy_(grads, list(torch.split(d, sizes)))
+
+    ep["unfused_decode_setgrad_ms"] = sync_ms(unfused_setgrad)
+    ep["fused_decode_setgrad_ms"] = sync_ms(
+        lambda: codec.qsgd_decode_segments(w3, nrm, 4, segs, world, 1.0 / world, lanes=ln3))
+    for fused in (False, True):
+        red = gcodec.QSGDMaxNormReducer(dev, quantization_level=4, generator=gen, fused=fused)
+        ep[f"reducer_step_ms_{'fused' if fused else 'unfused'}"] = sync_ms(lambda: red.reduce(grads, grads))
+    res["epilogue_resnet50_qsgd4"] = ep
+    del base, grads, segs, flat
+
     # config 4: GRandK K=10000, 4-bit, VGG16-sized bucket: gather -> encode -> RCCL -> decode/scatter
     n4, K4 = 14_728_266, 10_000
     g = torch.Generator(device=dev).manual_seed(12 + rank)

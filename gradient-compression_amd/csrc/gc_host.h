@@ -24,6 +24,10 @@ int check_lanes(const gc_lanes *l, uint64_t n, const char *what);
 int check_bits(uint32_t bits, const char *what);
 int check_levels(const gc_levels *lv, const char *what);
 
+struct SegArg;  // segments.h
+// validate a gc_segments for a bucket of n elements and make its kernel argument
+int seg_arg(const gc_segments *segs, uint64_t n, SegArg *out, const char *what);
+
 }  // namespace gc
 
 #define GC_REQUIRE(cond, ...)                      \

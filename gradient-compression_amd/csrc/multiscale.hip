@@ -12,6 +12,7 @@
 // draw, so nothing but x is read twice.
 #include "gc_device.h"
 #include "gc_host.h"
+#include "segments.h"
 
 namespace gc {
 
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode(const uint32_t *__restrict
                                                       const int64_t *__restrict__ idx, uint64_t n,
                                                       const float *__restrict__ normp, LevelsArg lv, uint64_t Mq,
                                                       uint32_t wq, int32_t sub, int order, float alpha,
-                                                      float *__restrict__ out)
+                                                      float *__restrict__ out, SegArg sg)
 {
     const float norm = *normp;
     const uint32_t msk = wq >= 32 ? 0xffffffffu : ((1u << wq) - 1u);
@@ -204,7 +205,9 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode(const uint32_t *__restrict
                 o.y = ms_dq((int32_t)((wd.y >> sh) & msk) - sub, norm, sel_level(lv, m.y), order, alpha);
                 o.z = ms_dq((int32_t)((wd.z >> sh) & msk) - sub, norm, sel_level(lv, m.z), order, alpha);
                 o.w = ms_dq((int32_t)((wd.w >> sh) & msk) - sub, norm, sel_level(lv, m.w), order, alpha);
-                if (MODE == 0 && i0 + 4 <= n) {
+                if (MODE == 3) {
+                    seg_store4(sg, i0, n, o);
+                } else if (MODE == 0 && i0 + 4 <= n) {
                     *reinterpret_cast<float4 *>(out + i0) = o;
                 } else {
                     for (int e = 0; e < 4; ++e)
@@ -435,34 +438,54 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
     return launch_status("gc_ms_select_encode");
 }
 
-int gc_ms_decode(const uint32_t *words, const uint32_t *mask_words, const int64_t *idx, uint64_t n, const float *norm,
-                 const gc_levels *levels, const gc_lanes *mask_lanes, const gc_lanes *q_lanes, int order, float alpha,
-                 float *out, gc_stream_t stream)
+static int ms_decode(const char *what, const uint32_t *words, const uint32_t *mask_words, const int64_t *idx,
+                     uint64_t n, const float *norm, const gc_levels *levels, const gc_lanes *mask_lanes,
+                     const gc_lanes *q_lanes, int order, float alpha, float *out, const gc_segments *segs,
+                     gc_stream_t stream)
 {
     int rc;
-    if ((rc = check_levels(levels, "gc_ms_decode")) ||
-        (rc = check_mask_lanes(mask_lanes, levels, n, "gc_ms_decode")) ||
-        (rc = check_q_lanes(q_lanes, levels, n, "gc_ms_decode")))
+    if ((rc = check_levels(levels, what)) || (rc = check_mask_lanes(mask_lanes, levels, n, what)) ||
+        (rc = check_q_lanes(q_lanes, levels, n, what)))
         return rc;
-    GC_REQUIRE(mask_lanes->world == q_lanes->world, "gc_ms_decode: mask and q lanes sized for different worlds");
-    GC_REQUIRE(norm && mask_words && words && (n == 0 || out), "gc_ms_decode: null pointer");
-    GC_REQUIRE(order == 0 || order == 1, "gc_ms_decode: order must be 0 (multi-scale) or 1 (two-scale)");
-    GC_REQUIRE(aligned16(words) && aligned16(mask_words), "gc_ms_decode: words must be 16-byte aligned");
+    GC_REQUIRE(mask_lanes->world == q_lanes->world, "%s: mask and q lanes sized for different worlds", what);
+    GC_REQUIRE(norm && mask_words && words && (n == 0 || out || segs), "%s: null pointer", what);
+    GC_REQUIRE(order == 0 || order == 1, "%s: order must be 0 (multi-scale) or 1 (two-scale)", what);
+    GC_REQUIRE(aligned16(words) && aligned16(mask_words), "%s: words must be 16-byte aligned", what);
+    SegArg sg{};
+    if (segs && (rc = seg_arg(segs, n, &sg, what)))
+        return rc;
     if (q_lanes->plane_words == 0)
         return GC_OK;
     hipStream_t st = as_stream(stream);
     const LevelsArg la = levels_arg(levels);
     const MaskArg mk = mask_arg(mask_words, mask_lanes, levels->count);
-    const int mode = idx ? 2 : (aligned16(out) ? 0 : 1);
+    const int mode = segs ? 3 : idx ? 2 : (aligned16(out) ? 0 : 1);
     const unsigned grid = grid_for(q_lanes->plane_words >> 2);
     const int32_t sub = (int32_t)(q_lanes->world * q_lanes->offset);
 #define GC_MD(MODE_)                                                                                               \
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_decode<LL, MODE_>), dim3(grid), dim3(kBlock), 0, st, \
                                                          words, mk, idx, n, norm, la, q_lanes->plane_words,        \
-                                                         q_lanes->bits, sub, order, alpha, out))
-    if (mode == 0) { GC_MD(0); } else if (mode == 1) { GC_MD(1); } else { GC_MD(2); }
+                                                         q_lanes->bits, sub, order, alpha, out, sg))
+    if (mode == 0) { GC_MD(0); } else if (mode == 1) { GC_MD(1); } else if (mode == 2) { GC_MD(2); } else { GC_MD(3); }
 #undef GC_MD
-    return launch_status("gc_ms_decode");
+    return launch_status(what);
+}
+
+int gc_ms_decode(const uint32_t *words, const uint32_t *mask_words, const int64_t *idx, uint64_t n, const float *norm,
+                 const gc_levels *levels, const gc_lanes *mask_lanes, const gc_lanes *q_lanes, int order, float alpha,
+                 float *out, gc_stream_t stream)
+{
+    return ms_decode("gc_ms_decode", words, mask_words, idx, n, norm, levels, mask_lanes, q_lanes, order, alpha, out,
+                     nullptr, stream);
+}
+
+int gc_ms_decode_segments(const uint32_t *words, const uint32_t *mask_words, uint64_t n, const float *norm,
+                          const gc_levels *levels, const gc_lanes *mask_lanes, const gc_lanes *q_lanes, int order,
+                          float alpha, const gc_segments *segs, gc_stream_t stream)
+{
+    GC_REQUIRE(segs, "gc_ms_decode_segments: null segments");
+    return ms_decode("gc_ms_decode_segments", words, mask_words, nullptr, n, norm, levels, mask_lanes, q_lanes, order,
+                     alpha, nullptr, segs, stream);
 }
 
 int gc_ms_mask_unpack(const uint32_t *mask_words, const gc_lanes *mask_lanes, uint32_t levels_count, int8_t *mask,

@@ -15,12 +15,11 @@
 #include "gc_device.h"
 #include "gc_host.h"
 #include "qsgd_encode.h"
+#include "segments.h"
 
 #include <algorithm>
 
 namespace gc {
-
-__device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
 
 // ---------------------------------------------------------------------------
 // max-norm: uint max over |x| bit patterns (exact, order-free, NaN wins like
@@ -35,8 +34,7 @@ __device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v)
 // One 1024-thread block per CU: 16 waves x 4 float4 loads in flight = 64 KB
 // per CU (HBM-saturating), and at most 256 same-address atomics (one word
 // takes ~88 atomics/us, MI355X_MICROARCH.md 'dequeue': 2048 blocks cost ~20 us).
-constexpr unsigned kAbsmaxThreads = 1024;
-constexpr unsigned kAbsmaxMaxBlocks = 256;
+// (kAbsmaxThreads, kAbsmaxMaxBlocks, absmax_finish: segments.h)
 
 template <int MODE, bool WS>  // MODE 0: float4 dense, 1: scalar dense, 2: gather
 __global__ __launch_bounds__(kAbsmaxThreads) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
@@ -65,53 +63,7 @@ __global__ __launch_bounds__(kAbsmaxThreads) void k_absmax(const float *__restri
         for (; t < n; t += stride)
             m = max(m, absbits(MODE == 2 ? x[idx[t]] : x[t]));
     }
-    m = wave_max_u32(m);
-    __shared__ uint32_t part[kAbsmaxThreads / 64];
-    __shared__ int last;
-    if ((threadIdx.x & 63) == 0)
-        part[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if constexpr (!WS) {
-        if (threadIdx.x == 0) {
-            for (unsigned w = 1; w < kAbsmaxThreads / 64; ++w)
-                m = max(m, part[w]);
-            if (m)
-                atomicMax(out, m);
-        }
-        return;
-    } else {
-        uint32_t *ticket = ws;
-        uint32_t *partials = ws + 16;  // own cache line
-        if (threadIdx.x == 0) {
-            for (unsigned w = 1; w < kAbsmaxThreads / 64; ++w)
-                m = max(m, part[w]);
-            // sc1 store, drained, then the agent-scope ticket: the fence-free
-            // hand-off of MI355X_MICROARCH.md (row 1 of the sc1 table) — every
-            // store and every load of the partials is sc1, hipMalloc memory
-            __hip_atomic_store(&partials[blockIdx.x], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint32_t tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = tk == gridDim.x - 1;
-        }
-        __syncthreads();  // the other waves load only after the last add returned
-        if (!last)
-            return;
-        uint32_t v = 0;
-        for (uint32_t i = threadIdx.x; i < gridDim.x; i += kAbsmaxThreads)
-            v = max(v, __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        v = wave_max_u32(v);
-        __syncthreads();
-        if ((threadIdx.x & 63) == 0)
-            part[threadIdx.x >> 6] = v;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t r = part[0];
-            for (unsigned w = 1; w < kAbsmaxThreads / 64; ++w)
-                r = max(r, part[w]);
-            *out = r;
-            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    absmax_finish<WS>(m, out, ws);
 }
 
 // ---------------------------------------------------------------------------
@@ -134,10 +86,14 @@ __device__ __forceinline__ float4 load4(const float *__restrict__ x, const int64
 // ---------------------------------------------------------------------------
 // decode: out = RN(RN(c * (lane - W*qoff)) * alpha), c = RN(norm / s)
 // ---------------------------------------------------------------------------
-template <int MODE>
+template <int MODE>  // 0: float4 dense, 1: scalar dense, 2: scatter through idx, 3: into the tensors of a gc_segments
 __device__ __forceinline__ void store4(float *__restrict__ out, const int64_t *__restrict__ idx, uint64_t i0,
-                                       uint64_t n, float4 v)
+                                       uint64_t n, float4 v, const SegArg &sg)
 {
+    if constexpr (MODE == 3) {
+        seg_store4(sg, i0, n, v);
+        return;
+    }
     if (MODE == 0 && i0 + 4 <= n) {
         *reinterpret_cast<float4 *>(out + i0) = v;
         return;
@@ -163,7 +119,8 @@ template <int L, int MODE>
 __global__ __launch_bounds__(kBlock) void k_qsgd_decode(const uint32_t *__restrict__ words,
                                                         const int64_t *__restrict__ idx, uint64_t n,
                                                         const float *__restrict__ normp, float s, int32_t sub,
-                                                        uint32_t w, uint64_t M, float alpha, float *__restrict__ out)
+                                                        uint32_t w, uint64_t M, float alpha, float *__restrict__ out,
+                                                        SegArg sg)
 {
     const float c = *normp / s;
     const uint32_t mask = w >= 32 ? 0xffffffffu : ((1u << w) - 1u);
@@ -180,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_decode(const uint32_t *__restri
                 o.y = dq(wd.y, sh, mask, sub, c, alpha);
                 o.z = dq(wd.z, sh, mask, sub, c, alpha);
                 o.w = dq(wd.w, sh, mask, sub, c, alpha);
-                store4<MODE>(out, idx, i0, n, o);
+                store4<MODE>(out, idx, i0, n, o, sg);
             }
         }
     }
@@ -380,36 +337,55 @@ int gc_qsgd_encode(const float *x, const int64_t *idx, uint64_t n, const float *
     return launch_status("gc_qsgd_encode");
 }
 
-int gc_qsgd_decode(const uint32_t *words, const int64_t *idx, uint64_t n, const float *norm, uint32_t bits,
-                   const gc_lanes *lanes, float alpha, float *out, gc_stream_t stream)
+static int qsgd_decode(const char *what, const uint32_t *words, const int64_t *idx, uint64_t n, const float *norm,
+                       uint32_t bits, const gc_lanes *lanes, float alpha, float *out, const gc_segments *segs,
+                       gc_stream_t stream)
 {
     int rc;
-    if ((rc = check_bits(bits, "gc_qsgd_decode")) || (rc = check_lanes(lanes, n, "gc_qsgd_decode")))
+    if ((rc = check_bits(bits, what)) || (rc = check_lanes(lanes, n, what)))
         return rc;
     const uint32_t s = (1u << bits) - 1u;
-    GC_REQUIRE(lanes->offset == s && lanes->range == 2ull * s, "gc_qsgd_decode: lanes not made by gc_qsgd_layout");
-    GC_REQUIRE(norm && words && (n == 0 || out), "gc_qsgd_decode: null pointer");
-    GC_REQUIRE(aligned16(words), "gc_qsgd_decode: words must be 16-byte aligned");
+    GC_REQUIRE(lanes->offset == s && lanes->range == 2ull * s, "%s: lanes not made by gc_qsgd_layout", what);
+    GC_REQUIRE(norm && words && (n == 0 || out || segs), "%s: null pointer", what);
+    GC_REQUIRE(aligned16(words), "%s: words must be 16-byte aligned", what);
+    SegArg sg{};
+    if (segs && (rc = seg_arg(segs, n, &sg, what)))
+        return rc;
     if (lanes->plane_words == 0)
         return GC_OK;
     hipStream_t st = as_stream(stream);
-    const int mode = idx ? 2 : (aligned16(out) ? 0 : 1);
+    const int mode = segs ? 3 : idx ? 2 : (aligned16(out) ? 0 : 1);
     const int32_t sub = (int32_t)(lanes->world * s);
     const unsigned grid = grid_for(lanes->plane_words >> 2);
     const float sf = (float)s;
 #define GC_DEC(MODE_)                                                                                         \
     GC_DISPATCH_L(lanes->per_word, hipLaunchKernelGGL((k_qsgd_decode<LL, MODE_>), dim3(grid), dim3(kBlock), 0, \
                                                       st, words, idx, n, norm, sf, sub, lanes->bits,          \
-                                                      lanes->plane_words, alpha, out))
+                                                      lanes->plane_words, alpha, out, sg))
     if (mode == 0) {
         GC_DEC(0);
     } else if (mode == 1) {
         GC_DEC(1);
-    } else {
+    } else if (mode == 2) {
         GC_DEC(2);
+    } else {
+        GC_DEC(3);
     }
 #undef GC_DEC
-    return launch_status("gc_qsgd_decode");
+    return launch_status(what);
+}
+
+int gc_qsgd_decode(const uint32_t *words, const int64_t *idx, uint64_t n, const float *norm, uint32_t bits,
+                   const gc_lanes *lanes, float alpha, float *out, gc_stream_t stream)
+{
+    return qsgd_decode("gc_qsgd_decode", words, idx, n, norm, bits, lanes, alpha, out, nullptr, stream);
+}
+
+int gc_qsgd_decode_segments(const uint32_t *words, uint64_t n, const float *norm, uint32_t bits,
+                            const gc_lanes *lanes, float alpha, const gc_segments *segs, gc_stream_t stream)
+{
+    GC_REQUIRE(segs, "gc_qsgd_decode_segments: null segments");
+    return qsgd_decode("gc_qsgd_decode_segments", words, nullptr, n, norm, bits, lanes, alpha, nullptr, segs, stream);
 }
 
 int gc_qsgd_quantize(const float *x, uint64_t n, const float *norm, uint32_t bits, const gc_rng *rng,

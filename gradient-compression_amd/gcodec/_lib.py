@@ -61,9 +61,25 @@ class gc_levels(C.Structure):
     _fields_ = [("count", C.c_uint32), ("bits", C.c_uint32 * GC_MAX_LEVELS)]
 
 
+class gc_seg(C.Structure):
+    _fields_ = [("start", C.c_uint64), ("end", C.c_uint64), ("ptr", C.c_void_p), ("reserved", C.c_uint64)]
+
+
+class gc_segments(C.Structure):
+    _fields_ = [
+        ("count", C.c_uint64),
+        ("n", C.c_uint64),
+        ("seg", C.c_void_p),
+        ("chunk_seg", C.c_void_p),
+        ("chunk_shift", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
 P = C.c_void_p
 u64, u32, i32, f32, i64 = C.c_uint64, C.c_uint32, C.c_int32, C.c_float, C.c_int64
 RNGP, LANESP, LEVP = C.POINTER(gc_rng), C.POINTER(gc_lanes), C.POINTER(gc_levels)
+SEGSP = C.POINTER(gc_segments)
 
 # name -> (restype, argtypes); must match include/gcodec.h exactly
 SIGNATURES = {
@@ -84,9 +100,15 @@ SIGNATURES = {
     "gc_qsgd_dequantize": (C.c_int, [P, u32, u64, P, u32, f32, P, P]),
     "gc_lane_pack": (C.c_int, [P, u32, LANESP, P, P]),
     "gc_lane_unpack": (C.c_int, [P, LANESP, P, P]),
+    "gc_segments_chunks": (u64, [u64, u32]),
+    "gc_segments_plan": (C.c_int, [P, P, u64, u32, P, P, u64, P]),
+    "gc_segments_flatten_absmax": (C.c_int, [SEGSP, P, P, P, P]),
+    "gc_segments_scatter": (C.c_int, [P, f32, SEGSP, P]),
+    "gc_qsgd_decode_segments": (C.c_int, [P, u64, P, u32, LANESP, f32, SEGSP, P]),
     "gc_ms_mask_encode": (C.c_int, [P, P, u64, P, LEVP, RNGP, LANESP, P, P]),
     "gc_ms_select_encode": (C.c_int, [P, P, u64, P, LEVP, RNGP, P, LANESP, LANESP, P, P]),
     "gc_ms_decode": (C.c_int, [P, P, P, u64, P, LEVP, LANESP, LANESP, C.c_int, f32, P, P]),
+    "gc_ms_decode_segments": (C.c_int, [P, P, u64, P, LEVP, LANESP, LANESP, C.c_int, f32, SEGSP, P]),
     "gc_ms_mask_unpack": (C.c_int, [P, LANESP, u32, P, P]),
     "gc_ms_quantize_mask": (C.c_int, [P, u64, P, LEVP, RNGP, P, P]),
     "gc_ms_select_quantize": (C.c_int, [P, u64, P, LEVP, RNGP, P, P, u32, P]),

@@ -163,6 +163,94 @@ def qsgd_decode(words, n, norm, bits, world=1, alpha=1.0, idx=None, out=None, la
 
 
 # ---------------------------------------------------------------------------
+# per-parameter tensors (reducer.py:46-68 TensorBuffer, 543-549 setgrad)
+# ---------------------------------------------------------------------------
+class Segments:
+    """gc_segments for a list of contiguous fp32 tensors on one device: the
+    reference's TensorBuffer (reducer.py:46-68) as a device table, so flatten,
+    max-norm, decode and setgrad address the tensors in place.  Built once per
+    parameter list (one small H2D copy) and reused; it keeps the tensors alive
+    because the table holds their raw pointers."""
+
+    CHUNK_SHIFT = 12
+
+    def __init__(self, tensors, chunk_shift: int = CHUNK_SHIFT):
+        tensors = list(tensors)
+        if not tensors:
+            raise _lib.GCodecError(_lib.GC_EINVAL, "Segments: empty tensor list")
+        dev = _dev(tensors[0])
+        for t in tensors:
+            if t.device != dev or t.dtype != torch.float32 or not t.is_contiguous():
+                raise _lib.GCodecError(_lib.GC_EINVAL, "Segments: tensors must be contiguous float32 on "
+                                       f"{dev} (got {t.dtype} on {t.device}, contiguous={t.is_contiguous()})")
+        lib = _lib.load()
+        count = len(tensors)
+        sizes = np.array([t.numel() for t in tensors], dtype=np.uint64)
+        ptrs = (C.c_void_p * count)(*[t.data_ptr() or None for t in tensors])
+        n = int(sizes.sum())
+        chunks = int(lib.gc_segments_chunks(n, chunk_shift))
+        seg_host = np.zeros((count, 4), dtype=np.uint64)
+        chunk_host = np.zeros(max(chunks, 1), dtype=np.uint32)
+        n_out = C.c_uint64(0)
+        check(lib.gc_segments_plan(sizes.ctypes.data_as(C.c_void_p), ptrs, count, chunk_shift,
+                                   seg_host.ctypes.data_as(C.c_void_p), chunk_host.ctypes.data_as(C.c_void_p),
+                                   chunks, C.byref(n_out)), "gc_segments_plan")
+        self.device = dev
+        self.n = n
+        self.count = count
+        self.tensors = tensors
+        self.key = Segments.key_of(tensors)
+        self._seg = torch.from_numpy(seg_host.view(np.int64)).to(dev)
+        self._chunk = torch.from_numpy(chunk_host.view(np.int32)).to(dev)
+        self.struct = _lib.gc_segments(count, n, self._seg.data_ptr(), self._chunk.data_ptr(), chunk_shift, 0)
+
+    @staticmethod
+    def key_of(tensors):
+        return tuple((t.data_ptr(), t.numel(), t.dtype, t.device) for t in tensors)
+
+
+def segments_flatten_absmax(segs: Segments, flat: torch.Tensor | None = None, norm: torch.Tensor | None = None,
+                            store: bool = True):
+    """flat = cat(tensors) (if store) and norm = max |x| in one pass.  -> (flat | None, norm)"""
+    dev = segs.device
+    if store and flat is None:
+        flat = torch.empty(segs.n, dtype=torch.float32, device=dev)
+    if norm is None:
+        norm = torch.empty(1, dtype=torch.float32, device=dev)
+    st = _stream(dev)
+    check(_lib.load().gc_segments_flatten_absmax(C.byref(segs.struct), _p(flat) if store else None, _p(norm),
+                                                 _p(_absmax_ws(dev, st)), st), "gc_segments_flatten_absmax")
+    return (flat if store else None), norm
+
+
+def segments_scatter(flat: torch.Tensor, segs: Segments, alpha: float = 1.0):
+    """tensor[s][:] = RN(flat[start:end] * alpha) — the reference's setgrad loop."""
+    _dev(flat)
+    flat = _f32(flat, "segments_scatter")
+    check(_lib.load().gc_segments_scatter(_p(flat), float(alpha), C.byref(segs.struct), _stream(segs.device)),
+          "gc_segments_scatter")
+
+
+def qsgd_decode_segments(words, norm, bits, segs: Segments, world=1, alpha=1.0, lanes=None):
+    """qsgd_decode straight into the tensors (decode + 1/W + setgrad)."""
+    dev = _dev(words)
+    lanes = lanes or qsgd_layout(segs.n, bits, world)
+    nt = norm_tensor(norm, dev)
+    check(_lib.load().gc_qsgd_decode_segments(_p(words), segs.n, _p(nt), bits, C.byref(lanes), float(alpha),
+                                              C.byref(segs.struct), _stream(dev)), "gc_qsgd_decode_segments")
+
+
+def ms_decode_segments(words, mask_words, norm, levels, segs: Segments, world=1, order=0, alpha=1.0):
+    dev = _dev(words)
+    ql, ml = ms_layouts(segs.n, levels, world)
+    lv = levels_struct(levels)
+    nt = norm_tensor(norm, dev)
+    check(_lib.load().gc_ms_decode_segments(_p(words), _p(mask_words), segs.n, _p(nt), C.byref(lv), C.byref(ml),
+                                            C.byref(ql), int(order), float(alpha), C.byref(segs.struct),
+                                            _stream(dev)), "gc_ms_decode_segments")
+
+
+# ---------------------------------------------------------------------------
 # QSGD-MaxNorm unpacked (compressors.py compress/decompress semantics)
 # ---------------------------------------------------------------------------
 def qsgd_quantize(x, norm, bits, rng, level=0, dtype=torch.int8, le_bits=None):

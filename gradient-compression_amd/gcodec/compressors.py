@@ -69,6 +69,9 @@ class QSGDMaxNormCompressor(_Base):
     def decode(self, norm, words, n, world=1, alpha=1.0, idx=None, out=None):
         return self.backend.qsgd_decode(words, n, norm, self._quantization_level, world, alpha, idx, out)
 
+    def decode_segments(self, norm, words, segs, world=1, alpha=1.0):
+        return self.backend.qsgd_decode_segments(words, norm, self._quantization_level, segs, world, alpha)
+
 
 class GlobalRandKMaxNormCompressor(QSGDMaxNormCompressor):
     """compressors.py:419-456 — the same arithmetic applied to the K-subset."""
@@ -115,6 +118,9 @@ class QSGDMaxNormTwoScaleCompressor(_Base):
 
     def decode(self, norm, words, mask_words, n, world=1, alpha=1.0, idx=None, out=None):
         return self.backend.ms_decode(words, mask_words, n, norm, self.levels, world, 1, alpha, idx, out)
+
+    def decode_segments(self, norm, words, mask_words, segs, world=1, alpha=1.0):
+        return self.backend.ms_decode_segments(words, mask_words, norm, self.levels, segs, world, 1, alpha)
 
 
 class GlobalRandKMaxNormTwoScaleCompressor(QSGDMaxNormTwoScaleCompressor):
@@ -163,3 +169,7 @@ class QSGDMaxNormMultiScaleCompressor(_Base):
     def decode(self, norm, words, mask_words, n, world=1, alpha=1.0, idx=None, out=None):
         return self.backend.ms_decode(words, mask_words, n, norm, self._quantization_levels, world, 0, alpha, idx,
                                       out)
+
+    def decode_segments(self, norm, words, mask_words, segs, world=1, alpha=1.0):
+        return self.backend.ms_decode_segments(words, mask_words, norm, self._quantization_levels, segs, world, 0,
+                                               alpha)

@@ -50,7 +50,7 @@ def set_seed(seed: int, generator=None):
 class Reducer:
     """reducer.py:26-43."""
 
-    def __init__(self, device, timer=None, codec=None, generator=None, group=None):
+    def __init__(self, device, timer=None, codec=None, generator=None, group=None, fused=True):
         if dist.is_available() and dist.is_initialized():
             self.n_workers = dist.get_world_size(group)
             self.rank = dist.get_rank(group)
@@ -62,6 +62,8 @@ class Reducer:
         self._codec = codec or _hip_codec
         self._gen = generator or default_generator
         self._group = group
+        self._fused = fused
+        self._seg_cache = {}
 
     def reduce(self, grad_in, grad_out):
         raise NotImplementedError()
@@ -71,10 +73,6 @@ class Reducer:
         if self.n_workers > 1:
             dist.all_reduce(t, op=op, group=self._group)
         return t
-
-    def _norm(self, buffer, idx=None):
-        norm = self._codec.absmax(buffer, idx=idx)
-        return self._all_reduce(norm, dist.ReduceOp.MAX)
 
     def _compressor(self, cls, *args):
         c = cls(self._device, *args, generator=self._gen)
@@ -89,6 +87,54 @@ class Reducer:
         """reducer.py:543-549 (the 1/W is already folded into `flat`)."""
         for grad, out in zip(flat, grad_out):
             out.copy_(grad)
+
+    def _setgrad_scaled(self, flat, grad_out, alpha):
+        """reducer.py:755-761: out[:] = 0; out.add_(grad, alpha) — RN(alpha*g) + 0."""
+        segs = self._segments(grad_out)
+        if segs is not None:
+            self._codec.segments_scatter(flat.buffer, segs, alpha)
+            return
+        for grad, out in zip(flat, grad_out):
+            out.zero_()
+            out.add_(grad, alpha=alpha)
+
+    # -- fused TensorBuffer (gc_segments) ----------------------------------
+    def _segments(self, tensors):
+        """The codec's device table for a parameter list (cached per list), or
+        None when the codec has none or a tensor is not contiguous fp32 on the
+        GPU — then the reducer takes the TensorBuffer path."""
+        make = getattr(self._codec, "Segments", None)
+        tensors = list(tensors)
+        if not self._fused or make is None or not tensors:
+            return None
+        if any(not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous() for t in tensors):
+            return None
+        key = make.key_of(tensors)
+        segs = self._seg_cache.get(key)
+        if segs is None:
+            if len(self._seg_cache) >= 4:
+                self._seg_cache.pop(next(iter(self._seg_cache)))
+            segs = self._seg_cache[key] = make(tensors)
+        return segs
+
+    def _flat_pack(self, grad_in):
+        """reducer.py:512-516: TensorBuffer(grad_in) (+ the local max-norm).
+        Fused: one pass over the tensors writes the flat bucket and the norm.
+        -> (flat TensorBuffer, local norm or None)"""
+        segs = self._segments(grad_in)
+        if segs is None:
+            with self._timer("reduce.flat_pack"):
+                flat = TensorBuffer(grad_in)
+            return flat, None
+        with self._timer("reduce.flat_pack"):
+            buf, norm = self._codec.segments_flatten_absmax(segs)
+        return TensorBuffer.of_flat(grad_in, buf), norm
+
+    def _max_norm(self, flat, local=None, idx=None):
+        with self._timer("reduce.norm", verbosity=2):
+            if local is None or idx is not None:
+                local = self._codec.absmax(flat.buffer, idx=idx)
+            return self._all_reduce(local, dist.ReduceOp.MAX)
 
 
 class TensorBuffer:
@@ -110,6 +156,20 @@ class TensorBuffer:
     def __len__(self):
         return self._len_tensors
 
+    @classmethod
+    def of_flat(cls, tensors, buffer):
+        """A TensorBuffer over an already-flattened bucket (no torch.cat)."""
+        self = cls.__new__(cls)
+        indices = [0]
+        for tensor in tensors:
+            indices.append(indices[-1] + tensor.nelement())
+        self._start_idx = indices[:-1]
+        self._end_idx = indices[1:]
+        self._len_tensors = len(tensors)
+        self._tensor_shapes = [tensor.size() for tensor in tensors]
+        self.buffer = buffer
+        return self
+
     def with_buffer(self, buffer):
         self.buffer = buffer
         return self
@@ -125,20 +185,23 @@ class QSGDMaxNormReducer(Reducer):
     def reduce(self, grad_in, grad_out):
         W = self.n_workers
         comp = self._compressor(C.QSGDMaxNormCompressor, self._quantization_level)
-        with self._timer("reduce.flat_pack"):
-            flat = TensorBuffer(grad_in)
+        flat, local = self._flat_pack(grad_in)
         n = flat.buffer.numel()
-        with self._timer("reduce.norm", verbosity=2):
-            norm = self._norm(flat.buffer)
+        norm = self._max_norm(flat, local)
         with self._timer("reduce.compress", verbosity=2):
             words = comp.encode(norm, flat.buffer, world=W)
         with self._timer("reduce.reduce.vector", verbosity=2):
             self._all_reduce(words)
         bits = self.n_bits(norm) + self.n_bits(words)
+        out_segs = self._segments(grad_out)
         with self._timer("reduce.decompress", verbosity=2):
-            flat.buffer = comp.decode(norm, words, n, world=W, alpha=1.0 / W)
+            if out_segs is not None:  # decode + 1/W straight into grad_out (setgrad fused)
+                comp.decode_segments(norm, words, out_segs, world=W, alpha=1.0 / W)
+            else:
+                flat.buffer = comp.decode(norm, words, n, world=W, alpha=1.0 / W)
         with self._timer("reduce.setgrad", verbosity=2):
-            self._setgrad(flat, grad_out)
+            if out_segs is None:
+                self._setgrad(flat, grad_out)
         return bits
 
 
@@ -165,13 +228,11 @@ class GlobalRandKMaxNormReducer(Reducer):
     def reduce(self, grad_in, grad_out):
         W = self.n_workers
         comp = self._randk_compressor()
-        with self._timer("reduce.flat_pack"):
-            flat = TensorBuffer(grad_in)
+        flat, _ = self._flat_pack(grad_in)
         n = flat.buffer.numel()
         idx = self._next_indices(n).to(flat.buffer.device, non_blocking=True)
         k = idx.numel()
-        with self._timer("reduce.norm", verbosity=2):
-            norm = self._norm(flat.buffer, idx)
+        norm = self._max_norm(flat, idx=idx)
         with self._timer("reduce.compress", verbosity=2):
             words = comp.encode(norm, flat.buffer, world=W, idx=idx)
         with self._timer("reduce.reduce.vector", verbosity=2):
@@ -180,8 +241,7 @@ class GlobalRandKMaxNormReducer(Reducer):
         with self._timer("reduce.decompress", verbosity=2):
             comp.decode(norm, words, k, world=W, alpha=1.0, idx=idx, out=flat.buffer)
         with self._timer("reduce.setgrad", verbosity=2):
-            flat.buffer = flat.buffer * (1.0 / W) if W > 1 else flat.buffer
-            self._setgrad(flat, grad_out)
+            self._setgrad_scaled(flat, grad_out, 1.0 / W)
         return bits
 
 
@@ -199,10 +259,9 @@ class QSGDMaxNormTwoScaleReducer(Reducer):
     def _make(self):
         return self._compressor(self._cls, self._lower_quantization_level, self._higher_quantization_level)
 
-    def _reduce_scales(self, comp, flat, idx, n):
+    def _reduce_scales(self, comp, flat, idx, n, local=None):
         W = self.n_workers
-        with self._timer("reduce.norm", verbosity=2):
-            norm = self._norm(flat.buffer, idx)
+        norm = self._max_norm(flat, local, idx)
         with self._timer("reduce.compress", verbosity=2):
             mask = comp.encode_mask(norm, flat.buffer, world=W, idx=idx)
             self._all_reduce(mask)
@@ -215,14 +274,18 @@ class QSGDMaxNormTwoScaleReducer(Reducer):
     def reduce(self, grad_in, grad_out):
         W = self.n_workers
         comp = self._make()
-        with self._timer("reduce.flat_pack"):
-            flat = TensorBuffer(grad_in)
+        flat, local = self._flat_pack(grad_in)
         n = flat.buffer.numel()
-        norm, mask, words, bits = self._reduce_scales(comp, flat, None, n)
+        norm, mask, words, bits = self._reduce_scales(comp, flat, None, n, local)
+        out_segs = self._segments(grad_out)
         with self._timer("reduce.decompress", verbosity=2):
-            flat.buffer = comp.decode(norm, words, mask, n, world=W, alpha=1.0 / W)
+            if out_segs is not None:  # decode + 1/W straight into grad_out (setgrad fused)
+                comp.decode_segments(norm, words, mask, out_segs, world=W, alpha=1.0 / W)
+            else:
+                flat.buffer = comp.decode(norm, words, mask, n, world=W, alpha=1.0 / W)
         with self._timer("reduce.setgrad", verbosity=2):
-            self._setgrad(flat, grad_out)
+            if out_segs is None:
+                self._setgrad(flat, grad_out)
         return bits
 
 
@@ -243,8 +306,7 @@ class GlobalRandKMaxNormTwoScaleReducer(QSGDMaxNormTwoScaleReducer):
     def reduce(self, grad_in, grad_out):
         W = self.n_workers
         comp = self._make()
-        with self._timer("reduce.flat_pack"):
-            flat = TensorBuffer(grad_in)
+        flat, _ = self._flat_pack(grad_in)
         n = flat.buffer.numel()
         idx = self._next_indices(n).to(flat.buffer.device, non_blocking=True)
         k = idx.numel()
@@ -252,8 +314,7 @@ class GlobalRandKMaxNormTwoScaleReducer(QSGDMaxNormTwoScaleReducer):
         with self._timer("reduce.decompress", verbosity=2):
             comp.decode(norm, words, mask, k, world=W, alpha=1.0, idx=idx, out=flat.buffer)
         with self._timer("reduce.setgrad", verbosity=2):
-            flat.buffer = flat.buffer * (1.0 / W) if W > 1 else flat.buffer
-            self._setgrad(flat, grad_out)
+            self._setgrad_scaled(flat, grad_out, 1.0 / W)
         return bits
 
 

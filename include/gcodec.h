@@ -30,6 +30,10 @@
  *                              consumed by torch.bernoulli (compressors.py:310)
  *   gc_greedy4_pack/_unpack .. extensions/Extension CPU/bitpacking.cpp:5-124 (host, same format)
  *   gc_bytepack8/_unpack8 .... extensions/Extension CPU BP/bytepacking.cpp:6-64 (device)
+ *   gc_segments_* ............ reducer.py:46-68 TensorBuffer (flatten / views) and the setgrad
+ *                              loop reducer.py:543-549 (+ 753-761, 1521-1527, 1705-1711):
+ *                              fused flatten + max-norm, decode straight into the per-parameter
+ *                              gradients, and the scaled scatter of a flat bucket
  */
 #ifndef GCODEC_H
 #define GCODEC_H
@@ -144,6 +148,46 @@ int gc_lane_pack(const void *q, uint32_t q_dtype, const gc_lanes *lanes, uint32_
 /* q[i] = lane - world*offset (the W-way sum) */
 int gc_lane_unpack(const uint32_t *words, const gc_lanes *lanes, int32_t *q, gc_stream_t stream);
 
+/* ---- per-parameter tensors (the reference's TensorBuffer) ------------------
+ * A gc_segments describes `count` contiguous fp32 tensors laid end to end as
+ * one flat bucket of n elements (reducer.py:46-68): flat element e lives at
+ * seg[s].ptr[e - seg[s].start] for the s with seg[s].start <= e < seg[s].end.
+ * The gc_segments struct is host memory; seg/chunk_seg are device arrays the
+ * caller fills once per parameter list (gc_segments_plan builds their host
+ * images) and reuses every step.  chunk_seg[c] = the first segment holding
+ * element c << chunk_shift, so a kernel finds any element's tensor with two
+ * dependent loads (chunk -> record) plus a rare forward walk, no search.
+ * Tensors may be empty and have any 4-byte alignment. */
+typedef struct gc_seg {
+    uint64_t start;    /* first flat element */
+    uint64_t end;      /* one past the last */
+    float *ptr;        /* device base pointer of the tensor (contiguous fp32) */
+    uint64_t reserved; /* 0 (records are 32 bytes) */
+} gc_seg;
+typedef struct gc_segments {
+    uint64_t count;            /* tensors */
+    uint64_t n;                /* total elements = seg[count-1].end */
+    const gc_seg *seg;         /* device, count records; a sentinel is not needed */
+    const uint32_t *chunk_seg; /* device, gc_segments_chunks(n, chunk_shift) entries */
+    uint32_t chunk_shift;      /* 4..30 */
+    uint32_t reserved;         /* 0 */
+} gc_segments;
+uint64_t gc_segments_chunks(uint64_t n, uint32_t chunk_shift);
+/* host: (sizes[count], device ptrs[count]) -> seg[count], chunk_seg[chunk_capacity >=
+ * gc_segments_chunks(n, chunk_shift)] (host buffers to upload); *n_out = total elements */
+int gc_segments_plan(const uint64_t *sizes, float *const *ptrs, uint64_t count, uint32_t chunk_shift,
+                     gc_seg *seg, uint32_t *chunk_seg, uint64_t chunk_capacity, uint64_t *n_out);
+/* flat[e] = tensor element e (flat may be NULL: max-norm only) and *norm = max |x| over all tensors;
+ * workspace as for gc_absmax_f32.  = TensorBuffer(grad_in) + buffer.abs().max() in one pass. */
+int gc_segments_flatten_absmax(const gc_segments *segs, float *flat, float *norm, void *workspace,
+                               gc_stream_t stream);
+/* tensor element e = RN(flat[e] * alpha) + 0.0f — the setgrad loop `out[:] = 0; out.add_(g, alpha)`
+ * (reducer.py:543-549, 755-761); the + 0 maps -0 to +0 exactly as the reference does */
+int gc_segments_scatter(const float *flat, float alpha, const gc_segments *segs, gc_stream_t stream);
+/* gc_qsgd_decode writing each element straight into its tensor (decode + 1/W + setgrad fused) */
+int gc_qsgd_decode_segments(const uint32_t *words, uint64_t n, const float *norm, uint32_t bits,
+                            const gc_lanes *lanes, float alpha, const gc_segments *segs, gc_stream_t stream);
+
 /* ---- multi-scale / two-scale --------------------------------------------- */
 int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, const gc_levels *levels,
                       const gc_rng *rng, const gc_lanes *mask_lanes, uint32_t *mask_words, gc_stream_t stream);
@@ -156,6 +200,10 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
 int gc_ms_decode(const uint32_t *words, const uint32_t *mask_words, const int64_t *idx, uint64_t n,
                  const float *norm, const gc_levels *levels, const gc_lanes *mask_lanes,
                  const gc_lanes *q_lanes, int order, float alpha, float *out, gc_stream_t stream);
+/* gc_ms_decode writing each element straight into its tensor */
+int gc_ms_decode_segments(const uint32_t *words, const uint32_t *mask_words, uint64_t n, const float *norm,
+                          const gc_levels *levels, const gc_lanes *mask_lanes, const gc_lanes *q_lanes, int order,
+                          float alpha, const gc_segments *segs, gc_stream_t stream);
 /* unpacked selected level per element (int8), from a thermometer stream */
 int gc_ms_mask_unpack(const uint32_t *mask_words, const gc_lanes *mask_lanes, uint32_t levels_count,
                       int8_t *mask, gc_stream_t stream);

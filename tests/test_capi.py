@@ -145,3 +145,39 @@ def test_reference_extension_oracle_agrees_with_host_packers():
         assert torch.equal(bitpacking.packing(src), ref_bit.packing(src))
         b = torch.from_numpy(rng.integers(-500, 500, n).astype(np.int32))
         assert torch.equal(bytepacking.packing(b), ref_byte.packing(b))
+
+
+@pytest.mark.parametrize("shift", [4, 7, 12])
+def test_segments_plan(shift):
+    """gc_segments_plan (host): records are the TensorBuffer offsets
+    (reducer.py:51-58) and chunk_seg[c] is the segment holding element c<<shift."""
+    from gcodec import _lib
+    from gcodec.shapes import resnet50_sizes
+
+    lib = _lib.load()
+    for sizes in ([0, 1, 3, 0, 0, 17, 1000, 4, 0], resnet50_sizes(), [5]):
+        count = len(sizes)
+        sz = np.array(sizes, dtype=np.uint64)
+        ptrs = (C.c_void_p * count)(*[0x1000 * (i + 1) for i in range(count)])
+        n = int(sz.sum())
+        chunks = int(lib.gc_segments_chunks(n, shift))
+        assert chunks == (n + (1 << shift) - 1) >> shift
+        seg = np.zeros((count, 4), dtype=np.uint64)
+        cs = np.zeros(max(chunks, 1), dtype=np.uint32)
+        n_out = C.c_uint64(0)
+        rc = lib.gc_segments_plan(sz.ctypes.data_as(C.c_void_p), ptrs, count, shift,
+                                  seg.ctypes.data_as(C.c_void_p), cs.ctypes.data_as(C.c_void_p), chunks,
+                                  C.byref(n_out))
+        assert rc == 0 and n_out.value == n
+        starts = np.concatenate([[0], np.cumsum(sz)]).astype(np.uint64)
+        assert (seg[:, 0] == starts[:-1]).all() and (seg[:, 1] == starts[1:]).all()
+        assert (seg[:, 2] == np.array([0x1000 * (i + 1) for i in range(count)], dtype=np.uint64)).all()
+        first = np.arange(chunks, dtype=np.uint64) << np.uint64(shift)
+        want = np.searchsorted(starts[1:], first, side="right")  # first segment with end > e
+        assert (cs[:chunks] == want).all()
+        # too small a chunk table / bad shift are errors, not crashes
+        if chunks > 1:
+            assert lib.gc_segments_plan(sz.ctypes.data_as(C.c_void_p), ptrs, count, shift,
+                                        seg.ctypes.data_as(C.c_void_p), cs.ctypes.data_as(C.c_void_p),
+                                        chunks - 1, None) == _lib.GC_EINVAL
+    assert lib.gc_segments_chunks(10, 3) == 0
