@@ -255,7 +255,7 @@ int main(int argc, char **argv)
                                (uint64_t)M, ra, words2);
         };
     };
-    {
+    if (getenv("LAB_PLACE")) {
         // placement: do the HBM addresses of the 6 plane read streams and the
         // write stream (relative to each other) change the encode time?
         float *xp;
@@ -313,6 +313,10 @@ int main(int argc, char **argv)
     row("encode NORNG|NODIV g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 16384)), enc_bytes);
     for (int rep = 0; rep < 3; ++rep) {
         row("A/B: encode product (MINW=1) g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, 0>, 2048)), enc_bytes);
+        row("A/B: encode PF g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PF>, 2048)), enc_bytes);
+        row("A/B: encode PF g=1536", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PF>, 1536)), enc_bytes);
+        row("A/B: encode PF g=3072", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PF>, 3072)), enc_bytes);
+        row("A/B: encode PF MINW=4 g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PF, 4>, 2048)), enc_bytes);
         row("A/B: encode planes in pairs", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_GRP2>, 2048)), enc_bytes);
         row("A/B: encode planes in triples", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_GRP3>, 2048)), enc_bytes);
         row("A/B: encode SEQ planes", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_SEQ>, 2048)), enc_bytes);
@@ -394,5 +398,7 @@ int main(int argc, char **argv)
     same("planes in pairs", k_qsgd_encode<6, 0, 0, ENC_GRP2>);
     same("SEQ planes", k_qsgd_encode<6, 0, 0, ENC_SEQ>);
     same("SEQ planes >=8 waves", k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>);
+    same("register prefetch", k_qsgd_encode<6, 0, 0, ENC_PF>);
+    same("register prefetch MINW=4", k_qsgd_encode<6, 0, 0, ENC_PF, 4>);
     return 0;
 }
