@@ -36,8 +36,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def _args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle", type=float, default=0.5,
+                    help="seconds of untimed steps before the W warmup steps: MI355X clocks ramp over ~0.1-0.3 s "
+                         "of sustained load (profiles/r01h_*: 181 us/step after 5 steps, 163 us after 1000)")
     ap.add_argument("--n", type=int, default=100_000_000)
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-oracle sample budget (0 = skip)")
@@ -233,10 +236,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GC_BENCH_BACKEND=gloo: rehearsal of the N>1 control flow on a 1-GPU box
+    # (ranks share the card, collectives go through gloo; not a perf number)
+    backend = os.environ.get("GC_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     n, bits, K, Wm = args.n, args.bits, args.steps, args.warmup
 
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -259,6 +270,19 @@ def main():
         norm_step()
         encode_step()
 
+    # clock settle (untimed), then the W warmup steps
+    settle_steps = 0
+    t_settle = time.perf_counter()
+    while args.settle > 0:
+        for _ in range(20):
+            step()
+        settle_steps += 20
+        torch.cuda.synchronize()
+        done = torch.tensor([float(time.perf_counter() - t_settle >= args.settle)], device=dev)
+        if world > 1:  # every rank runs the same number of steps (each step holds collectives)
+            dist.all_reduce(done, op=dist.ReduceOp.MAX)
+        if done.item() > 0:
+            break
     for _ in range(Wm):
         step()
     torch.cuda.synchronize()
@@ -306,6 +330,8 @@ def main():
                                f"{lanes.bits}-bit lanes x{lanes.per_word}/word",
                    "global_batch": n * world, "parallelism": f"dp{world}",
                    "step": "absmax -> all_reduce(MAX) if N>1 -> quantize+round+pack"},
+        "clock_settle": {"seconds": args.settle, "steps": settle_steps},
+        "collectives": backend if world > 1 else None,
         "pct_hbm_peak_step": 100.0 * step_bytes * K / el / 1e9 / HBM_PEAK_GBS,
         "roofline": {"bound": "hbm", "kernel": "k_qsgd_encode", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -28,6 +28,7 @@ enum : int {
     ENC_GRP2 = 128,     // schedule the planes in pairs (fewer live Philox chains -> fewer VGPRs)
     ENC_GRP3 = 256,     // schedule the planes in triples
     ENC_SEQ = 512,      // one plane at a time: per-plane range check, sched barrier between planes
+    ENC_PF = 1024,      // register prefetch: the next tile's L loads are issued before this tile's math
 };
 
 // lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
@@ -102,6 +103,50 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
     const uint64_t last = (uint64_t)(L - 1) * M;
     const uint64_t full = (MODE == 0 && fast && n >= last + 4 && n < (1ull << 32)) ? (n - last) >> 2 : 0;
     const uint32_t M32 = (uint32_t)M;
+    if constexpr ((ABL & ENC_PF) != 0) {
+        float4 nx[L];
+        if (t < full) {
+#pragma unroll
+            for (int k = 0; k < L; ++k)
+                nx[k] = *reinterpret_cast<const float4 *>(x + (k * M32 + (uint32_t)t * 4u));
+        }
+        for (; t < full; t += stride) {
+            const uint32_t t4 = (uint32_t)t * 4u;
+            float4 xv[L];
+#pragma unroll
+            for (int k = 0; k < L; ++k)
+                xv[k] = nx[k];
+            if (t + stride < full) {
+                const uint32_t n4 = (uint32_t)(t + stride) * 4u;
+#pragma unroll
+                for (int k = 0; k < L; ++k)
+                    nx[k] = *reinterpret_cast<const float4 *>(x + (k * M32 + n4));
+            }
+            float4 q[L];
+            Range rg;
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                q[k] = quot4_fast<ABL>(xv[k], dv);
+                rg.add4(xv[k]);
+            }
+            if (__builtin_expect(rg.slow(dv), 0)) {
+#pragma unroll
+                for (int k = 0; k < L; ++k)
+                    q[k] = quot4_ieee(xv[k], norm);
+            }
+            uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const uint4 r = draws4_abl<KIND, ABL>(rng, 0, k * M32 + t4);
+                const uint32_t sh = (uint32_t)k * w;
+                acc.x |= enc_lane<ABL>(xv[k].x, q[k].x, s, qmax, r.x) << sh;
+                acc.y |= enc_lane<ABL>(xv[k].y, q[k].y, s, qmax, r.y) << sh;
+                acc.z |= enc_lane<ABL>(xv[k].z, q[k].z, s, qmax, r.z) << sh;
+                acc.w |= enc_lane<ABL>(xv[k].w, q[k].w, s, qmax, r.w) << sh;
+            }
+            *reinterpret_cast<uint4 *>(words + t4) = acc;
+        }
+    }
     for (; t < full; t += stride) {
         const uint32_t t4 = (uint32_t)((ABL & ENC_REV) ? (full - 1 - t) : t) * 4u;
         float4 xv[L];

@@ -117,6 +117,10 @@ SIGNATURES = {
     "gc_mt19937_generate": (C.c_int, [P, P, u64, P]),
     "gc_greedy4_pack": (i64, [P, u64, P, u64]),
     "gc_greedy4_unpack": (i64, [P, u64, P, u64]),
+    "gc_greedy4_workspace_size": (C.c_size_t, [u64]),
+    "gc_greedy4_pack_device": (C.c_int, [P, u64, P, u64, P, P, P, P]),
+    "gc_greedy4_unpack_workspace_size": (C.c_size_t, [u64]),
+    "gc_greedy4_unpack_device": (C.c_int, [P, u64, P, u64, P, P, P, P]),
     "gc_bytepack8": (C.c_int, [P, u32, u64, P, P]),
     "gc_byteunpack8": (C.c_int, [P, u64, P, P]),
     "gc_bytepack8_host": (C.c_int, [P, u64, P]),

@@ -454,19 +454,59 @@ def byteunpack8(words: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _g4_result(res: torch.Tensor, what: str) -> int:
+    """(count, status) written by the device packer: one 16-byte D2H read."""
+    count, status = (int(v) for v in res.cpu().tolist())
+    if status & 1:
+        raise _lib.GCodecError(_lib.GC_ERANGE, f"{what}: a value outside [0, 255] (the greedy format's domain)")
+    if status & 2:
+        raise _lib.GCodecError(_lib.GC_ENOSPC, f"{what}: output capacity too small")
+    return count
+
+
 def greedy4_pack(src: torch.Tensor) -> torch.Tensor:
-    """Host implementation of the reference's sequential greedy format
-    (extensions/Extension CPU/bitpacking.cpp); device tensors are staged."""
-    a = np.ascontiguousarray(src.detach().cpu().numpy().astype(np.int32, copy=False)).reshape(-1)
+    """The reference's greedy 4-mode format (extensions/Extension CPU/bitpacking.cpp:5-124).
+    Device tensors: HIP list-ranking packer (gc_greedy4_pack_device); host
+    tensors: the host packer, like the reference's CPU extension."""
+    lib = _lib.load()
+    if src.is_cuda:
+        dev = _dev(src)
+        a = src.detach().contiguous().view(-1)
+        if a.dtype != torch.int32:
+            a = a.to(torch.int32)
+        n = a.numel()
+        cap = n // 3 + 2
+        out = torch.empty(cap, dtype=torch.int32, device=dev)
+        ws = torch.empty(int(lib.gc_greedy4_workspace_size(n)), dtype=torch.uint8, device=dev)
+        res = torch.zeros(2, dtype=torch.int64, device=dev)
+        check(lib.gc_greedy4_pack_device(_p(a), n, _p(out), cap, _p(res), C.c_void_p(res.data_ptr() + 8), _p(ws),
+                                         _stream(dev)), "gc_greedy4_pack_device")
+        return out[:_g4_result(res, "greedy4_pack")]
+    a = np.ascontiguousarray(src.detach().numpy().astype(np.int32, copy=False)).reshape(-1)
     out = np.empty(a.size + 1, dtype=np.int32)
-    nw = check(_lib.load().gc_greedy4_pack(a.ctypes.data_as(C.c_void_p), a.size, out.ctypes.data_as(C.c_void_p),
-                                           out.size), "gc_greedy4_pack")
-    return torch.from_numpy(out[:nw].copy()).to(src.device)
+    nw = check(lib.gc_greedy4_pack(a.ctypes.data_as(C.c_void_p), a.size, out.ctypes.data_as(C.c_void_p),
+                                   out.size), "gc_greedy4_pack")
+    return torch.from_numpy(out[:nw].copy())
 
 
 def greedy4_unpack(words: torch.Tensor) -> torch.Tensor:
-    a = np.ascontiguousarray(words.detach().cpu().numpy().astype(np.int32, copy=False)).reshape(-1)
+    """Inverse of greedy4_pack; emits whole words (callers truncate, compressors.py:371)."""
+    lib = _lib.load()
+    if words.is_cuda:
+        dev = _dev(words)
+        a = words.detach().contiguous().view(-1)
+        if a.dtype != torch.int32:
+            a = a.to(torch.int32)
+        nw = a.numel()
+        cap = 15 * nw
+        out = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+        ws = torch.empty(int(lib.gc_greedy4_unpack_workspace_size(nw)), dtype=torch.uint8, device=dev)
+        res = torch.zeros(2, dtype=torch.int64, device=dev)
+        check(lib.gc_greedy4_unpack_device(_p(a), nw, _p(out), cap, _p(res), C.c_void_p(res.data_ptr() + 8), _p(ws),
+                                           _stream(dev)), "gc_greedy4_unpack_device")
+        return out[:_g4_result(res, "greedy4_unpack")]
+    a = np.ascontiguousarray(words.detach().numpy().astype(np.int32, copy=False)).reshape(-1)
     out = np.empty(15 * a.size + 1, dtype=np.int32)
-    cnt = check(_lib.load().gc_greedy4_unpack(a.ctypes.data_as(C.c_void_p), a.size, out.ctypes.data_as(C.c_void_p),
-                                              out.size), "gc_greedy4_unpack")
-    return torch.from_numpy(out[:cnt].copy()).to(words.device)
+    cnt = check(lib.gc_greedy4_unpack(a.ctypes.data_as(C.c_void_p), a.size, out.ctypes.data_as(C.c_void_p),
+                                      out.size), "gc_greedy4_unpack")
+    return torch.from_numpy(out[:cnt].copy())

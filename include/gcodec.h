@@ -29,6 +29,8 @@
  *   gc_mt19937_seed/_generate  seed.py:6-11 torch.manual_seed + torch CPU generator stream
  *                              consumed by torch.bernoulli (compressors.py:310)
  *   gc_greedy4_pack/_unpack .. extensions/Extension CPU/bitpacking.cpp:5-124 (host, same format)
+ *   gc_greedy4_*_device ...... the same format on the device (Extension GPU/gpu_bitpacking.cpp:5-125
+ *                              is host code despite its name; this is the GPU drop-in)
  *   gc_bytepack8/_unpack8 .... extensions/Extension CPU BP/bytepacking.cpp:6-64 (device)
  *   gc_segments_* ............ reducer.py:46-68 TensorBuffer (flatten / views) and the setgrad
  *                              loop reducer.py:543-549 (+ 753-761, 1521-1527, 1705-1711):
@@ -147,6 +149,22 @@ int gc_qsgd_dequantize(const void *q, uint32_t q_dtype, uint64_t n, const float 
 int gc_lane_pack(const void *q, uint32_t q_dtype, const gc_lanes *lanes, uint32_t *words, gc_stream_t stream);
 /* q[i] = lane - world*offset (the W-way sum) */
 int gc_lane_unpack(const uint32_t *words, const gc_lanes *lanes, int32_t *q, gc_stream_t stream);
+
+/* ---- greedy 4-mode packer on the device --------------------------------------
+ * The format of gc_greedy4_pack (Extension CPU/bitpacking.cpp:5-124) produced by
+ * a parallel list ranking (chunk transition tables + pointer doubling in LDS).
+ * Results are asynchronous: *nwords / *count (device uint64) receive the
+ * number of words / values, *status (device uint32) 0 or a bit set: 1 = a
+ * value outside [0, 255] (nothing written), 2 = more than cap outputs
+ * (nothing written).  workspace: gc_greedy4[_unpack]_workspace_size bytes,
+ * device, no initialisation needed.  unpack emits whole words (the caller
+ * truncates, as compressors.py:371 does). */
+size_t gc_greedy4_workspace_size(uint64_t n);
+int gc_greedy4_pack_device(const int32_t *src, uint64_t n, int32_t *out, uint64_t cap, uint64_t *nwords,
+                           uint32_t *status, void *workspace, gc_stream_t stream);
+size_t gc_greedy4_unpack_workspace_size(uint64_t nwords);
+int gc_greedy4_unpack_device(const int32_t *words, uint64_t nwords, int32_t *out, uint64_t cap, uint64_t *count,
+                             uint32_t *status, void *workspace, gc_stream_t stream);
 
 /* ---- per-parameter tensors (the reference's TensorBuffer) ------------------
  * A gc_segments describes `count` contiguous fp32 tensors laid end to end as

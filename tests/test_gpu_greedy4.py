@@ -1,0 +1,72 @@
+"""Device greedy 4-mode packer (gc_greedy4_*_device) — the reference's
+bitpacking format (extensions/Extension CPU/bitpacking.cpp:5-124), produced
+by parallel list ranking.  Bit-exact against the reference extension's own
+known-answer vectors (tests/golden/packers.npz) and against the oracle /
+host packer on inputs that stress the chunk boundaries (2048-element chunks,
+256-chunk groups): all-mode-0 runs, all-mode-3 runs, mixes, ragged ends."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # collected on CPU, skipped there
+    pytest.skip("no GPU", allow_module_level=True)
+
+import gcodec  # noqa: E402
+from gcodec import codec  # noqa: E402
+from gcodec.packing import gpu_bitpacking  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_device_packer_matches_reference_vectors():
+    z = np.load(os.path.join(GOLD, "packers.npz"), allow_pickle=False)
+    names = sorted({k.split("/")[1] for k in z.files if k.startswith("g4/")})
+    assert names
+    for nm in names:
+        src = z[f"g4/{nm}/src"]
+        w = codec.greedy4_pack(torch.from_numpy(src.astype(np.int32)).to(DEV))
+        assert w.is_cuda
+        assert np.array_equal(w.cpu().numpy(), z[f"g4/{nm}/packed"].astype(np.int32)), nm
+        u = codec.greedy4_unpack(w)
+        assert np.array_equal(u.cpu().numpy(), z[f"g4/{nm}/unpacked"].astype(np.int32)), nm
+
+
+def _inputs():
+    rng = np.random.default_rng(4)
+    yield "empty", np.zeros(0, np.int32)
+    yield "one", np.array([200], np.int32)
+    for n in (2047, 2048, 2049, 2048 * 256 - 1, 2048 * 256 + 5, 1_000_003):
+        yield f"mix{n}", rng.choice([0, 1, 3, 9, 15, 100, 255], n, p=[.3, .2, .15, .15, .1, .05, .05]).astype(np.int32)
+    yield "zeros", np.zeros(2048 * 300 + 17, np.int32)
+    yield "max", np.full(2048 * 3 + 1, 255, np.int32)
+    # runs that flip modes right at chunk boundaries
+    a = np.zeros(2048 * 8, np.int32)
+    for c in range(1, 8):
+        a[2048 * c - 7:2048 * c + 3] = 200
+    yield "edges", a
+    yield "qsgd4", np.abs(rng.normal(0, 4, 3_000_000)).clip(0, 15).astype(np.int32)
+
+
+@pytest.mark.parametrize("name,src", list(_inputs()), ids=lambda v: v if isinstance(v, str) else "")
+def test_device_packer_matches_host(name, src):
+    want = O.greedy4_pack(src) if src.size <= 200_000 else None
+    host = codec.greedy4_pack(torch.from_numpy(src))  # host packer (pinned to the oracle in test_capi)
+    if want is not None:
+        assert np.array_equal(host.numpy(), want)
+    w = gpu_bitpacking.packing(torch.from_numpy(src).to(DEV))
+    assert np.array_equal(w.cpu().numpy(), host.numpy()), name
+    u = gpu_bitpacking.unpacking(w)
+    assert np.array_equal(u.cpu().numpy()[:src.size], src)
+    assert np.array_equal(u.cpu().numpy(), codec.greedy4_unpack(host).numpy())
+
+
+def test_device_packer_rejects_out_of_domain():
+    for bad in ([1, 2, 256], [-1, 3]):
+        with pytest.raises(gcodec.GCodecError):
+            codec.greedy4_pack(torch.tensor(bad, dtype=torch.int32, device=DEV))

@@ -373,6 +373,18 @@ int main(int argc, char **argv)
     row("encode ABL=NORNG|NODIV g=2048",
         T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 2048)), enc_bytes);
 
+    // the same product rows again, late in the process (clock / power ramp check)
+    row("late: product gc_qsgd_encode", T.run([&] { gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr); }),
+        enc_bytes);
+    row("late: product absmax + encode (one step)", T.run([&] {
+            gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
+            gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr);
+        }), 8.0 * n + 4.0 * M);
+    row("late: product absmax + encode x200", T.run([&] {
+            gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
+            gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr);
+        }, 200), 8.0 * n + 4.0 * M);
+
     // the lab's ABL=0 instantiation must equal the product's words
     hipLaunchKernelGGL((k_qsgd_encode<6, 0, 0, 0>), dim3(2048), dim3(256), 0, 0, x, (const int64_t *)nullptr, n, norm,
                        s, qmax, ln.bits, (uint64_t)M, ra, words2);
