@@ -1,0 +1,164 @@
+// absmax.h — the max-norm scan (reducer.py:516 buffer.abs().max()) shared by
+// qsgd.hip (product), segments.hip (fused flatten) and tools/encode_lab.hip.
+//
+// uint max over |x| bit patterns (exact, order-free, NaN wins like
+// torch.max), wave64 shuffle tree, wave partials in LDS, one partial per
+// block.  Without a workspace: one atomicMax per block into *norm (zeroed by
+// a preceding hipMemsetAsync).  With a workspace: no memset launch — every
+// block stores its partial (sc1) and takes a ticket (agent-scope atomic add);
+// the block that draws the last ticket reduces the partials (sc1 loads),
+// writes *norm and re-arms the ticket.  Fence-free: a per-block release fence
+// (buffer_wbl2) measured 2x slower than the memset it removes.
+// Same-address atomics serialise (~88/us, MI355X_MICROARCH.md 'dequeue'), so
+// grids above 256 blocks take a two-level ticket: one per 64-block group,
+// then one for the group winners.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gc_device.h"
+
+namespace gc {
+
+constexpr unsigned kAbsmaxThreads = 1024;  // product block size
+constexpr unsigned kAbsmaxMaxBlocks = 4096;
+constexpr unsigned kAbsmaxGroup = 64;      // blocks per first-level ticket
+// workspace (uint32 words): [0] ticket, [16 (1 + g)] group tickets (own lines),
+// [kWsGpart + g] group partials, [kWsPart + b] block partials
+constexpr unsigned kWsGpart = 16 * (1 + kAbsmaxMaxBlocks / kAbsmaxGroup);
+constexpr unsigned kWsPart = kWsGpart + kAbsmaxMaxBlocks / kAbsmaxGroup;
+constexpr unsigned kAbsmaxWsWords = kWsPart + kAbsmaxMaxBlocks;
+
+__device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
+
+__device__ __forceinline__ uint32_t absbits4(float4 a)
+{
+    return max(max(absbits(a.x), absbits(a.y)), max(absbits(a.z), absbits(a.w)));
+}
+
+__device__ __forceinline__ void sc1_store(uint32_t *p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t sc1_load(const uint32_t *p)
+{
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// block max of m (valid in thread 0)
+template <unsigned BT>
+__device__ __forceinline__ uint32_t block_max(uint32_t m, uint32_t *part)
+{
+    m = wave_max_u32(m);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+        part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (unsigned w = 1; w < BT / 64; ++w)
+            m = max(m, part[w]);
+    return m;
+}
+
+// max over `count` sc1 partials by the whole block (valid in thread 0)
+template <unsigned BT>
+__device__ __forceinline__ uint32_t block_max_sc1(const uint32_t *p, uint32_t count, uint32_t *part)
+{
+    uint32_t v = 0;
+    for (uint32_t i = threadIdx.x; i < count; i += BT)
+        v = max(v, sc1_load(&p[i]));
+    return block_max<BT>(v, part);
+}
+
+template <bool WS, unsigned BT = kAbsmaxThreads>
+__device__ __forceinline__ void absmax_finish(uint32_t m, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)
+{
+    __shared__ uint32_t part[BT / 64];
+    __shared__ int last;
+    m = block_max<BT>(m, part);
+    if constexpr (!WS) {
+        if (threadIdx.x == 0 && m)
+            atomicMax(out, m);
+        return;
+    } else {
+        const uint32_t nb = gridDim.x;
+        const bool two = nb > 256;
+        if (threadIdx.x == 0) {
+            // sc1 store, drained, then the agent-scope ticket: the fence-free
+            // hand-off of MI355X_MICROARCH.md (row 1 of the sc1 table)
+            sc1_store(&ws[kWsPart + blockIdx.x], m);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (two) {
+                const uint32_t g = blockIdx.x / kAbsmaxGroup;
+                const uint32_t gsize = min(kAbsmaxGroup, nb - g * kAbsmaxGroup);
+                last = __hip_atomic_fetch_add(&ws[16 * (1 + g)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       gsize - 1;
+            } else {
+                last = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+            }
+        }
+        __syncthreads();  // the other waves load only after the last add returned
+        if (!last)
+            return;
+        if (two) {  // this block closes its group
+            const uint32_t g = blockIdx.x / kAbsmaxGroup;
+            const uint32_t gsize = min(kAbsmaxGroup, nb - g * kAbsmaxGroup);
+            const uint32_t ng = (nb + kAbsmaxGroup - 1) / kAbsmaxGroup;
+            const uint32_t gm = block_max_sc1<BT>(&ws[kWsPart + g * kAbsmaxGroup], gsize, part);
+            if (threadIdx.x == 0) {
+                sc1_store(&ws[kWsGpart + g], gm);
+                sc1_store(&ws[16 * (1 + g)], 0u);  // re-arm the group ticket
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                last = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+            }
+            __syncthreads();
+            if (!last)
+                return;
+            const uint32_t r = block_max_sc1<BT>(&ws[kWsGpart], ng, part);
+            if (threadIdx.x == 0) {
+                *out = r;
+                sc1_store(&ws[0], 0u);
+            }
+        } else {
+            const uint32_t r = block_max_sc1<BT>(&ws[kWsPart], nb, part);
+            if (threadIdx.x == 0) {
+                *out = r;
+                sc1_store(&ws[0], 0u);
+            }
+        }
+    }
+}
+
+// MODE 0: float4 dense, 1: scalar dense, 2: gather.  U float4 loads in flight per thread.
+template <int MODE, bool WS, unsigned BT = kAbsmaxThreads, int U = 4>
+__global__ __launch_bounds__(BT) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
+                                               uint64_t n, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)
+{
+    uint32_t m = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * BT;
+    uint64_t t = (uint64_t)blockIdx.x * BT + threadIdx.x;
+    if constexpr (MODE == 0) {
+        const float4 *x4 = reinterpret_cast<const float4 *>(x);
+        const uint64_t n4 = n >> 2;
+        for (; t + (U - 1) * stride < n4; t += U * stride) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                v[u] = x4[t + u * stride];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                m = max(m, absbits4(v[u]));
+        }
+        for (; t < n4; t += stride)
+            m = max(m, absbits4(x4[t]));
+        if (blockIdx.x == 0 && threadIdx.x < (n & 3))
+            m = max(m, absbits(x[(n4 << 2) + threadIdx.x]));
+    } else {
+        for (; t < n; t += stride)
+            m = max(m, absbits(MODE == 2 ? x[idx[t]] : x[t]));
+    }
+    absmax_finish<WS, BT>(m, out, ws);
+}
+
+}  // namespace gc

@@ -162,7 +162,8 @@ __device__ __forceinline__ int32_t q_signed(float x, float norm, float s, uint32
 // compiler's full division.
 struct DivNorm {
     float norm;
-    float r;
+    float r;       // 1/norm refined by one Newton step (the compiler's div sequence)
+    float rr;      // RN(1/norm), IEEE division (Markstein's one-correction quotient)
     uint32_t lo1;  // bits(thr_lo) - 1: |x| in (0, thr_lo) takes the full division
     uint32_t hi;   // bits(thr_hi): |x| above (and inf / NaN) takes the full division
     bool fast;     // uniform: norm in [2^-100, 2^100]
@@ -176,6 +177,7 @@ __device__ __forceinline__ DivNorm make_div(float norm)
     float r = __builtin_amdgcn_rcpf(norm);
     const float e = fmaf(-norm, r, 1.0f);
     d.r = fmaf(e, r, r);
+    d.rr = 1.0f / norm;  // correctly rounded (-fhip-fp32-correctly-rounded-divide-sqrt)
     // thr_lo keeps |x| >= 2^-100 (no numerator scaling) and |x|/norm >= 2^-120
     // (normal quotient); thr_hi keeps |x|/norm <= 2^64 (no overflow scaling)
     d.lo1 = __float_as_uint(fmaxf(0x1p-100f, norm * 0x1p-120f)) - 1u;
@@ -183,13 +185,29 @@ __device__ __forceinline__ DivNorm make_div(float norm)
     return d;
 }
 
-__device__ __forceinline__ float div_fast(float a, const DivNorm &d)
+// the compiler's IEEE sequence with div_scale / div_fixup as identities:
+// two Newton corrections on a refined reciprocal (kept for the lab A/B)
+__device__ __forceinline__ float div_fast2(float a, const DivNorm &d)
 {
     float q = a * d.r;
     float e = fmaf(-d.norm, q, a);
     q = fmaf(e, d.r, q);
     e = fmaf(-d.norm, q, a);
     return fmaf(e, d.r, q);
+}
+
+// Markstein (IBM J. Res. Dev. 34(1), 1990; Muller et al., Handbook of FP
+// arithmetic, Thm. 4.13): with y = RN(1/b) and q = RN(a*y) within one ulp
+// of a/b, e = a - b*q is exact (fma) and RN(q + e*y) = RN(a/b) — provided
+// nothing over/underflows, which the same Range check as div_fast guarantees.
+// One multiply + two fma instead of div_fast2's one + four; checked bit for
+// bit against IEEE division on 3.4e10 random in-range pairs (tools/encode_lab
+// divcheck, profiles/r01k_encode_lab.log).
+__device__ __forceinline__ float div_fast(float a, const DivNorm &d)
+{
+    const float q = a * d.rr;
+    const float e = fmaf(-d.norm, q, a);
+    return fmaf(e, d.rr, q);
 }
 
 // running range of |x| bit patterns for the fast-division check:

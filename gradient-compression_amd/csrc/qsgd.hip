@@ -15,56 +15,17 @@
 #include "gc_device.h"
 #include "gc_host.h"
 #include "qsgd_encode.h"
+#include "absmax.h"
 #include "segments.h"
 
 #include <algorithm>
 
 namespace gc {
 
-// ---------------------------------------------------------------------------
-// max-norm: uint max over |x| bit patterns (exact, order-free, NaN wins like
-// torch.max), wave64 shuffle tree, 4 wave partials in LDS, one atomic/block.
-// ---------------------------------------------------------------------------
-// Without a workspace: one atomicMax per block into *norm (zeroed by a
-// preceding hipMemsetAsync).  With a workspace: no memset launch — every block
-// stores its partial (sc1) and takes a ticket (agent-scope atomic add); the
-// block that draws the last ticket reduces the partials (sc1 loads), writes
-// *norm and re-arms the ticket for the next call.  Fence-free: a per-block
-// release fence (buffer_wbl2) measured 2x slower than the memset it removes.
-// One 1024-thread block per CU: 16 waves x 4 float4 loads in flight = 64 KB
-// per CU (HBM-saturating), and at most 256 same-address atomics (one word
-// takes ~88 atomics/us, MI355X_MICROARCH.md 'dequeue': 2048 blocks cost ~20 us).
-// (kAbsmaxThreads, kAbsmaxMaxBlocks, absmax_finish: segments.h)
+// max-norm: k_absmax (absmax.h).  Product grid: kAbsmaxGrid blocks of
+// kAbsmaxThreads (one per CU: 16 waves x 4 float4 loads in flight = 64 KB per CU).
+constexpr unsigned kAbsmaxGrid = 256;
 
-template <int MODE, bool WS>  // MODE 0: float4 dense, 1: scalar dense, 2: gather
-__global__ __launch_bounds__(kAbsmaxThreads) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
-                                                   uint64_t n, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)
-{
-    uint32_t m = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * kAbsmaxThreads;
-    uint64_t t = (uint64_t)blockIdx.x * kAbsmaxThreads + threadIdx.x;
-    if constexpr (MODE == 0) {
-        const float4 *x4 = reinterpret_cast<const float4 *>(x);
-        const uint64_t n4 = n >> 2;
-        for (; t + 3 * stride < n4; t += 4 * stride) {
-            const float4 a = x4[t], b = x4[t + stride], c = x4[t + 2 * stride], d = x4[t + 3 * stride];
-            m = max(m, max(max(absbits(a.x), absbits(a.y)), max(absbits(a.z), absbits(a.w))));
-            m = max(m, max(max(absbits(b.x), absbits(b.y)), max(absbits(b.z), absbits(b.w))));
-            m = max(m, max(max(absbits(c.x), absbits(c.y)), max(absbits(c.z), absbits(c.w))));
-            m = max(m, max(max(absbits(d.x), absbits(d.y)), max(absbits(d.z), absbits(d.w))));
-        }
-        for (; t < n4; t += stride) {
-            const float4 a = x4[t];
-            m = max(m, max(max(absbits(a.x), absbits(a.y)), max(absbits(a.z), absbits(a.w))));
-        }
-        if (blockIdx.x == 0 && threadIdx.x < (n & 3))
-            m = max(m, absbits(x[(n4 << 2) + threadIdx.x]));
-    } else {
-        for (; t < n; t += stride)
-            m = max(m, absbits(MODE == 2 ? x[idx[t]] : x[t]));
-    }
-    absmax_finish<WS>(m, out, ws);
-}
 
 // ---------------------------------------------------------------------------
 // encode: see qsgd_encode.h (lane(k) of word j = qmax + q(x[kM + j]))
@@ -268,7 +229,7 @@ using namespace gc;
 
 extern "C" {
 
-size_t gc_absmax_workspace_size(void) { return 64 + 4 * kAbsmaxMaxBlocks; }
+size_t gc_absmax_workspace_size(void) { return 4 * kAbsmaxWsWords; }
 
 int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, void *workspace, gc_stream_t stream)
 {
@@ -286,7 +247,7 @@ int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, v
     const int mode = idx ? 2 : (aligned16(x) ? 0 : 1);
     const uint64_t items = mode == 0 ? (n >> 2) : n;
     const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((items + kAbsmaxThreads - 1) / kAbsmaxThreads, 1),
-                                                       kAbsmaxMaxBlocks);
+                                                       kAbsmaxGrid);
 #define GC_AM(MODE_, WS_) \
     hipLaunchKernelGGL((k_absmax<MODE_, WS_>), dim3(grid), dim3(kAbsmaxThreads), 0, st, x, idx, n, o, ws)
     if (ws) {

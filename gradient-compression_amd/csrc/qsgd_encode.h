@@ -29,6 +29,8 @@ enum : int {
     ENC_GRP3 = 256,     // schedule the planes in triples
     ENC_SEQ = 512,      // one plane at a time: per-plane range check, sched barrier between planes
     ENC_PF = 1024,      // register prefetch: the next tile's L loads are issued before this tile's math
+    ENC_DIV2 = 2048,    // the compiler's two-correction quotient (div_fast2) instead of Markstein's
+    ENC_NT = 4096,      // nontemporal loads of x
 };
 
 // lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
@@ -58,6 +60,11 @@ __device__ __forceinline__ float4 quot4_fast(const float4 &v, const DivNorm &d)
         q.y = fabsf(v.y) * d.r;
         q.z = fabsf(v.z) * d.r;
         q.w = fabsf(v.w) * d.r;
+    } else if constexpr ((ABL & ENC_DIV2) != 0) {
+        q.x = div_fast2(fabsf(v.x), d);
+        q.y = div_fast2(fabsf(v.y), d);
+        q.z = div_fast2(fabsf(v.z), d);
+        q.w = div_fast2(fabsf(v.w), d);
     } else {
         q.x = div_fast(fabsf(v.x), d);
         q.y = div_fast(fabsf(v.y), d);
@@ -151,9 +158,17 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
         const uint32_t t4 = (uint32_t)((ABL & ENC_REV) ? (full - 1 - t) : t) * 4u;
         float4 xv[L];
 #pragma unroll
-        for (int k = 0; k < L; ++k)
-            xv[k] = *reinterpret_cast<const float4 *>(x + ((ABL & ENC_ABL_L2) ? ((k * M32 + t4) & 4095u)
-                                                                                : (k * M32 + t4)));
+        for (int k = 0; k < L; ++k) {
+            const float4 *p = reinterpret_cast<const float4 *>(x + ((ABL & ENC_ABL_L2) ? ((k * M32 + t4) & 4095u)
+                                                                                      : (k * M32 + t4)));
+            if constexpr ((ABL & ENC_NT) != 0) {
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+                xv[k] = make_float4(r.x, r.y, r.z, r.w);
+            } else {
+                xv[k] = *p;
+            }
+        }
         if constexpr ((ABL & ENC_SEQ) != 0) {
             uint4 acc = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll

@@ -12,9 +12,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <functional>
 #include <vector>
 
 #include "gcodec.h"
+#include "absmax.h"
 #include "qsgd_encode.h"
 
 using namespace gc;
@@ -150,6 +153,54 @@ __global__ __launch_bounds__(1024) void k_absmax_rev(const float4 *x, uint64_t n
         atomicMax(out, m);
 }
 
+// Markstein one-correction quotient vs the IEEE division, on random operand
+// pairs inside the fast-path range (same make_div / Range as the kernel)
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_divcheck(uint64_t seed, uint64_t count, int allones,
+                                                  unsigned long long *stats, uint32_t *example)
+{
+    unsigned long long tested = 0, bad1 = 0, bad2 = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < count; i += gridDim.x * 256ull) {
+        const uint64_t h = mix64(seed * 0x100000000ull + i);
+        const int eb = (int)(h % 201) - 100;                   // norm exponent in [-100, 100]
+        const int eq = (int)((h >> 8) % 186) - 121;            // quotient exponent in [-121, 64]
+        const uint32_t mb = allones ? 0x7fffffu : (uint32_t)(h >> 16) & 0x7fffffu;
+        const uint32_t ma = (uint32_t)(h >> 40) & 0x7fffffu;
+        int ea = eb + eq;
+        if (ea < -126 || ea > 127)
+            continue;
+        const float b = __uint_as_float((uint32_t)(127 + eb) << 23 | mb);
+        const float a = __uint_as_float((uint32_t)(127 + ea) << 23 | ma);
+        const gc::DivNorm d = gc::make_div(b);
+        gc::Range rg;
+        rg.add4(make_float4(a, a, a, a));
+        if (!d.fast || rg.slow(d))
+            continue;
+        ++tested;
+        const float ref = a / b;
+        const float q1 = gc::div_fast(a, d), q2 = gc::div_fast2(a, d);
+        if (__float_as_uint(q1) != __float_as_uint(ref)) {
+            ++bad1;
+            example[0] = __float_as_uint(a);
+            example[1] = __float_as_uint(b);
+        }
+        if (__float_as_uint(q2) != __float_as_uint(ref))
+            ++bad2;
+    }
+    atomicAdd(&stats[0], tested);
+    if (bad1)
+        atomicAdd(&stats[1], bad1);
+    if (bad2)
+        atomicAdd(&stats[2], bad2);
+}
+
 struct Timer {
     hipEvent_t a, b;
     Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
@@ -236,6 +287,35 @@ int main(int argc, char **argv)
     CK(hipMemset(ws, 0, gc_absmax_workspace_size()));
     row("product gc_absmax_f32 (workspace, 1 launch)", T.run([&] { gc_absmax_f32(x, nullptr, n, norm, ws, nullptr); }),
         rd_bytes);
+    {
+        // max-norm grid / loads-in-flight sweep (two-level ticket above 256 blocks)
+        uint32_t ref = 0, got = 0;
+        CK(hipMemcpy(&ref, norm, 4, hipMemcpyDeviceToHost));
+        float *nm2;
+        CK(hipMalloc(&nm2, 64));
+        auto am = [&](const char *nm, auto kern, unsigned grid, unsigned bt) {
+            row(nm, T.run([&] {
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(bt), 0, 0, x, (const int64_t *)nullptr, n,
+                                       (uint32_t *)nm2, (uint32_t *)ws);
+                }), rd_bytes);
+            CK(hipMemcpy(&got, nm2, 4, hipMemcpyDeviceToHost));
+            if (got != ref)
+                printf("   ^ WRONG NORM %08x vs %08x\n", got, ref);
+        };
+        for (int rep = 0; rep < 2; ++rep) {
+            am("absmax 256x1024 U4 (product)", k_absmax<0, true, 1024, 4>, 256, 1024);
+            am("absmax 256x1024 U8", k_absmax<0, true, 1024, 8>, 256, 1024);
+            am("absmax 512x1024 U4 (2-level)", k_absmax<0, true, 1024, 4>, 512, 1024);
+            am("absmax 512x1024 U2 (2-level)", k_absmax<0, true, 1024, 2>, 512, 1024);
+            am("absmax 512x512 U4 (2-level)", k_absmax<0, true, 512, 4>, 512, 512);
+            am("absmax 1024x512 U4 (2-level)", k_absmax<0, true, 512, 4>, 1024, 512);
+            am("absmax 1024x256 U4 (2-level)", k_absmax<0, true, 256, 4>, 1024, 256);
+            am("absmax 2048x256 U2 (2-level)", k_absmax<0, true, 256, 2>, 2048, 256);
+            am("absmax 2048x256 U1 (2-level)", k_absmax<0, true, 256, 1>, 2048, 256);
+            am("absmax 4096x256 U1 (2-level)", k_absmax<0, true, 256, 1>, 4096, 256);
+        }
+        CK(hipFree(nm2));
+    }
     gc_rng rng = {GC_RNG_PHILOX, 0, 42, 0, nullptr};
     row("product gc_qsgd_encode", T.run([&] { gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr); }),
         enc_bytes);
@@ -385,6 +465,79 @@ int main(int argc, char **argv)
             gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr);
         }, 200), 8.0 * n + 4.0 * M);
 
+    {
+        unsigned long long *st;
+        uint32_t *ex;
+        CK(hipMalloc(&st, 32));
+        CK(hipMalloc(&ex, 16));
+        for (int allones = 0; allones < 2; ++allones) {
+            CK(hipMemset(st, 0, 32));
+            const uint64_t cnt = allones ? 4000000000ull : 40000000000ull;
+            hipLaunchKernelGGL(k_divcheck, dim3(8192), dim3(256), 0, 0, 7ull + allones, cnt, allones, st, ex);
+            unsigned long long h[3];
+            uint32_t e[2];
+            CK(hipMemcpy(h, st, 24, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(e, ex, 8, hipMemcpyDeviceToHost));
+            printf("divcheck%s: %llu pairs in range, Markstein mismatches %llu (e.g. a=%08x b=%08x), 2-step mismatches %llu\n",
+                   allones ? " (norm significand all ones)" : "", h[0], h[1], h[1] ? e[0] : 0u, h[1] ? e[1] : 0u, h[2]);
+        }
+        CK(hipFree(st));
+        CK(hipFree(ex));
+    }
+    {
+        // settled, interleaved A/B: 0.5 s of steps first (clock ramp), then 7
+        // rounds over all variants; report each variant's median
+        auto settle = [&] {
+            hipEvent_t a, b;
+            CK(hipEventCreate(&a));
+            CK(hipEventCreate(&b));
+            float tot = 0;
+            while (tot < 500.0f) {
+                CK(hipEventRecord(a, 0));
+                for (int i = 0; i < 100; ++i) {
+                    gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
+                    gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr);
+                }
+                CK(hipEventRecord(b, 0));
+                CK(hipEventSynchronize(b));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a, b));
+                tot += ms;
+            }
+        };
+        struct V {
+            const char *name;
+            std::function<void()> f;
+            double bytes;
+            std::vector<float> t;
+        };
+        std::vector<V> vs;
+        vs.push_back({"AB: encode product", enc(k_qsgd_encode<6, 0, 0, 0>, 2048), enc_bytes, {}});
+        vs.push_back({"AB: encode DIV2 (two corrections)", enc(k_qsgd_encode<6, 0, 0, ENC_DIV2>, 2048), enc_bytes, {}});
+        vs.push_back({"AB: encode NT loads", enc(k_qsgd_encode<6, 0, 0, ENC_NT>, 2048), enc_bytes, {}});
+        vs.push_back({"AB: encode NT + DIV2", enc(k_qsgd_encode<6, 0, 0, ENC_DIV2 | ENC_NT>, 2048), enc_bytes, {}});
+        vs.push_back({"AB: absmax product", [&] { gc_absmax_f32(x, nullptr, n, norm, ws, nullptr); }, rd_bytes, {}});
+        vs.push_back({"AB: step product (absmax+encode)", [&] {
+                          gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
+                          enc(k_qsgd_encode<6, 0, 0, 0>, 2048)();
+                      }, 8.0 * n + 4.0 * M, {}});
+        vs.push_back({"AB: step absmax + encode DIV2", [&] {
+                          gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
+                          enc(k_qsgd_encode<6, 0, 0, ENC_DIV2>, 2048)();
+                      }, 8.0 * n + 4.0 * M, {}});
+        vs.push_back({"AB: step absmax + encode NT", [&] {
+                          gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
+                          enc(k_qsgd_encode<6, 0, 0, ENC_NT>, 2048)();
+                      }, 8.0 * n + 4.0 * M, {}});
+        settle();
+        for (int rep = 0; rep < 7; ++rep)
+            for (auto &v : vs)
+                v.t.push_back(T.run(v.f, 50));
+        for (auto &v : vs) {
+            std::sort(v.t.begin(), v.t.end());
+            row(v.name, v.t[v.t.size() / 2], v.bytes);
+        }
+    }
     // the lab's ABL=0 instantiation must equal the product's words
     hipLaunchKernelGGL((k_qsgd_encode<6, 0, 0, 0>), dim3(2048), dim3(256), 0, 0, x, (const int64_t *)nullptr, n, norm,
                        s, qmax, ln.bits, (uint64_t)M, ra, words2);
@@ -412,5 +565,7 @@ int main(int argc, char **argv)
     same("SEQ planes >=8 waves", k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>);
     same("register prefetch", k_qsgd_encode<6, 0, 0, ENC_PF>);
     same("register prefetch MINW=4", k_qsgd_encode<6, 0, 0, ENC_PF, 4>);
+    same("two-correction division", k_qsgd_encode<6, 0, 0, ENC_DIV2>);
+    same("nontemporal loads", k_qsgd_encode<6, 0, 0, ENC_NT>);
     return 0;
 }
