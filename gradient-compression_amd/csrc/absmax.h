@@ -130,8 +130,16 @@ __device__ __forceinline__ void absmax_finish(uint32_t m, uint32_t *__restrict__
     }
 }
 
-// MODE 0: float4 dense, 1: scalar dense, 2: gather.  U float4 loads in flight per thread.
-template <int MODE, bool WS, unsigned BT = kAbsmaxThreads, int U = 4>
+__device__ __forceinline__ float4 ld_nt(const float4 *p)
+{
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+    return make_float4(r.x, r.y, r.z, r.w);
+}
+
+// MODE 0: float4 dense, 1: scalar dense, 2: gather.  U float4 loads in flight
+// per thread; NT: nontemporal loads (streamed once)
+template <int MODE, bool WS, unsigned BT = kAbsmaxThreads, int U = 4, bool NT = false>
 __global__ __launch_bounds__(BT) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
                                                uint64_t n, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)
 {
@@ -145,7 +153,7 @@ __global__ __launch_bounds__(BT) void k_absmax(const float *__restrict__ x, cons
             float4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                v[u] = x4[t + u * stride];
+                v[u] = NT ? ld_nt(x4 + t + u * stride) : x4[t + u * stride];
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 m = max(m, absbits4(v[u]));

@@ -25,6 +25,7 @@ namespace gc {
 // max-norm: k_absmax (absmax.h).  Product grid: kAbsmaxGrid blocks of
 // kAbsmaxThreads (one per CU: 16 waves x 4 float4 loads in flight = 64 KB per CU).
 constexpr unsigned kAbsmaxGrid = 256;
+constexpr unsigned kEncodeGrid = 12288;  // blocks of the dense encode (see launch_encode)
 
 
 // ---------------------------------------------------------------------------
@@ -218,9 +219,14 @@ template <int L, int KIND, int MODE>
 static void launch_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, float s, int32_t qmax,
                           const gc_lanes *ln, RngArgs ra, uint32_t *words, hipStream_t st)
 {
+    // Product variant (tools/lab2, profiles/r01m_*): integer stochastic rounding
+    // on full tiles + nontemporal loads of x (read once per pass); a grid of
+    // up to 12288 blocks (48 per CU, ~1.4 tiles per thread at 1e8 floats)
+    // keeps more of the 6 plane streams in flight than a 2048-block grid-stride.
     const uint64_t quads = ln->plane_words >> 2;
-    hipLaunchKernelGGL((k_qsgd_encode<L, KIND, MODE, 0>), dim3(grid_for(quads)), dim3(kBlock), 0, st, x, idx, n, norm,
-                       s, qmax, ln->bits, ln->plane_words, ra, words);
+    constexpr int ABL = ENC_INT | ENC_NT;
+    hipLaunchKernelGGL((k_qsgd_encode<L, KIND, MODE, ABL>), dim3(grid_for(quads, kEncodeGrid)), dim3(kBlock), 0, st, x,
+                       idx, n, norm, s, qmax, ln->bits, ln->plane_words, ra, words);
 }
 
 }  // namespace gc
@@ -248,8 +254,11 @@ int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, v
     const uint64_t items = mode == 0 ? (n >> 2) : n;
     const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((items + kAbsmaxThreads - 1) / kAbsmaxThreads, 1),
                                                        kAbsmaxGrid);
+    // dense reads are nontemporal (x is streamed once per pass: 61 vs 67 us at
+    // 1e8 floats, profiles/r01m_lab2_*.log)
 #define GC_AM(MODE_, WS_) \
-    hipLaunchKernelGGL((k_absmax<MODE_, WS_>), dim3(grid), dim3(kAbsmaxThreads), 0, st, x, idx, n, o, ws)
+    hipLaunchKernelGGL((k_absmax<MODE_, WS_, kAbsmaxThreads, 4, MODE_ == 0>), dim3(grid), dim3(kAbsmaxThreads), 0, st, \
+                       x, idx, n, o, ws)
     if (ws) {
         if (mode == 0) GC_AM(0, true); else if (mode == 1) GC_AM(1, true); else GC_AM(2, true);
     } else {

@@ -31,6 +31,84 @@ enum : int {
     ENC_PF = 1024,      // register prefetch: the next tile's L loads are issued before this tile's math
     ENC_DIV2 = 2048,    // the compiler's two-correction quotient (div_fast2) instead of Markstein's
     ENC_NT = 4096,      // nontemporal loads of x
+    ENC_INT = 8192,     // integer stochastic rounding on full tiles (same outputs; needs s * 2^24 < 2^31)
+};
+
+// ---------------------------------------------------------------------------
+// Integer form of the stochastic rounding (ENC_INT), bit-identical to
+// enc_lane on the fast path (|x| <= norm, no tiny |x|, norm in range):
+//   q  = RN(x / norm)                 signed Markstein quotient (RN is odd)
+//   Ls = RN(q * s*2^24)               = RN(|x|/norm * s) * 2^24 exactly (power-of-two
+//                                       scaling of a normal product; |Ls| <= s*2^24)
+//   Ac = ceil(|Ls|) = fl*2^24 + F     F = ceil(p*2^24): for l >= 1/2, Ls is an
+//                                       integer; below, fl = 0 and F = ceil(l*2^24)
+//   [u < p] = [m < F]                 u = m*2^-24, m = r & 0xFFFFFF integer
+//   h  = (floor(-|Ls|) + m) >> 24     = -fl - [m < F] = -xi   (arithmetic shift)
+// so the lane needs one v_cvt_flr_i32_f32 (-|Ls| as a source modifier), one
+// and, one add and a 24-bit multiply whose SDWA byte-3 select is the shift.
+// The sign is folded into that multiply: sgk = med3(bits(x), -2^sh, 2^sh) is
+// +-2^sh for every nonzero fast-path x (|x| >= 2^-100 has bits >= 2^27 > 2^sh)
+// and h = 0 whenever x is +-0, so  h * sgk = -q * 2^sh.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t cvt_flr_neg_abs(float v)
+{
+    int32_t r;
+    asm("v_cvt_flr_i32_f32_e64 %0, -|%1|" : "=v"(r) : "v"(v));
+    return r;
+}
+
+__device__ __forceinline__ int32_t med3_i32(int32_t a, int32_t lo, int32_t hi)
+{
+    int32_t r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(lo), "s"(hi));
+    return r;
+}
+
+// (r & 0xFFFFFF) + c in one op: v_mad_u32_u24 reads only the low 24 bits
+__device__ __forceinline__ int32_t add_low24(uint32_t r, int32_t c)
+{
+    int32_t o;
+    asm("v_mad_u32_u24 %0, %1, 1, %2" : "=v"(o) : "v"(r), "v"(c));
+    return o;
+}
+
+// -q * 2^sh for one element (see above) from Ls = RN(q * s*2^24); lo = -2^sh, hi = 2^sh
+__device__ __forceinline__ int32_t enc_negq_int(float x, float Ls, uint32_t r, int32_t lo, int32_t hi)
+{
+    const int32_t t = add_low24(r, cvt_flr_neg_abs(Ls));
+    return __mul24(t >> 24, med3_i32(__float_as_int(x), lo, hi));
+}
+
+typedef float gc_f2 __attribute__((ext_vector_type(2)));
+
+// Ls = RN(RN(x / norm) * S24) for a pair, as packed fp32 (v_pk_mul_f32 /
+// v_pk_fma_f32): the signed Markstein quotient (RN is odd), then the scale
+__device__ __forceinline__ gc_f2 ls2(float a, float b, const DivNorm &d, float S24)
+{
+    const gc_f2 x = {a, b};
+    const gc_f2 y = {d.rr, d.rr};
+    const gc_f2 nb = {-d.norm, -d.norm};
+    const gc_f2 q0 = x * y;
+    const gc_f2 e = __builtin_elementwise_fma(nb, q0, x);
+    const gc_f2 q = __builtin_elementwise_fma(e, y, q0);
+    const gc_f2 sc = {S24, S24};
+    return q * sc;
+}
+
+// fast-path tile check for ENC_INT: every |x| <= norm (inf / NaN excluded by
+// the bit compare) and no nonzero |x| below the division's low threshold.
+// 2*bits drops the sign; 2*bits - 2 wraps +-0 to 0xFFFFFFFE.
+struct RangeI {
+    uint32_t mn = 0xffffffffu, mx = 0u;
+    __device__ __forceinline__ void add4(const float4 &v)
+    {
+        const uint32_t a = __float_as_uint(v.x), b = __float_as_uint(v.y);
+        const uint32_t c = __float_as_uint(v.z), e = __float_as_uint(v.w);
+        mn = min(min(mn, 2u * a - 2u), min(min(2u * b - 2u, 2u * c - 2u), 2u * e - 2u));
+        mx = max(max(mx, 2u * a), max(max(2u * b, 2u * c), 2u * e));
+    }
+    // lo2 = 2 * bits(thr_lo) - 2, hi2 = 2 * bits(norm)
+    __device__ __forceinline__ bool slow(uint32_t lo2, uint32_t hi2) const { return (mn < lo2) | (mx > hi2); }
 };
 
 // lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
@@ -110,6 +188,13 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
     const uint64_t last = (uint64_t)(L - 1) * M;
     const uint64_t full = (MODE == 0 && fast && n >= last + 4 && n < (1ull << 32)) ? (n - last) >> 2 : 0;
     const uint32_t M32 = (uint32_t)M;
+    // ENC_INT constants (uniform): s * 2^24 must stay below 2^31 (b <= 7)
+    const bool intok = s <= 127.0f;
+    const float S24 = s * 16777216.0f;
+    const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
+    uint32_t Cw = 0;
+    for (int k = 0; k < L; ++k)
+        Cw += (uint32_t)qmax << (k * w);
     if constexpr ((ABL & ENC_PF) != 0) {
         float4 nx[L];
         if (t < full) {
@@ -167,6 +252,41 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
                 xv[k] = make_float4(r.x, r.y, r.z, r.w);
             } else {
                 xv[k] = *p;
+            }
+        }
+        if constexpr ((ABL & ENC_INT) != 0) {
+            if (intok) {
+                RangeI rg;
+#pragma unroll
+                for (int k = 0; k < L; ++k)
+                    rg.add4(xv[k]);
+                if (__builtin_expect(!rg.slow(lo2, hi2), 1)) {
+                    // lanes k < H accumulate at shift k*w, lanes k >= H at (k-H)*w,
+                    // so every 24-bit multiplier is +-2^sh with sh <= 15
+                    constexpr int H = L / 2;
+                    int32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int k = 0; k < L; ++k) {
+                        const gc_f2 l01 = ls2(xv[k].x, xv[k].y, dv, S24);
+                        const gc_f2 l23 = ls2(xv[k].z, xv[k].w, dv, S24);
+                        const uint4 r = draws4_abl<KIND, ABL>(rng, 0, k * M32 + t4);
+                        const uint32_t sh = (uint32_t)(k < H ? k : k - H) * w;
+                        const int32_t bl = -(1 << sh), bh = 1 << sh;
+                        int32_t *a = k < H ? lo : hi;
+                        a[0] += enc_negq_int(xv[k].x, l01.x, r.x, bl, bh);
+                        a[1] += enc_negq_int(xv[k].y, l01.y, r.y, bl, bh);
+                        a[2] += enc_negq_int(xv[k].z, l23.x, r.z, bl, bh);
+                        a[3] += enc_negq_int(xv[k].w, l23.y, r.w, bl, bh);
+                    }
+                    const uint32_t hs = (uint32_t)H * w;
+                    uint4 acc;
+                    acc.x = Cw - ((uint32_t)lo[0] + ((uint32_t)hi[0] << hs));
+                    acc.y = Cw - ((uint32_t)lo[1] + ((uint32_t)hi[1] << hs));
+                    acc.z = Cw - ((uint32_t)lo[2] + ((uint32_t)hi[2] << hs));
+                    acc.w = Cw - ((uint32_t)lo[3] + ((uint32_t)hi[3] << hs));
+                    *reinterpret_cast<uint4 *>(words + t4) = acc;
+                    continue;
+                }
             }
         }
         if constexpr ((ABL & ENC_SEQ) != 0) {

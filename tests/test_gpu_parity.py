@@ -123,6 +123,47 @@ def test_encode_non_finite_and_tiny_inputs(world):
         assert bits_eq(u32(words), O.qsgd_encode(x, tiny, bits, world, O.philox_rng(77, 1))), tiny
 
 
+def _int_path_input(n, norm, s, seed):
+    """Values that stress the integer stochastic rounding of full tiles:
+    exact level boundaries k*norm/s and their float neighbours (p = 0 and p
+    just above 0 / just below 1), +-norm, +-0, l < 1/2 with a non-integer
+    l*2^24, and a few subnormals (their tiles take the IEEE branch)."""
+    rng = np.random.default_rng(seed)
+    x = O.gen_input(n, seed=seed, kind=seed % 2) * np.float32(norm / 0.05)
+    k = rng.integers(-s, s + 1, n).astype(np.float32)
+    lvl = (k * np.float32(norm)) / np.float32(s)
+    pick = rng.random(n)
+    x = np.where(pick < 0.15, lvl, x)
+    x = np.where((pick >= 0.15) & (pick < 0.25), np.nextafter(lvl, np.float32(np.inf)), x)
+    x = np.where((pick >= 0.25) & (pick < 0.35), np.nextafter(lvl, np.float32(-np.inf)), x)
+    tiny = (rng.random(n).astype(np.float32) * np.float32(norm) * np.float32(2.0**-28))
+    x = np.where((pick >= 0.35) & (pick < 0.40), tiny, x)
+    x = np.clip(x, -norm, norm).astype(np.float32)
+    x[::4099] = norm
+    x[7::4111] = -norm
+    x[3::1009] = 0.0
+    x[5::1013] = -0.0
+    x[11::50021] = np.float32(1e-40)  # subnormal: that tile takes the IEEE branch
+    return x
+
+
+@pytest.mark.parametrize("bits", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_encode_integer_rounding_path_edges(bits, world):
+    """The dense full-tile body rounds in integers (v_cvt_flr of -|Ls| +
+    24-bit add, qsgd_encode.h ENC_INT) for b <= 7 and in floats for b = 8:
+    both must equal the oracle's float arithmetic on adversarial values."""
+    s = (1 << bits) - 1
+    n = 6 * 4 * 4096 + 13
+    for norm in (np.float32(0.05), np.float32(3.0), np.float32(2.0**-60)):
+        x = _int_path_input(n, norm, s, seed=bits * 31 + world)
+        nh = O.absmax(x)
+        r = gcodec.rng.Reservation(0, 4242 + bits, 5, None, n, 1)
+        words = codec.qsgd_encode(dev(x), float(nh), bits, r, world)
+        ref = O.qsgd_encode(x, nh, bits, world, O.philox_rng(4242 + bits, 5))
+        assert bits_eq(u32(words), ref), (bits, world, float(norm))
+
+
 def test_zero_bucket_gives_zero():
     n, bits = 1000, 4
     x = np.zeros(n, np.float32)

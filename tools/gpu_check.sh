@@ -18,7 +18,7 @@ run() {  # name, timeout, cmd...
   if [ $rc -ge 124 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-[ -x tools/encode_lab ] && run lab_$TAG 200 tools/encode_lab
+[ -x tools/lab2 ] && run lab_$TAG 200 tools/lab2
 [ "$MODE" = "lab" ] && exit 0
 run smoke_$TAG 400 python -c "import __graft_entry__ as g; g.smoke()"
 run pytest_gpu_$TAG 900 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider
