@@ -267,6 +267,16 @@ __device__ __forceinline__ int32_t xi_from_q(float ql, float s, uint32_t r)
 
 __device__ __forceinline__ int32_t sgn_of(float x) { return (x > 0.0f) ? 1 : ((x < 0.0f) ? -1 : 0); }
 
+// nontemporal 16-byte store: streamed outputs written once (decoded floats,
+// packed words) bypass the cache hierarchy's allocation; 400 MB of decode
+// stores take 69 instead of 92 us (profiles/r01n_lab2_nt.log)
+__device__ __forceinline__ void st_nt4(float *p, const float4 &v)
+{
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v r = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(r, reinterpret_cast<f4v *>(p));
+}
+
 // ---------------------------------------------------------------------------
 // wave64 / block reductions
 // ---------------------------------------------------------------------------

@@ -26,6 +26,7 @@ namespace gc {
 // kAbsmaxThreads (one per CU: 16 waves x 4 float4 loads in flight = 64 KB per CU).
 constexpr unsigned kAbsmaxGrid = 256;
 constexpr unsigned kEncodeGrid = 12288;  // blocks of the dense encode (see launch_encode)
+constexpr unsigned kDecodeGrid = 16384;  // blocks of the dense decode (see qsgd_decode)
 
 
 // ---------------------------------------------------------------------------
@@ -57,7 +58,7 @@ __device__ __forceinline__ void store4(float *__restrict__ out, const int64_t *_
         return;
     }
     if (MODE == 0 && i0 + 4 <= n) {
-        *reinterpret_cast<float4 *>(out + i0) = v;
+        st_nt4(out + i0, v);
         return;
     }
     if (i0 + 0 < n)
@@ -219,12 +220,13 @@ template <int L, int KIND, int MODE>
 static void launch_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, float s, int32_t qmax,
                           const gc_lanes *ln, RngArgs ra, uint32_t *words, hipStream_t st)
 {
-    // Product variant (tools/lab2, profiles/r01m_*): integer stochastic rounding
-    // on full tiles + nontemporal loads of x (read once per pass); a grid of
+    // Product variant (tools/lab2, profiles/r01m_*, r01n_*): integer stochastic
+    // rounding on full tiles, nontemporal loads of x (read once per pass) and
+    // nontemporal stores of the words (-5 us per absmax+encode step); a grid of
     // up to 12288 blocks (48 per CU, ~1.4 tiles per thread at 1e8 floats)
     // keeps more of the 6 plane streams in flight than a 2048-block grid-stride.
     const uint64_t quads = ln->plane_words >> 2;
-    constexpr int ABL = ENC_INT | ENC_NT;
+    constexpr int ABL = ENC_INT | ENC_NT | ENC_NTS;
     hipLaunchKernelGGL((k_qsgd_encode<L, KIND, MODE, ABL>), dim3(grid_for(quads, kEncodeGrid)), dim3(kBlock), 0, st, x,
                        idx, n, norm, s, qmax, ln->bits, ln->plane_words, ra, words);
 }
@@ -326,7 +328,9 @@ static int qsgd_decode(const char *what, const uint32_t *words, const int64_t *i
     hipStream_t st = as_stream(stream);
     const int mode = segs ? 3 : idx ? 2 : (aligned16(out) ? 0 : 1);
     const int32_t sub = (int32_t)(lanes->world * s);
-    const unsigned grid = grid_for(lanes->plane_words >> 2);
+    // dense / per-tensor decode: one word quad per thread (16384 blocks at 1e8
+    // floats) with nontemporal stores, 69 vs 92 us (profiles/r01n_lab2_nt.log)
+    const unsigned grid = grid_for(lanes->plane_words >> 2, (mode == 0 || mode == 3) ? kDecodeGrid : 0);
     const float sf = (float)s;
 #define GC_DEC(MODE_)                                                                                         \
     GC_DISPATCH_L(lanes->per_word, hipLaunchKernelGGL((k_qsgd_decode<LL, MODE_>), dim3(grid), dim3(kBlock), 0, \

@@ -32,7 +32,20 @@ enum : int {
     ENC_DIV2 = 2048,    // the compiler's two-correction quotient (div_fast2) instead of Markstein's
     ENC_NT = 4096,      // nontemporal loads of x
     ENC_INT = 8192,     // integer stochastic rounding on full tiles (same outputs; needs s * 2^24 < 2^31)
+    ENC_NTS = 16384,    // nontemporal stores of the packed words
 };
+
+template <int ABL>
+__device__ __forceinline__ void store_words(uint32_t *p, const uint4 &v)
+{
+    if constexpr ((ABL & ENC_NTS) != 0) {
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        const u4v r = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(r, reinterpret_cast<u4v *>(p));
+    } else {
+        *reinterpret_cast<uint4 *>(p) = v;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // Integer form of the stochastic rounding (ENC_INT), bit-identical to
@@ -284,7 +297,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
                     acc.y = Cw - ((uint32_t)lo[1] + ((uint32_t)hi[1] << hs));
                     acc.z = Cw - ((uint32_t)lo[2] + ((uint32_t)hi[2] << hs));
                     acc.w = Cw - ((uint32_t)lo[3] + ((uint32_t)hi[3] << hs));
-                    *reinterpret_cast<uint4 *>(words + t4) = acc;
+                    store_words<ABL>(words + t4, acc);
                     continue;
                 }
             }

@@ -58,7 +58,7 @@ __device__ __forceinline__ void seg_store4(const SegArg &sg, uint64_t i0, uint64
     if (i0 + 4 <= p.r.end) {
         float *d = p.r.ptr + (i0 - p.r.start);
         if ((reinterpret_cast<uintptr_t>(d) & 15u) == 0) {
-            *reinterpret_cast<float4 *>(d) = v;
+            st_nt4(d, v);
         } else {
             d[0] = v.x;
             d[1] = v.y;

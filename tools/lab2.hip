@@ -73,6 +73,19 @@ __global__ __launch_bounds__(256) void k_read_planar(const float *x, uint32_t M,
         out[0] = m;
 }
 
+template <bool NT>
+__global__ __launch_bounds__(256) void k_write(uint4 *o, uint64_t n4)
+{
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < n4; t += gridDim.x * 256ull) {
+        const u4v v = {(uint32_t)t, 1u, 2u, 3u};
+        if (NT)
+            __builtin_nontemporal_store(v, reinterpret_cast<u4v *>(o + t));
+        else
+            *reinterpret_cast<u4v *>(o + t) = v;
+    }
+}
+
 // read-only flush: fills the Infinity Cache with clean lines of another buffer
 __global__ __launch_bounds__(256) void k_flush(const uint4 *o, uint64_t n4, uint32_t *out)
 {
@@ -81,6 +94,71 @@ __global__ __launch_bounds__(256) void k_flush(const uint4 *o, uint64_t n4, uint
         acc ^= o[t].x;
     if (acc == 0x12345678u)
         out[0] = acc;
+}
+
+// the encode's memory pattern with no arithmetic, NT loads / NT stores
+template <int L, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_copy_planar(const float *x, uint32_t M, uint32_t *words)
+{
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    const uint32_t quads = M >> 2;
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < quads; t += gridDim.x * 256u) {
+        u4v acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            const f4v *p = reinterpret_cast<const f4v *>(x + k * M + 4 * t);
+            const f4v v = NTL ? __builtin_nontemporal_load(p) : *p;
+            acc ^= __builtin_bit_cast(u4v, v);
+        }
+        if (NTS)
+            __builtin_nontemporal_store(acc, reinterpret_cast<u4v *>(words + 4 * t));
+        else
+            *reinterpret_cast<u4v *>(words + 4 * t) = acc;
+    }
+}
+
+// dense decode (qsgd.hip k_qsgd_decode MODE 0) with variants: NT stores,
+// U words per thread in flight
+template <int L, bool NTS, int U>
+__global__ __launch_bounds__(256) void k_decode_lab(const uint32_t *__restrict__ words, uint64_t n,
+                                                    const float *__restrict__ normp, float s, int32_t sub, uint32_t w,
+                                                    uint64_t M, float alpha, float *__restrict__ out)
+{
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const float c = *normp / s;
+    const uint32_t mask = (1u << w) - 1u;
+    const uint32_t quads = (uint32_t)(M >> 2);
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t t0 = blockIdx.x * 256u + threadIdx.x; t0 < quads; t0 += U * stride) {
+        uint4 wd[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t0 + u * stride < quads)
+                wd[u] = *reinterpret_cast<const uint4 *>(words + 4ull * (t0 + u * stride));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t t = t0 + u * stride;
+            if (t >= quads)
+                break;
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const uint64_t i0 = (uint64_t)k * M + 4ull * t;
+                if (i0 + 4 <= n) {
+                    const uint32_t sh = (uint32_t)k * w;
+                    f4v o;
+                    o.x = (c * (float)((int32_t)((wd[u].x >> sh) & mask) - sub)) * alpha;
+                    o.y = (c * (float)((int32_t)((wd[u].y >> sh) & mask) - sub)) * alpha;
+                    o.z = (c * (float)((int32_t)((wd[u].z >> sh) & mask) - sub)) * alpha;
+                    o.w = (c * (float)((int32_t)((wd[u].w >> sh) & mask) - sub)) * alpha;
+                    if (NTS)
+                        __builtin_nontemporal_store(o, reinterpret_cast<f4v *>(out + i0));
+                    else
+                        *reinterpret_cast<f4v *>(out + i0) = o;
+                }
+            }
+        }
+    }
 }
 
 struct Timer {
@@ -120,12 +198,13 @@ int main(int argc, char **argv)
         return 1;
     }
     const uint32_t M = (uint32_t)ln.plane_words;
-    float *x, *norm;
+    float *x, *norm, *dec_out;
     uint32_t *words, *words2, *scratch;
     uint4 *fl;
     const uint64_t flbytes = 600ull << 20;
     CK(hipMalloc(&x, n * 4 + 64));
     CK(hipMalloc(&norm, 64));
+    CK(hipMalloc(&dec_out, n * 4 + 64));
     CK(hipMalloc(&words, (size_t)M * 4 + 64));
     CK(hipMalloc(&words2, (size_t)M * 4 + 64));
     CK(hipMalloc(&scratch, 64));
@@ -173,6 +252,21 @@ int main(int argc, char **argv)
     same("ENC_INT", enc(k_qsgd_encode<6, 0, 0, ENC_INT>, 2048, words2));
     same("ENC_INT | ENC_REV", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_REV>, 2048, words2));
     same("ENC_INT | ENC_NT", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 8192, words2));
+    same("ENC_INT | ENC_NT | ENC_NTS", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 8192, words2));
+    {
+        // lab decode == product decode
+        float *d2;
+        CK(hipMalloc(&d2, n * 4 + 64));
+        gc_qsgd_decode(words, nullptr, n, norm, bits, &ln, 1.0f, dec_out, nullptr);
+        hipLaunchKernelGGL((k_decode_lab<6, true, 2>), dim3(4096), dim3(256), 0, 0, words, n, norm, s, qmax, ln.bits,
+                           (uint64_t)M, 1.0f, d2);
+        CK(hipDeviceSynchronize());
+        std::vector<uint32_t> da(n), db(n);
+        CK(hipMemcpy(da.data(), dec_out, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(db.data(), d2, n * 4, hipMemcpyDeviceToHost));
+        printf("%-40s == product: %s\n", "decode lab NTS U2", memcmp(da.data(), db.data(), n * 4) == 0 ? "yes" : "NO");
+        CK(hipFree(d2));
+    }
 
     // ---- 2. settled interleaved A/B ----
     {
@@ -193,26 +287,45 @@ int main(int argc, char **argv)
         vs.push_back({"AB: encode product", product_enc, enc_bytes, {}});
         static char names[64][96];
         int ni = 0;
-        auto am_nt = [&] {
-            hipLaunchKernelGGL((k_absmax<0, true, 1024, 4, true>), dim3(256), dim3(1024), 0, 0, x,
-                               (const int64_t *)nullptr, n, (uint32_t *)norm, (uint32_t *)ws);
+        (void)ni;
+        auto cp = [&](auto kern, unsigned g) {
+            return [=] { hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, 0, x, M, words2); };
         };
-        for (unsigned g : {8192u, 12288u, 16384u}) {
-            snprintf(names[ni], 96, "AB: encode INT g=%u", g);
-            vs.push_back({names[ni++], enc(k_qsgd_encode<6, 0, 0, ENC_INT>, g, words2), enc_bytes, {}});
-            snprintf(names[ni], 96, "AB: encode INT NT g=%u", g);
-            vs.push_back({names[ni++], enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, g, words2), enc_bytes, {}});
-            snprintf(names[ni], 96, "AB: step absmax + INT g=%u", g);
-            vs.push_back({names[ni++], step(product_am, enc(k_qsgd_encode<6, 0, 0, ENC_INT>, g, words2)), step_bytes, {}});
-            snprintf(names[ni], 96, "AB: step absmax + INT NT g=%u", g);
-            vs.push_back({names[ni++], step(product_am, enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, g, words2)),
-                          step_bytes, {}});
-            snprintf(names[ni], 96, "AB: step absmax NT + INT NT g=%u", g);
-            vs.push_back({names[ni++], step(am_nt, enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, g, words2)),
-                          step_bytes, {}});
-        }
-        vs.push_back({"AB: absmax NT", am_nt, rd_bytes, {}});
-        vs.push_back({"AB: compute only INT g=8192", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_ABL_L2>, 8192, words2), enc_bytes, {}});
+        vs.push_back({"roof: planar R+W plain g=8192", cp(k_copy_planar<6, false, false>, 8192), enc_bytes, {}});
+        vs.push_back({"roof: planar R+W NT loads g=8192", cp(k_copy_planar<6, true, false>, 8192), enc_bytes, {}});
+        vs.push_back({"roof: planar R+W NT loads g=12288", cp(k_copy_planar<6, true, false>, 12288), enc_bytes, {}});
+        vs.push_back({"roof: planar R+W NT ld+st g=12288", cp(k_copy_planar<6, true, true>, 12288), enc_bytes, {}});
+        vs.push_back({"roof: planar R+W NT ld+st g=16384", cp(k_copy_planar<6, true, true>, 16384), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT g=12288 (product)", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 12288, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT NTS g=12288", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 12288, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT g=16384", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 16384, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT NTS g=16384", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 16384, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT g=24576", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 24576, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT MINW=5 g=12288", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT, 5>, 12288, words2), enc_bytes, {}});
+        vs.push_back({"AB: step product", step(product_am, product_enc), step_bytes, {}});
+        vs.push_back({"AB: step + NTS", step(product_am, enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 12288, words2)), step_bytes, {}});
+        vs.push_back({"AB: step + NTS g=16384", step(product_am, enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 16384, words2)), step_bytes, {}});
+        vs.push_back({"AB: compute only INT g=12288", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_ABL_L2>, 12288, words2), enc_bytes, {}});
+        const double dec_bytes = 4.0 * n + 4.0 * M;
+        auto dec = [&](auto kern, unsigned g) {
+            return [=] {
+                hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, 0, words, n, norm, s, qmax, ln.bits, (uint64_t)M, 1.0f,
+                                   dec_out);
+            };
+        };
+        vs.push_back({"AB: decode product", [&] { gc_qsgd_decode(words, nullptr, n, norm, bits, &ln, 1.0f, dec_out, nullptr); }, dec_bytes, {}});
+        vs.push_back({"AB: decode lab U1 g=2048", dec(k_decode_lab<6, false, 1>, 2048), dec_bytes, {}});
+        vs.push_back({"AB: decode lab U1 g=16384", dec(k_decode_lab<6, false, 1>, 16384), dec_bytes, {}});
+        vs.push_back({"AB: decode lab NTS U1 g=2048", dec(k_decode_lab<6, true, 1>, 2048), dec_bytes, {}});
+        vs.push_back({"AB: decode lab NTS U1 g=16384", dec(k_decode_lab<6, true, 1>, 16384), dec_bytes, {}});
+        vs.push_back({"AB: decode lab U2 g=4096", dec(k_decode_lab<6, false, 2>, 4096), dec_bytes, {}});
+        vs.push_back({"AB: decode lab NTS U2 g=4096", dec(k_decode_lab<6, true, 2>, 4096), dec_bytes, {}});
+        vs.push_back({"roof: write-only 400 MB", [&] {
+                          hipLaunchKernelGGL(k_write<false>, dim3(8192), dim3(256), 0, 0, (uint4 *)dec_out, n / 4);
+                      }, rd_bytes, {}});
+        vs.push_back({"roof: write-only 400 MB NT", [&] {
+                          hipLaunchKernelGGL(k_write<true>, dim3(8192), dim3(256), 0, 0, (uint4 *)dec_out, n / 4);
+                      }, rd_bytes, {}});
         vs.push_back({"AB: absmax product", product_am, rd_bytes, {}});
         vs.push_back({"AB: read-only roofline", [&] {
                           hipLaunchKernelGGL(k_read<false>, dim3(2048), dim3(256), 0, 0, (const float4 *)x, n / 4, scratch);
