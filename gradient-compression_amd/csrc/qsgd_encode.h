@@ -31,7 +31,7 @@ enum : int {
     ENC_PF = 1024,      // register prefetch: the next tile's L loads are issued before this tile's math
     ENC_DIV2 = 2048,    // the compiler's two-correction quotient (div_fast2) instead of Markstein's
     ENC_NT = 4096,      // nontemporal loads of x
-    ENC_INT = 8192,     // integer stochastic rounding on full tiles (same outputs; needs s * 2^24 < 2^31)
+    ENC_INT = 8192,     // integer stochastic rounding on full tiles (same outputs; b <= 8)
     ENC_NTS = 16384,    // nontemporal stores of the packed words
 };
 
@@ -106,6 +106,63 @@ __device__ __forceinline__ gc_f2 ls2(float a, float b, const DivNorm &d, float S
     const gc_f2 q = __builtin_elementwise_fma(e, y, q0);
     const gc_f2 sc = {S24, S24};
     return q * sc;
+}
+
+// b = 8 (s*2^24 >= 2^31): the unsigned form.  Ac = ceil(|Ls|) <= 255*2^24,
+// t = Ac + (~r & 0xFFFFFF) < 2^32, xi = t >> 24 = fl + [m < F]; returns +q * 2^sh
+__device__ __forceinline__ int32_t enc_q_wide(float x, float Ls, uint32_t r, int32_t lo, int32_t hi)
+{
+    const uint32_t ac = (uint32_t)__builtin_ceilf(fabsf(Ls));
+    const uint32_t t = (uint32_t)add_low24(~r, (int32_t)ac);
+    return __mul24((int32_t)(t >> 24), med3_i32(__float_as_int(x), lo, hi));
+}
+
+template <int KIND, int ABL>
+__device__ __forceinline__ uint4 draws4_abl(const RngArgs &rng, uint32_t level, uint64_t i0);
+
+// one full tile (L planes x 4 words) on the integer path.  Lanes k < H
+// accumulate at shift k*w, lanes k >= H at (k-H)*w, so every 24-bit
+// multiplier is +-2^sh with sh <= 15; word = C -+ (lo + (hi << H*w)).
+template <int L, int KIND, int ABL, bool WIDE>
+__device__ __forceinline__ uint4 enc_tile_int(const float4 (&xv)[L], uint32_t t4, uint32_t M32, const DivNorm &dv,
+                                              float S24, uint32_t w, uint32_t Cw, const RngArgs &rng)
+{
+    constexpr int H = L / 2;
+    int32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+        const gc_f2 l01 = ls2(xv[k].x, xv[k].y, dv, S24);
+        const gc_f2 l23 = ls2(xv[k].z, xv[k].w, dv, S24);
+        const uint4 r = draws4_abl<KIND, ABL>(rng, 0, k * M32 + t4);
+        const uint32_t sh = (uint32_t)(k < H ? k : k - H) * w;
+        const int32_t bl = -(1 << sh), bh = 1 << sh;
+        int32_t *a = k < H ? lo : hi;
+        if constexpr (WIDE) {
+            a[0] += enc_q_wide(xv[k].x, l01.x, r.x, bl, bh);
+            a[1] += enc_q_wide(xv[k].y, l01.y, r.y, bl, bh);
+            a[2] += enc_q_wide(xv[k].z, l23.x, r.z, bl, bh);
+            a[3] += enc_q_wide(xv[k].w, l23.y, r.w, bl, bh);
+        } else {
+            a[0] += enc_negq_int(xv[k].x, l01.x, r.x, bl, bh);
+            a[1] += enc_negq_int(xv[k].y, l01.y, r.y, bl, bh);
+            a[2] += enc_negq_int(xv[k].z, l23.x, r.z, bl, bh);
+            a[3] += enc_negq_int(xv[k].w, l23.y, r.w, bl, bh);
+        }
+    }
+    const uint32_t hs = (uint32_t)H * w;
+    uint4 acc;
+    if constexpr (WIDE) {
+        acc.x = Cw + ((uint32_t)lo[0] + ((uint32_t)hi[0] << hs));
+        acc.y = Cw + ((uint32_t)lo[1] + ((uint32_t)hi[1] << hs));
+        acc.z = Cw + ((uint32_t)lo[2] + ((uint32_t)hi[2] << hs));
+        acc.w = Cw + ((uint32_t)lo[3] + ((uint32_t)hi[3] << hs));
+    } else {
+        acc.x = Cw - ((uint32_t)lo[0] + ((uint32_t)hi[0] << hs));
+        acc.y = Cw - ((uint32_t)lo[1] + ((uint32_t)hi[1] << hs));
+        acc.z = Cw - ((uint32_t)lo[2] + ((uint32_t)hi[2] << hs));
+        acc.w = Cw - ((uint32_t)lo[3] + ((uint32_t)hi[3] << hs));
+    }
+    return acc;
 }
 
 // fast-path tile check for ENC_INT: every |x| <= norm (inf / NaN excluded by
@@ -201,8 +258,9 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
     const uint64_t last = (uint64_t)(L - 1) * M;
     const uint64_t full = (MODE == 0 && fast && n >= last + 4 && n < (1ull << 32)) ? (n - last) >> 2 : 0;
     const uint32_t M32 = (uint32_t)M;
-    // ENC_INT constants (uniform): s * 2^24 must stay below 2^31 (b <= 7)
-    const bool intok = s <= 127.0f;
+    // ENC_INT constants (uniform): b <= 7 (s * 2^24 < 2^31) takes the signed
+    // floor form, b = 8 the unsigned ceil form
+    const bool intok = s <= 255.0f, narrow = s <= 127.0f;
     const float S24 = s * 16777216.0f;
     const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
     uint32_t Cw = 0;
@@ -274,29 +332,8 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
                 for (int k = 0; k < L; ++k)
                     rg.add4(xv[k]);
                 if (__builtin_expect(!rg.slow(lo2, hi2), 1)) {
-                    // lanes k < H accumulate at shift k*w, lanes k >= H at (k-H)*w,
-                    // so every 24-bit multiplier is +-2^sh with sh <= 15
-                    constexpr int H = L / 2;
-                    int32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
-#pragma unroll
-                    for (int k = 0; k < L; ++k) {
-                        const gc_f2 l01 = ls2(xv[k].x, xv[k].y, dv, S24);
-                        const gc_f2 l23 = ls2(xv[k].z, xv[k].w, dv, S24);
-                        const uint4 r = draws4_abl<KIND, ABL>(rng, 0, k * M32 + t4);
-                        const uint32_t sh = (uint32_t)(k < H ? k : k - H) * w;
-                        const int32_t bl = -(1 << sh), bh = 1 << sh;
-                        int32_t *a = k < H ? lo : hi;
-                        a[0] += enc_negq_int(xv[k].x, l01.x, r.x, bl, bh);
-                        a[1] += enc_negq_int(xv[k].y, l01.y, r.y, bl, bh);
-                        a[2] += enc_negq_int(xv[k].z, l23.x, r.z, bl, bh);
-                        a[3] += enc_negq_int(xv[k].w, l23.y, r.w, bl, bh);
-                    }
-                    const uint32_t hs = (uint32_t)H * w;
-                    uint4 acc;
-                    acc.x = Cw - ((uint32_t)lo[0] + ((uint32_t)hi[0] << hs));
-                    acc.y = Cw - ((uint32_t)lo[1] + ((uint32_t)hi[1] << hs));
-                    acc.z = Cw - ((uint32_t)lo[2] + ((uint32_t)hi[2] << hs));
-                    acc.w = Cw - ((uint32_t)lo[3] + ((uint32_t)hi[3] << hs));
+                    const uint4 acc = narrow ? enc_tile_int<L, KIND, ABL, false>(xv, t4, M32, dv, S24, w, Cw, rng)
+                                             : enc_tile_int<L, KIND, ABL, true>(xv, t4, M32, dv, S24, w, Cw, rng);
                     store_words<ABL>(words + t4, acc);
                     continue;
                 }
