@@ -130,13 +130,6 @@ __device__ __forceinline__ void absmax_finish(uint32_t m, uint32_t *__restrict__
     }
 }
 
-__device__ __forceinline__ float4 ld_nt(const float4 *p)
-{
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
-    return make_float4(r.x, r.y, r.z, r.w);
-}
-
 // MODE 0: float4 dense, 1: scalar dense, 2: gather.  U float4 loads in flight
 // per thread; NT: nontemporal loads (streamed once)
 template <int MODE, bool WS, unsigned BT = kAbsmaxThreads, int U = 4, bool NT = false>

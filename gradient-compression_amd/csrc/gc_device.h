@@ -267,6 +267,14 @@ __device__ __forceinline__ int32_t xi_from_q(float ql, float s, uint32_t r)
 
 __device__ __forceinline__ int32_t sgn_of(float x) { return (x > 0.0f) ? 1 : ((x < 0.0f) ? -1 : 0); }
 
+// nontemporal 16-byte load: streamed inputs read once per pass (x)
+__device__ __forceinline__ float4 ld_nt(const float4 *p)
+{
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+    return make_float4(r.x, r.y, r.z, r.w);
+}
+
 // nontemporal 16-byte store: streamed outputs written once (decoded floats,
 // packed words) bypass the cache hierarchy's allocation; 400 MB of decode
 // stores take 69 instead of 92 us (profiles/r01n_lab2_nt.log)

@@ -1,0 +1,518 @@
+// ms_fast.h — dense fast paths of the multi-scale / two-scale kernels
+// (multiscale.hip; compressors.py:754-826 and 612-680).  Same outputs as the
+// generic kernels, bit for bit; what changes is the cost per element:
+//   * the level decision and the selected level's rounding use the integer
+//     stochastic rounding of qsgd_encode.h (ENC_INT): one signed Markstein
+//     quotient per element, then per level one packed scale, one
+//     v_cvt_flr_i32_f32 and one v_mad_u32_u24;
+//   * the mask-plane position of an element (i / M_mask) is a multiply-high
+//     division by the plane size (no 64-bit divide);
+//   * the order-0 decode RN(RN(Q*norm) / s) divides by the level scale with
+//     Markstein's one-correction quotient (y = RN(1/s) per level);
+//   * x, the mask words and the decoded floats are streamed nontemporally.
+// Work split: a block owns 64 word quads; its 4 waves take the planes
+// p = wave, wave+4, ... of those quads (lanes = consecutive quads, so every
+// load is a 1 KB contiguous wave access).  A thread walks at most
+// ceil(planes/4) planes instead of all of them: one thread per quad and 32
+// sequential plane loads (the mask at W=1) ran 41 us at 23.5M floats, latency
+// bound on 11 waves per CU (profiles/r01q_lab_ms*.log).  Encoders combine the
+// waves' partial words through LDS; the decode needs no combine.
+// Taken when: dense aligned x (MODE 0), n < 2^32, 2 or 3 levels (NL, a
+// template argument: level tables and mask fields resolve at compile time),
+// every level <= 7 bits (s * 2^24 < 2^31).  Anything else, and any quad whose |x| fail the
+// RangeI check (or whose norm is outside the Markstein range), runs the
+// generic per-element code.
+#pragma once
+
+#include "gc_device.h"
+#include "ms_common.h"
+#include "qsgd_encode.h"
+
+namespace gc {
+
+// x / d for any 32-bit x, d >= 2 (the "round-up" multiply-high method with
+// the add-and-halve fix; m = floor(2^32 (2^s - d) / d) + 1, s = ceil(log2 d))
+struct FastDiv {
+    uint32_t m, s1, d;
+};
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv &f)
+{
+    const uint32_t t = __umulhi(x, f.m);
+    return (t + ((x - t) >> 1)) >> f.s1;
+}
+
+inline FastDiv make_fastdiv(uint32_t d)
+{
+    uint32_t s = 0;
+    while ((1ull << s) < d)
+        ++s;
+    FastDiv f;
+    f.d = d;
+    f.s1 = s - 1;
+    f.m = (uint32_t)((((1ull << s) - d) << 32) / d + 1);
+    return f;
+}
+
+// lab variants (tools/lab_ms.hip); the product uses VAR = 0
+enum : int {
+    MSV_PERTHREAD = 1,  // one thread walks all planes of its word quad (no wave split)
+    MSV_NORNG = 2,      // measurement only: draws = a hash of the element index (no Philox)
+    MSV_NOSLOW = 4,     // measurement only: no generic fallback (assumes every quad is fast)
+};
+
+template <int KIND, int VAR>
+__device__ __forceinline__ uint4 ms_draws4(const RngArgs &rng, uint32_t level, uint32_t i0)
+{
+    if constexpr ((VAR & MSV_NORNG) != 0) {
+        const uint32_t b = (i0 + level * 0x9E3779B9u) * 2654435761u;
+        return make_uint4(b, b ^ 0x5bd1e995u, b + 0x27d4eb2fu, b * 3u);
+    } else {
+        return draws4<KIND>(rng, level, i0);
+    }
+}
+
+// per-level constants of the fast path (uniform)
+struct MsFastArg {
+    float S24[GC_MAX_LEVELS];  // s_l * 2^24
+    float y[GC_MAX_LEVELS];    // RN(1 / s_l)
+    int32_t thr;               // -maxv * 2^24: level l qualifies iff T_l >= thr
+};
+
+// the mask level of 4 elements, from W-summed thermometer fields; the plane
+// of element i0 is i0 / M (fast division), all 4 share it (M % 4 == 0)
+template <int NL>
+__device__ __forceinline__ uint4 mask_levels4_fast(const MaskArg &mk, const FastDiv &fd, uint32_t i0)
+{
+    const uint32_t plane = fdiv(i0, fd);
+    const uint32_t pos = i0 - plane * fd.d;
+    const uint32_t sh = plane * mk.w;
+    const uint32_t msk = (1u << mk.w) - 1u;
+    uint4 m = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int f = 0; f < NL - 1; ++f) {
+        const uint4 wd = *reinterpret_cast<const uint4 *>(mk.words + (uint64_t)f * mk.M + pos);
+        m.x += ((wd.x >> sh) & msk) == mk.world;
+        m.y += ((wd.y >> sh) & msk) == mk.world;
+        m.z += ((wd.z >> sh) & msk) == mk.world;
+        m.w += ((wd.w >> sh) & msk) == mk.world;
+    }
+    return m;
+}
+
+// T = floor(-|RN(q * S24)|) + (r & 0xFFFFFF); T >> 24 = -xi (qsgd_encode.h)
+__device__ __forceinline__ int32_t ms_t(float Ls, uint32_t r) { return add_low24(r, cvt_flr_neg_abs(Ls)); }
+
+// signed Markstein quotient pair RN(x / norm)
+__device__ __forceinline__ gc_f2 quot2_signed(float a, float b, const DivNorm &d)
+{
+    const gc_f2 x = {a, b};
+    const gc_f2 y = {d.rr, d.rr};
+    const gc_f2 nb = {-d.norm, -d.norm};
+    const gc_f2 q0 = x * y;
+    const gc_f2 e = __builtin_elementwise_fma(nb, q0, x);
+    return __builtin_elementwise_fma(e, y, q0);
+}
+
+// mask levels of 4 fast-path elements: last level l whose xi_l <= maxv
+template <int KIND, int NL, int VAR = 0>
+__device__ __forceinline__ uint4 ms_levels4_int(const float4 &v, const DivNorm &dv, const LevelsArg &lv,
+                                                const MsFastArg &fa, const RngArgs &rng, uint32_t i0)
+{
+    const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+    uint4 m = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int l = 1; l < NL; ++l) {
+        const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
+        const gc_f2 S = {fa.S24[l], fa.S24[l]};
+        const gc_f2 a = q01 * S, b = q23 * S;
+        m.x = ms_t(a.x, r.x) >= fa.thr ? (uint32_t)l : m.x;
+        m.y = ms_t(a.y, r.y) >= fa.thr ? (uint32_t)l : m.y;
+        m.z = ms_t(b.x, r.z) >= fa.thr ? (uint32_t)l : m.z;
+        m.w = ms_t(b.y, r.w) >= fa.thr ? (uint32_t)l : m.w;
+    }
+    return m;
+}
+
+template <int MODE>
+__device__ __forceinline__ float4 load4_nt_tail(const float *__restrict__ x, uint32_t i0, uint32_t n)
+{
+    if (i0 + 4 <= n)
+        return ld_nt(reinterpret_cast<const float4 *>(x + i0));
+    float4 v;
+    v.x = x[i0];
+    v.y = i0 + 1 < n ? x[i0 + 1] : 0.0f;
+    v.z = i0 + 2 < n ? x[i0 + 2] : 0.0f;
+    v.w = i0 + 3 < n ? x[i0 + 3] : 0.0f;
+    return v;
+}
+
+__device__ __forceinline__ void st_nt4u(uint32_t *p, const uint4 &v)
+{
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    const u4v r = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(r, reinterpret_cast<u4v *>(p));
+}
+
+// ---------------------------------------------------------------------------
+// per-plane work (4 elements i0..i0+3 of one plane)
+// ---------------------------------------------------------------------------
+// resolution levels (0 past n)
+template <int KIND, int NL, int VAR = 0>
+__device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                            uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                            const RngArgs &rng)
+{
+    const float4 v = load4_nt_tail<0>(x, i0, n);
+    RangeI rg;
+    rg.add4(v);
+    const bool fast = (VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2));
+    uint4 m = make_uint4(0u, 0u, 0u, 0u);
+    gc_f2 q01, q23;
+    float4 ql;
+    if (fast) {
+        q01 = quot2_signed(v.x, v.y, dv);
+        q23 = quot2_signed(v.z, v.w, dv);
+    } else {
+        ql = quot4_exact(v, dv);
+    }
+#pragma unroll
+    for (int l = 1; l < NL; ++l) {
+        const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);  // one draw block per level, either path
+        if (fast) {
+            const gc_f2 S = {fa.S24[l], fa.S24[l]};
+            const gc_f2 a = q01 * S, b = q23 * S;
+            m.x = ms_t(a.x, r.x) >= fa.thr ? (uint32_t)l : m.x;
+            m.y = ms_t(a.y, r.y) >= fa.thr ? (uint32_t)l : m.y;
+            m.z = ms_t(b.x, r.z) >= fa.thr ? (uint32_t)l : m.z;
+            m.w = ms_t(b.y, r.w) >= fa.thr ? (uint32_t)l : m.w;
+        } else {
+            const float s = lv.s[l];
+            m.x = xi_from_q(ql.x, s, r.x) <= lv.maxv ? (uint32_t)l : m.x;
+            m.y = xi_from_q(ql.y, s, r.y) <= lv.maxv ? (uint32_t)l : m.y;
+            m.z = xi_from_q(ql.z, s, r.z) <= lv.maxv ? (uint32_t)l : m.z;
+            m.w = xi_from_q(ql.w, s, r.w) <= lv.maxv ? (uint32_t)l : m.w;
+        }
+    }
+    if (i0 + 4 > n) {
+        m.y = i0 + 1 < n ? m.y : 0u;
+        m.z = i0 + 2 < n ? m.z : 0u;
+        m.w = i0 + 3 < n ? m.w : 0u;
+    }
+    return m;
+}
+
+// thermometer bits [m > f] of 4 elements into the field accumulators
+template <int NL>
+__device__ __forceinline__ void mask_bits(uint4 (&acc)[NL - 1], const uint4 &m, uint32_t sh)
+{
+#pragma unroll
+    for (int f = 0; f < NL - 1; ++f) {
+        acc[f].x |= (uint32_t)(m.x > (uint32_t)f) << sh;
+        acc[f].y |= (uint32_t)(m.y > (uint32_t)f) << sh;
+        acc[f].z |= (uint32_t)(m.z > (uint32_t)f) << sh;
+        acc[f].w |= (uint32_t)(m.w > (uint32_t)f) << sh;
+    }
+}
+
+template <int KIND, int NL, int VAR = 0>
+__device__ __forceinline__ uint4 draws_at(const RngArgs &rng, uint32_t i0, uint4 m)
+{
+    uint4 r = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (uint32_t l = 0; l < (uint32_t)NL; ++l) {
+        if (m.x != l && m.y != l && m.z != l && m.w != l)
+            continue;
+        const uint4 d = ms_draws4<KIND, VAR>(rng, l, i0);
+        r.x = m.x == l ? d.x : r.x;
+        r.y = m.y == l ? d.y : r.y;
+        r.z = m.z == l ? d.z : r.z;
+        r.w = m.w == l ? d.w : r.w;
+    }
+    return r;
+}
+
+template <int NL>
+__device__ __forceinline__ float pick_level(const float (&a)[GC_MAX_LEVELS], uint32_t m)
+{
+    float v = a[0];
+#pragma unroll
+    for (int l = 1; l < NL; ++l)
+        v = m == (uint32_t)l ? a[l] : v;
+    return v;
+}
+
+// lane value q + qmax of one fast-path element at scale S (q clamped to +-qmax)
+__device__ __forceinline__ uint32_t ms_lane(float x, float Ls, uint32_t r, int32_t qmax)
+{
+    const int32_t nq = __mul24(ms_t(Ls, r) >> 24, med3_i32(__float_as_int(x), -1, 1));  // -q
+    return (uint32_t)(qmax - min(max(nq, -qmax), qmax));
+}
+
+// lane values of 4 elements at their common levels (0 past n)
+template <int KIND, int NL, int VAR = 0>
+__device__ __forceinline__ uint4 select_plane(const float *__restrict__ x, uint32_t n, uint32_t i0,
+                                              const MaskArg &mk, const FastDiv &fd, const DivNorm &dv, uint32_t lo2,
+                                              uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                              const RngArgs &rng, int32_t qmax)
+{
+    const float4 v = load4_nt_tail<0>(x, i0, n);
+    const uint4 m = mask_levels4_fast<NL>(mk, fd, i0);
+    RangeI rg;
+    rg.add4(v);
+    const uint4 r = draws_at<KIND, NL, VAR>(rng, i0, m);  // the selected level's draw, either path
+    uint4 ln;
+    if ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2))) {
+        const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+        const gc_f2 S01 = {pick_level<NL>(fa.S24, m.x), pick_level<NL>(fa.S24, m.y)};
+        const gc_f2 S23 = {pick_level<NL>(fa.S24, m.z), pick_level<NL>(fa.S24, m.w)};
+        const gc_f2 a = q01 * S01, b = q23 * S23;
+        ln.x = ms_lane(v.x, a.x, r.x, qmax);
+        ln.y = ms_lane(v.y, a.y, r.y, qmax);
+        ln.z = ms_lane(v.z, b.x, r.z, qmax);
+        ln.w = ms_lane(v.w, b.y, r.w, qmax);
+    } else {
+        const float4 ql = quot4_exact(v, dv);
+        const int32_t q0 = sgn_of(v.x) * xi_from_q(ql.x, pick_level<NL>(lv.s, m.x), r.x);
+        const int32_t q1 = sgn_of(v.y) * xi_from_q(ql.y, pick_level<NL>(lv.s, m.y), r.y);
+        const int32_t q2 = sgn_of(v.z) * xi_from_q(ql.z, pick_level<NL>(lv.s, m.z), r.z);
+        const int32_t q3 = sgn_of(v.w) * xi_from_q(ql.w, pick_level<NL>(lv.s, m.w), r.w);
+        ln.x = (uint32_t)(min(max(q0, -qmax), qmax) + qmax);
+        ln.y = (uint32_t)(min(max(q1, -qmax), qmax) + qmax);
+        ln.z = (uint32_t)(min(max(q2, -qmax), qmax) + qmax);
+        ln.w = (uint32_t)(min(max(q3, -qmax), qmax) + qmax);
+    }
+    if (i0 + 4 > n) {
+        ln.y = i0 + 1 < n ? ln.y : 0u;
+        ln.z = i0 + 2 < n ? ln.z : 0u;
+        ln.w = i0 + 3 < n ? ln.w : 0u;
+    }
+    return ln;
+}
+
+// decoded floats of 4 elements (compressors.py:819-826 order 0; 668-680 order 1) * alpha
+template <int ORDER, int NL>
+__device__ __forceinline__ void decode_plane(const uint4 &wd, uint32_t sh, uint32_t msk, int32_t sub, const uint4 &m,
+                                             float norm, const LevelsArg &lv, const MsFastArg &fa,
+                                             const float (&c)[GC_MAX_LEVELS], bool mk0, float alpha,
+                                             float *__restrict__ out, uint32_t i0, uint32_t n)
+{
+    float4 o;
+    float *op = &o.x;
+    const uint32_t *wp = &wd.x;
+    const uint32_t *mp = &m.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int32_t Q = (int32_t)((wp[e] >> sh) & msk) - sub;
+        float d;
+        if constexpr (ORDER == 1) {
+            d = pick_level<NL>(c, mp[e]) * (float)Q;
+        } else {
+            const float a = (float)Q * norm;
+            const float s = pick_level<NL>(lv.s, mp[e]);
+            if (mk0) {
+                const float y = pick_level<NL>(fa.y, mp[e]);
+                const float q0 = a * y;
+                d = fmaf(fmaf(-s, q0, a), y, q0);
+            } else {
+                d = a / s;
+            }
+        }
+        op[e] = d * alpha;
+    }
+    if (i0 + 4 <= n) {
+        st_nt4(out + i0, o);
+    } else {
+        for (int e = 0; e < 4; ++e)
+            if (i0 + e < n)
+                out[i0 + e] = pickf(o, e);
+    }
+}
+
+constexpr uint32_t kMsQuadsPerBlock = 64;  // word quads per block (one per lane; 4 waves split the planes)
+
+// ---------------------------------------------------------------------------
+// mask encode: thermometer fields of the resolution level (compressors.py:799-807)
+// ---------------------------------------------------------------------------
+template <int LM, int KIND, int NL, int VAR = 0>
+__global__ __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict__ x, uint32_t n,
+                                                         const float *__restrict__ normp, LevelsArg lv, MsFastArg fa,
+                                                         RngArgs rng, uint32_t M, uint32_t w, uint32_t fields,
+                                                         uint32_t *__restrict__ mask_words)
+{
+    const float norm = *normp;
+    const DivNorm dv = make_div(norm);
+    const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
+    const uint32_t quads = M >> 2;
+    if constexpr ((VAR & MSV_PERTHREAD) != 0) {
+        for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < quads; t += gridDim.x * kBlock) {
+            uint4 acc[NL - 1] = {};
+#pragma unroll
+            for (int j = 0; j < LM; ++j) {
+                const uint32_t i0 = (uint32_t)j * M + 4u * t;
+                if (i0 >= n)
+                    break;
+                mask_bits<NL>(acc, mask_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng), (uint32_t)j * w);
+            }
+#pragma unroll
+            for (int f = 0; f < NL - 1; ++f)
+                st_nt4u(mask_words + (uint64_t)f * M + 4u * t, acc[f]);
+        }
+        return;
+    }
+    constexpr int PW = (LM + 3) / 4;  // planes per wave
+    __shared__ uint4 part[3][kMsQuadsPerBlock];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
+        const uint32_t t = tb + lane;
+        uint4 acc[NL - 1] = {};
+        if (t < quads) {
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                const uint32_t p = wave + 4u * j;
+                if (p >= (uint32_t)LM)
+                    break;
+                const uint32_t i0 = p * M + 4u * t;
+                if (i0 >= n)
+                    break;
+                mask_bits<NL>(acc, mask_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng), p * w);
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < NL - 1; ++f) {
+            if (wave)
+                part[wave - 1][lane] = acc[f];
+            __syncthreads();
+            if (wave == 0 && t < quads) {
+                const uint4 a = part[0][lane], b = part[1][lane], c = part[2][lane];
+                st_nt4u(mask_words + (uint64_t)f * M + 4u * t,
+                        make_uint4(acc[f].x | a.x | b.x | c.x, acc[f].y | a.y | b.y | c.y,
+                                   acc[f].z | a.z | b.z | c.z, acc[f].w | a.w | b.w | c.w));
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// select encode: q at each element's common level, packed (compressors.py:809-817)
+// ---------------------------------------------------------------------------
+template <int LQ, int KIND, int NL, int VAR = 0>
+__global__ __launch_bounds__(kBlock) void k_ms_select_fast(const float *__restrict__ x, uint32_t n,
+                                                           const float *__restrict__ normp, LevelsArg lv,
+                                                           MsFastArg fa, RngArgs rng, MaskArg mk, FastDiv fd,
+                                                           uint32_t Mq, uint32_t wq, int32_t qmax,
+                                                           uint32_t *__restrict__ words)
+{
+    const float norm = *normp;
+    const DivNorm dv = make_div(norm);
+    const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
+    const uint32_t quads = Mq >> 2;
+    if constexpr ((VAR & MSV_PERTHREAD) != 0) {
+        for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < quads; t += gridDim.x * kBlock) {
+            uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int k = 0; k < LQ; ++k) {
+                const uint32_t i0 = (uint32_t)k * Mq + 4u * t;
+                if (i0 >= n)
+                    break;
+                const uint4 ln = select_plane<KIND, NL, VAR>(x, n, i0, mk, fd, dv, lo2, hi2, lv, fa, rng, qmax);
+                const uint32_t sh = (uint32_t)k * wq;
+                acc.x += ln.x << sh;
+                acc.y += ln.y << sh;
+                acc.z += ln.z << sh;
+                acc.w += ln.w << sh;
+            }
+            st_nt4u(words + 4u * t, acc);
+        }
+        return;
+    }
+    constexpr int PW = (LQ + 3) / 4;
+    __shared__ uint4 part[3][kMsQuadsPerBlock];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
+        const uint32_t t = tb + lane;
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+        if (t < quads) {
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                const uint32_t p = wave + 4u * j;
+                if (p >= (uint32_t)LQ)
+                    break;
+                const uint32_t i0 = p * Mq + 4u * t;
+                if (i0 >= n)
+                    break;
+                const uint4 ln = select_plane<KIND, NL, VAR>(x, n, i0, mk, fd, dv, lo2, hi2, lv, fa, rng, qmax);
+                const uint32_t sh = p * wq;
+                acc.x += ln.x << sh;
+                acc.y += ln.y << sh;
+                acc.z += ln.z << sh;
+                acc.w += ln.w << sh;
+            }
+        }
+        if (wave)
+            part[wave - 1][lane] = acc;
+        __syncthreads();
+        if (wave == 0 && t < quads) {
+            const uint4 a = part[0][lane], b = part[1][lane], c = part[2][lane];
+            st_nt4u(words + 4u * t, make_uint4(acc.x + a.x + b.x + c.x, acc.y + a.y + b.y + c.y,
+                                               acc.z + a.z + b.z + c.z, acc.w + a.w + b.w + c.w));
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// decode (compressors.py:819-826 order 0; 668-680 order 1) + alpha
+// ---------------------------------------------------------------------------
+template <int LQ, int ORDER, int NL, int VAR = 0>
+__global__ __launch_bounds__(kBlock) void k_ms_decode_fast(const uint32_t *__restrict__ words, MaskArg mk, FastDiv fd,
+                                                           uint32_t n, const float *__restrict__ normp, LevelsArg lv,
+                                                           MsFastArg fa, uint32_t Mq, uint32_t wq, int32_t sub,
+                                                           float alpha, float *__restrict__ out)
+{
+    const float norm = *normp;
+    // order 1: c_l = RN(norm / s_l); order 0: Markstein by s_l when Q*norm stays normal
+    float c[GC_MAX_LEVELS] = {};
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+        c[l] = ORDER == 1 ? norm / lv.s[l] : 0.0f;
+    const bool mk0 = norm >= 0x1p-100f && norm <= 0x1p100f;
+    const uint32_t msk = (1u << wq) - 1u;
+    const uint32_t quads = Mq >> 2;
+    if constexpr ((VAR & MSV_PERTHREAD) != 0) {
+        for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < quads; t += gridDim.x * kBlock) {
+            const uint4 wd = *reinterpret_cast<const uint4 *>(words + 4u * t);
+#pragma unroll
+            for (int k = 0; k < LQ; ++k) {
+                const uint32_t i0 = (uint32_t)k * Mq + 4u * t;
+                if (i0 >= n)
+                    break;
+                decode_plane<ORDER, NL>(wd, (uint32_t)k * wq, msk, sub, mask_levels4_fast<NL>(mk, fd, i0), norm, lv, fa, c,
+                                    mk0, alpha, out, i0, n);
+            }
+        }
+        return;
+    }
+    constexpr int PW = (LQ + 3) / 4;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
+        const uint32_t t = tb + lane;
+        if (t >= quads)
+            continue;
+        const uint4 wd = *reinterpret_cast<const uint4 *>(words + 4u * t);
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const uint32_t p = wave + 4u * j;
+            if (p >= (uint32_t)LQ)
+                break;
+            const uint32_t i0 = p * Mq + 4u * t;
+            if (i0 >= n)
+                break;
+            decode_plane<ORDER, NL>(wd, p * wq, msk, sub, mask_levels4_fast<NL>(mk, fd, i0), norm, lv, fa, c, mk0, alpha,
+                                out, i0, n);
+        }
+    }
+}
+
+}  // namespace gc

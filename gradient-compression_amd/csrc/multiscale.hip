@@ -13,99 +13,9 @@
 #include "gc_device.h"
 #include "gc_host.h"
 #include "segments.h"
-
+#include "ms_common.h"
+#include "ms_fast.h"
 namespace gc {
-
-struct LevelsArg {
-    uint32_t count;
-    int32_t maxv;  // 2^bits[0] - 1 (compressors.py:800)
-    float s[GC_MAX_LEVELS];
-};
-
-__device__ __forceinline__ float sel_level(const LevelsArg &lv, uint32_t m)
-{
-    float s = lv.s[0];
-#pragma unroll
-    for (int l = 1; l < GC_MAX_LEVELS; ++l)
-        if ((uint32_t)l < lv.count && m == (uint32_t)l)
-            s = lv.s[l];
-    return s;
-}
-
-template <int MODE>
-__device__ __forceinline__ float4 load4m(const float *__restrict__ x, const int64_t *__restrict__ idx, uint64_t i0,
-                                         uint64_t n)
-{
-    if (MODE == 0 && i0 + 4 <= n)
-        return *reinterpret_cast<const float4 *>(x + i0);
-    float4 v;
-    v.x = i0 + 0 < n ? (MODE == 2 ? x[idx[i0 + 0]] : x[i0 + 0]) : 0.0f;
-    v.y = i0 + 1 < n ? (MODE == 2 ? x[idx[i0 + 1]] : x[i0 + 1]) : 0.0f;
-    v.z = i0 + 2 < n ? (MODE == 2 ? x[idx[i0 + 2]] : x[i0 + 2]) : 0.0f;
-    v.w = i0 + 3 < n ? (MODE == 2 ? x[idx[i0 + 3]] : x[i0 + 3]) : 0.0f;
-    return v;
-}
-
-// resolution level of 4 elements: last level whose |q| <= maxv (level 0 always
-// qualifies, so its draws are not needed here; level l uses draw block l)
-template <int KIND>
-__device__ __forceinline__ uint4 ms_levels4(const float4 &q, const LevelsArg &lv, const RngArgs &rng, uint64_t i0)
-{
-    uint4 m = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t l = 1; l < lv.count; ++l) {
-        const uint4 r = draws4<KIND>(rng, l, i0);
-        const float s = lv.s[l];
-        if (xi_from_q(q.x, s, r.x) <= lv.maxv) m.x = l;
-        if (xi_from_q(q.y, s, r.y) <= lv.maxv) m.y = l;
-        if (xi_from_q(q.z, s, r.z) <= lv.maxv) m.z = l;
-        if (xi_from_q(q.w, s, r.w) <= lv.maxv) m.w = l;
-    }
-    return m;
-}
-
-// q of 4 elements at their own levels m (same draws as the mask pass)
-template <int KIND>
-__device__ __forceinline__ int4 ms_select4(const float4 &v, const float4 &q, const LevelsArg &lv, const RngArgs &rng,
-                                           uint64_t i0, uint4 m)
-{
-    int4 o = make_int4(0, 0, 0, 0);
-    for (uint32_t l = 0; l < lv.count; ++l) {
-        if (m.x != l && m.y != l && m.z != l && m.w != l)
-            continue;
-        const uint4 r = draws4<KIND>(rng, l, i0);
-        const float s = lv.s[l];
-        if (m.x == l) o.x = sgn_of(v.x) * xi_from_q(q.x, s, r.x);
-        if (m.y == l) o.y = sgn_of(v.y) * xi_from_q(q.y, s, r.y);
-        if (m.z == l) o.z = sgn_of(v.z) * xi_from_q(q.z, s, r.z);
-        if (m.w == l) o.w = sgn_of(v.w) * xi_from_q(q.w, s, r.w);
-    }
-    return o;
-}
-
-struct MaskArg {
-    const uint32_t *words;
-    uint64_t M;       // words per field stream
-    uint32_t w;       // lane bits
-    uint32_t fields;  // count - 1
-    uint32_t world;
-};
-
-// common level of elements pos..pos+3 (pos % 4 == 0, same plane) from W-summed fields
-__device__ __forceinline__ uint4 mask_levels4(const MaskArg &mk, uint64_t i0)
-{
-    const uint64_t plane = i0 / mk.M, pos = i0 - plane * mk.M;
-    const uint32_t sh = (uint32_t)plane * mk.w;
-    const uint32_t msk = (1u << mk.w) - 1u;
-    uint4 m = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t f = 0; f < mk.fields; ++f) {
-        const uint4 wd = *reinterpret_cast<const uint4 *>(mk.words + f * mk.M + pos);
-        m.x += ((wd.x >> sh) & msk) == mk.world;
-        m.y += ((wd.y >> sh) & msk) == mk.world;
-        m.z += ((wd.z >> sh) & msk) == mk.world;
-        m.w += ((wd.w >> sh) & msk) == mk.world;
-    }
-    return m;
-}
 
 template <int LM, int KIND, int MODE>
 __global__ __launch_bounds__(kBlock) void k_ms_mask_encode(const float *__restrict__ x, const int64_t *__restrict__ idx,
@@ -351,6 +261,32 @@ static MaskArg mask_arg(const uint32_t *w, const gc_lanes *ml, uint32_t count)
     return m;
 }
 
+
+// dense fast path (ms_fast.h): aligned dense x, n < 2^32, every level <= 7 bits
+static bool ms_fast_ok(int mode, uint64_t n, const gc_levels *lv)
+{
+    return mode == 0 && n < (1ull << 32) && (lv->count == 2 || lv->count == 3) && lv->bits[lv->count - 1] <= 7;
+}
+
+static MsFastArg ms_fast_arg(const gc_levels *lv)
+{
+    MsFastArg a;
+    for (int i = 0; i < GC_MAX_LEVELS; ++i) {
+        const float s = i < (int)lv->count ? (float)((1u << lv->bits[i]) - 1u) : 1.0f;
+        a.S24[i] = s * 16777216.0f;
+        a.y[i] = 1.0f / s;
+    }
+    a.thr = -(int32_t)((1u << lv->bits[0]) - 1u) * (1 << 24);
+    return a;
+}
+
+// blocks of the wave-split fast kernels: one per 64 word quads (ms_fast.h)
+static unsigned ms_grid(uint64_t quads)
+{
+    const uint64_t b = (quads + kMsQuadsPerBlock - 1) / kMsQuadsPerBlock;
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, 65535));
+}
+
 #define GC_DISPATCH_L2(L, ...)                                                   \
     switch (L) {                                                                 \
     case 1: { constexpr int LL = 1; __VA_ARGS__; } break;                        \
@@ -394,7 +330,20 @@ int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const floa
     GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_encode<LL, KIND_, MODE_>), dim3(grid),    \
                                                             dim3(kBlock), 0, st, x, idx, n, norm, la, ra, M, w,  \
                                                             fields, mask_words))
-    if (rng->kind == GC_RNG_PHILOX) {
+    if (ms_fast_ok(mode, n, levels)) {
+        const MsFastArg fa = ms_fast_arg(levels);
+        const unsigned g = ms_grid(M >> 2);
+#define GC_MF(KIND_, NL_)                                                                                            \
+    GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_fast<LL, KIND_, NL_>), dim3(g), dim3(kBlock), 0, \
+                                                            st, x, (uint32_t)n, norm, la, fa, ra, (uint32_t)M, w,  \
+                                                            fields, mask_words))
+        if (levels->count == 2) {
+            if (rng->kind == GC_RNG_PHILOX) { GC_MF(0, 2); } else { GC_MF(1, 2); }
+        } else {
+            if (rng->kind == GC_RNG_PHILOX) { GC_MF(0, 3); } else { GC_MF(1, 3); }
+        }
+#undef GC_MF
+    } else if (rng->kind == GC_RNG_PHILOX) {
         if (mode == 0) { GC_ME(0, 0); } else if (mode == 1) { GC_ME(0, 1); } else { GC_ME(0, 2); }
     } else {
         if (mode == 0) { GC_ME(1, 0); } else if (mode == 1) { GC_ME(1, 1); } else { GC_ME(1, 2); }
@@ -429,7 +378,21 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_encode<LL, KIND_, MODE_>), dim3(grid),       \
                                                          dim3(kBlock), 0, st, x, idx, n, norm, la, ra, mk, Mq, wq, \
                                                          qmax, words))
-    if (rng->kind == GC_RNG_PHILOX) {
+    if (ms_fast_ok(mode, n, levels) && mask_lanes->plane_words >= 2 && mask_lanes->plane_words < (1ull << 32)) {
+        const MsFastArg fa = ms_fast_arg(levels);
+        const FastDiv fd = make_fastdiv((uint32_t)mask_lanes->plane_words);
+        const unsigned g = ms_grid(Mq >> 2);
+#define GC_SF(KIND_, NL_)                                                                                             \
+    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_fast<LL, KIND_, NL_>), dim3(g), dim3(kBlock), 0,   \
+                                                         st, x, (uint32_t)n, norm, la, fa, ra, mk, fd, (uint32_t)Mq, \
+                                                         wq, qmax, words))
+        if (levels->count == 2) {
+            if (rng->kind == GC_RNG_PHILOX) { GC_SF(0, 2); } else { GC_SF(1, 2); }
+        } else {
+            if (rng->kind == GC_RNG_PHILOX) { GC_SF(0, 3); } else { GC_SF(1, 3); }
+        }
+#undef GC_SF
+    } else if (rng->kind == GC_RNG_PHILOX) {
         if (mode == 0) { GC_SE(0, 0); } else if (mode == 1) { GC_SE(0, 1); } else { GC_SE(0, 2); }
     } else {
         if (mode == 0) { GC_SE(1, 0); } else if (mode == 1) { GC_SE(1, 1); } else { GC_SE(1, 2); }
@@ -466,7 +429,21 @@ static int ms_decode(const char *what, const uint32_t *words, const uint32_t *ma
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_decode<LL, MODE_>), dim3(grid), dim3(kBlock), 0, st, \
                                                          words, mk, idx, n, norm, la, q_lanes->plane_words,        \
                                                          q_lanes->bits, sub, order, alpha, out, sg))
-    if (mode == 0) { GC_MD(0); } else if (mode == 1) { GC_MD(1); } else if (mode == 2) { GC_MD(2); } else { GC_MD(3); }
+    if (ms_fast_ok(mode, n, levels) && mask_lanes->plane_words >= 2 && mask_lanes->plane_words < (1ull << 32)) {
+        const MsFastArg fa = ms_fast_arg(levels);
+        const FastDiv fd = make_fastdiv((uint32_t)mask_lanes->plane_words);
+        const unsigned g = ms_grid(q_lanes->plane_words >> 2);
+#define GC_DF(ORD_, NL_)                                                                                               \
+    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_decode_fast<LL, ORD_, NL_>), dim3(g), dim3(kBlock), 0, st, \
+                                                         words, mk, fd, (uint32_t)n, norm, la, fa,                  \
+                                                         (uint32_t)q_lanes->plane_words, q_lanes->bits, sub, alpha, out))
+        if (levels->count == 2) {
+            if (order == 0) { GC_DF(0, 2); } else { GC_DF(1, 2); }
+        } else {
+            if (order == 0) { GC_DF(0, 3); } else { GC_DF(1, 3); }
+        }
+#undef GC_DF
+    } else if (mode == 0) { GC_MD(0); } else if (mode == 1) { GC_MD(1); } else if (mode == 2) { GC_MD(2); } else { GC_MD(3); }
 #undef GC_MD
     return launch_status(what);
 }

@@ -150,9 +150,10 @@ def _int_path_input(n, norm, s, seed):
 @pytest.mark.parametrize("bits", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("world", [1, 2, 8])
 def test_encode_integer_rounding_path_edges(bits, world):
-    """The dense full-tile body rounds in integers (v_cvt_flr of -|Ls| +
-    24-bit add, qsgd_encode.h ENC_INT) for b <= 7 and in floats for b = 8:
-    both must equal the oracle's float arithmetic on adversarial values."""
+    """The dense full-tile body rounds in integers (qsgd_encode.h ENC_INT:
+    v_cvt_flr of -|Ls| + 24-bit add for b <= 7, ceil(|Ls|) + (~r & 0xFFFFFF)
+    for b = 8): it must equal the oracle's float arithmetic on adversarial
+    values, and so must the IEEE branch that tiny norms and subnormal tiles take."""
     s = (1 << bits) - 1
     n = 6 * 4 * 4096 + 13
     for norm in (np.float32(0.05), np.float32(3.0), np.float32(2.0**-60)):
@@ -312,6 +313,41 @@ def test_ms_packed_vs_oracle(levels, world, n):
         d = codec.ms_decode(wsum, mw_sum, n, float(norm), levels, world, order, 1.0)
         ref = O.ms_dequantize(q_ref * world, norm, levels, m_ref, order)
         assert bits_eq(u32(d), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("levels", [(2, 4), (1, 3), (3, 7), (2, 4, 6), (1, 2, 3, 4, 5, 6, 7)])
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_ms_fast_path_edges_vs_oracle(levels, world):
+    """ms_fast.h (dense, levels <= 7 bits): integer rounding per level,
+    multiply-high mask positions, Markstein order-0 decode — on adversarial
+    values (level boundaries of every level, +-norm, +-0, subnormal tiles)
+    and norms inside and outside the Markstein range, vs the oracle."""
+    n = 7 * 4 * 4096 + 9
+    L = len(levels)
+    for norm0 in (np.float32(0.05), np.float32(3.0), np.float32(2.0**-110)):
+        s = (1 << levels[-1]) - 1
+        x = _int_path_input(n, norm0, s, seed=world * 7 + L)
+        if len(levels) > 1:  # boundaries of the lowest level too
+            s0 = (1 << levels[0]) - 1
+            k = np.random.default_rng(L).integers(-s0, s0 + 1, n // 3).astype(np.float32)
+            x[: n // 3] = np.clip((k * np.float32(norm0)) / np.float32(s0), -norm0, norm0)
+        norm = O.absmax(x)
+        r = gcodec.rng.Reservation(0, 313 + L, 2, None, n, L)
+        xd = dev(x)
+        mw = codec.ms_mask_encode(xd, float(norm), levels, r, world)
+        m_ref = O.ms_mask(x, norm, levels, O.philox_rng(313 + L, 2))
+        mw_sum = (mw.to(torch.int64) * world).to(torch.int32)
+        assert bits_eq(codec.ms_mask_unpack(mw_sum, n, levels, world).cpu().numpy().astype(np.uint8), m_ref)
+        words = codec.ms_select_encode(xd, float(norm), levels, r, mw_sum, world)
+        q_ref = O.ms_select(x, norm, levels, O.philox_rng(313 + L, 2), m_ref)
+        ql, _ = codec.ms_layouts(n, levels, world)
+        assert bits_eq(u32(words), O.lane_pack(q_ref, ql.offset, ql.bits, ql.per_word, ql.plane_words))
+        wsum = (words.to(torch.int64) * world).to(torch.int32)
+        alpha = np.float32(1.0 / world)
+        for order in (0, 1):
+            d = codec.ms_decode(wsum, mw_sum, n, float(norm), levels, world, order, float(alpha))
+            ref = O.ms_dequantize(q_ref * world, norm, levels, m_ref, order, alpha)
+            assert bits_eq(u32(d), ref.view(np.uint32)), (order, float(norm))
 
 
 # --------------------------------------------------------------------------- GRandK

@@ -161,6 +161,26 @@ __global__ __launch_bounds__(256) void k_decode_lab(const uint32_t *__restrict__
     }
 }
 
+// Markstein quotient by a level scale s = 2^b - 1 (ms_fast.h order-0 decode):
+// every positive float a with exponent in [-100, 113], against IEEE a / s
+__global__ __launch_bounds__(256) void k_divcheck_s(float s, unsigned long long *bad, uint32_t *example)
+{
+    const float y = 1.0f / s;
+    unsigned long long nb = 0;
+    const uint32_t first = (uint32_t)(127 - 100) << 23, last = (uint32_t)(127 + 114) << 23;
+    for (uint32_t u = first + blockIdx.x * 256u + threadIdx.x; u < last; u += gridDim.x * 256u) {
+        const float a = __uint_as_float(u);
+        const float q0 = a * y;
+        const float d = fmaf(fmaf(-s, q0, a), y, q0);
+        if (__float_as_uint(d) != __float_as_uint(a / s)) {
+            ++nb;
+            example[0] = u;
+        }
+    }
+    if (nb)
+        atomicAdd(bad, nb);
+}
+
 struct Timer {
     hipEvent_t a, b;
     Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
@@ -268,6 +288,24 @@ int main(int argc, char **argv)
         CK(hipFree(d2));
     }
 
+    if (getenv("LAB_DIVS")) {
+        unsigned long long *bad;
+        uint32_t *ex;
+        CK(hipMalloc(&bad, 8));
+        CK(hipMalloc(&ex, 8));
+        for (int b = 1; b <= 16; ++b) {
+            CK(hipMemset(bad, 0, 8));
+            hipLaunchKernelGGL(k_divcheck_s, dim3(16384), dim3(256), 0, 0, (float)((1u << b) - 1u), bad, ex);
+            unsigned long long h = 0;
+            uint32_t e = 0;
+            CK(hipMemcpy(&h, bad, 8, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(&e, ex, 4, hipMemcpyDeviceToHost));
+            printf("divcheck s=2^%d-1: %llu mismatches over every a in [2^-100, 2^114)%s\n", b, h, h ? " (see example)" : "");
+            if (h)
+                printf("   e.g. a=%08x\n", e);
+        }
+        return 0;
+    }
     // ---- 2. settled interleaved A/B ----
     {
         float tot = 0;

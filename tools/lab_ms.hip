@@ -1,0 +1,283 @@
+// lab_ms.hip — measurement harness for the multi-scale / two-scale kernels
+// (not product code).  BASELINE config 3 bucket (ResNet50, 23,520,842 fp32),
+// levels [2, 4], W = 1: the product entry points, lab variants of the dense
+// fast kernels (ms_fast.h VAR flags), and the memory rooflines of each
+// kernel's access pattern.  Variant outputs are compared with the product's.
+// Build: make -C tools lab_ms ; run: tools/lab_ms [n]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <functional>
+#include <vector>
+
+#include "gcodec.h"
+#include "ms_common.h"
+#include "ms_fast.h"
+
+using namespace gc;
+
+#define CK(x)                                                                               \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess) {                                                             \
+            fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            exit(2);                                                                        \
+        }                                                                                   \
+    } while (0)
+#define GK(x)                                                                 \
+    do {                                                                      \
+        if ((x) != GC_OK) {                                                   \
+            fprintf(stderr, "gcodec %s at %d: %s\n", #x, __LINE__, gc_last_error()); \
+            exit(3);                                                          \
+        }                                                                     \
+    } while (0)
+
+// N(0, 0.01)-like values from a counter hash (sum of 4 uniforms)
+__global__ void k_fill(float *x, uint64_t n, uint32_t seed)
+{
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        float acc = 0.0f;
+        for (int j = 0; j < 4; ++j) {
+            uint32_t h = (uint32_t)(i * 4 + j) * 2654435761u ^ seed;
+            h ^= h >> 15;
+            h *= 2246822519u;
+            h ^= h >> 13;
+            acc += (float)(h >> 8) * 0x1p-24f - 0.5f;
+        }
+        x[i] = acc * 0.0173f;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_read_nt(const float4 *x, uint64_t n4, uint32_t *out)
+{
+    uint32_t m = 0;
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < n4; t += gridDim.x * 256ull) {
+        const float4 v = ld_nt(x + t);
+        m = max(m, max(max(__float_as_uint(v.x), __float_as_uint(v.y)), max(__float_as_uint(v.z), __float_as_uint(v.w))));
+    }
+    if (m == 0x7fffffffu)
+        out[0] = m;
+}
+
+// select-like pattern: L planes of x -> one packed word quad
+template <int L>
+__global__ __launch_bounds__(256) void k_rw_planar(const float *x, uint32_t M, uint32_t *words)
+{
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < (M >> 2); t += gridDim.x * 256u) {
+        uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < L; ++k) {
+            const float4 v = ld_nt(reinterpret_cast<const float4 *>(x + k * M + 4 * t));
+            acc.x ^= __float_as_uint(v.x);
+            acc.y ^= __float_as_uint(v.y);
+            acc.z ^= __float_as_uint(v.z);
+            acc.w ^= __float_as_uint(v.w);
+        }
+        st_nt4u(words + 4 * t, acc);
+    }
+}
+
+// decode-like pattern: one word quad -> L planes of floats
+template <int L>
+__global__ __launch_bounds__(256) void k_wr_planar(const uint32_t *words, uint32_t M, float *out)
+{
+    for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < (M >> 2); t += gridDim.x * 256u) {
+        const uint4 w = *reinterpret_cast<const uint4 *>(words + 4 * t);
+#pragma unroll
+        for (int k = 0; k < L; ++k)
+            st_nt4(out + k * M + 4 * t, make_float4((float)(w.x >> k), (float)(w.y >> k), (float)(w.z >> k),
+                                                    (float)(w.w >> k)));
+    }
+}
+
+struct Timer {
+    hipEvent_t a, b;
+    Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
+    template <class F>
+    float run(F f, int reps = 20)
+    {
+        f();
+        f();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a, 0));
+        for (int i = 0; i < reps; ++i)
+            f();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        return ms / reps;
+    }
+};
+
+static void row(const char *name, float ms, double bytes)
+{
+    double gbs = bytes / (ms * 1e-3) / 1e9;
+    printf("%-52s %9.1f us  %8.1f GB/s  %5.1f%% of 8 TB/s\n", name, ms * 1e3, gbs, 100.0 * gbs / 8000.0);
+    fflush(stdout);
+}
+
+static unsigned grid(uint64_t quads, unsigned cap = 16384)
+{
+    uint64_t b = (quads + 255) / 256;
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, cap));
+}
+
+int main(int argc, char **argv)
+{
+    const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 23520842ull;
+    gc_levels lv{};
+    lv.count = 2;
+    lv.bits[0] = 2;
+    lv.bits[1] = 4;
+    gc_lanes ql, ml;
+    GK(gc_ms_layout(n, &lv, 1, &ql));
+    GK(gc_ms_mask_layout(n, &lv, 1, &ml));
+    printf("n=%llu  q lanes w=%u L=%u M=%llu  mask lanes w=%u L=%u M=%llu\n", (unsigned long long)n, ql.bits,
+           ql.per_word, (unsigned long long)ql.plane_words, ml.bits, ml.per_word, (unsigned long long)ml.plane_words);
+    if (ql.per_word != 10 || ml.per_word != 32) {
+        fprintf(stderr, "lab expects L=10 q lanes and L=32 mask lanes\n");
+        return 1;
+    }
+    const uint32_t Mq = (uint32_t)ql.plane_words, Mm = (uint32_t)ml.plane_words;
+    float *x, *norm, *out, *out2;
+    uint32_t *mw, *mw2, *wq, *wq2, *scratch;
+    CK(hipMalloc(&x, n * 4 + 64));
+    CK(hipMalloc(&out, n * 4 + 64));
+    CK(hipMalloc(&out2, n * 4 + 64));
+    CK(hipMalloc(&norm, 64));
+    CK(hipMalloc(&mw, (size_t)Mm * 4 + 64));
+    CK(hipMalloc(&mw2, (size_t)Mm * 4 + 64));
+    CK(hipMalloc(&wq, (size_t)Mq * 4 + 64));
+    CK(hipMalloc(&wq2, (size_t)Mq * 4 + 64));
+    CK(hipMalloc(&scratch, 64));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, x, n, 11u);
+    GK(gc_absmax_f32(x, nullptr, n, norm, nullptr, nullptr));
+    CK(hipDeviceSynchronize());
+
+    gc_rng rng = {GC_RNG_PHILOX, 0, 5, 0, nullptr};
+    auto p_mask = [&] { GK(gc_ms_mask_encode(x, nullptr, n, norm, &lv, &rng, &ml, mw, nullptr)); };
+    auto p_sel = [&] { GK(gc_ms_select_encode(x, nullptr, n, norm, &lv, &rng, mw, &ml, &ql, wq, nullptr)); };
+    auto p_dec = [&](int order) {
+        return [&, order] {
+            GK(gc_ms_decode(wq, mw, nullptr, n, norm, &lv, &ml, &ql, order, 1.0f, out, nullptr));
+        };
+    };
+
+    // kernel arguments as multiscale.hip builds them
+    LevelsArg la;
+    la.count = lv.count;
+    la.maxv = (1 << lv.bits[0]) - 1;
+    MsFastArg fa;
+    for (int i = 0; i < GC_MAX_LEVELS; ++i) {
+        la.s[i] = i < (int)lv.count ? (float)((1u << lv.bits[i]) - 1u) : 1.0f;
+        fa.S24[i] = la.s[i] * 16777216.0f;
+        fa.y[i] = 1.0f / la.s[i];
+    }
+    fa.thr = -la.maxv * (1 << 24);
+    RngArgs ra{5, 0, nullptr, n};
+    MaskArg mk{mw, Mm, ml.bits, lv.count - 1, 1};
+    const FastDiv fd = make_fastdiv(Mm);
+    const uint32_t n32 = (uint32_t)n;
+    const int32_t qmax = (int32_t)ql.offset, sub = (int32_t)ql.offset;
+
+    auto v_mask = [&](auto kern, uint32_t *dst) {
+        return [=] {
+            hipLaunchKernelGGL(kern, dim3(grid(Mm / 4)), dim3(256), 0, 0, x, n32, norm, la, fa, ra, Mm, ml.bits,
+                               lv.count - 1, dst);
+        };
+    };
+    auto v_sel = [&](auto kern, uint32_t *dst) {
+        return [=] {
+            hipLaunchKernelGGL(kern, dim3(grid(Mq / 4)), dim3(256), 0, 0, x, n32, norm, la, fa, ra, mk, fd, Mq,
+                               ql.bits, qmax, dst);
+        };
+    };
+    auto v_mask64 = [&](auto kern, uint32_t *dst) {
+        return [=] {
+            hipLaunchKernelGGL(kern, dim3((Mm / 4 + 63) / 64), dim3(256), 0, 0, x, n32, norm, la, fa, ra, Mm, ml.bits,
+                               lv.count - 1, dst);
+        };
+    };
+    auto v_sel64 = [&](auto kern, uint32_t *dst) {
+        return [=] {
+            hipLaunchKernelGGL(kern, dim3((Mq / 4 + 63) / 64), dim3(256), 0, 0, x, n32, norm, la, fa, ra, mk, fd, Mq,
+                               ql.bits, qmax, dst);
+        };
+    };
+    auto v_dec = [&](auto kern, float *dst) {
+        return [=] {
+            hipLaunchKernelGGL(kern, dim3(grid(Mq / 4)), dim3(256), 0, 0, wq, mk, fd, n32, norm, la, fa, Mq, ql.bits,
+                               sub, 1.0f, dst);
+        };
+    };
+
+    // ---- equality of the lab variants with the product ----
+    auto cmp = [&](const char *nm, const void *a, const void *b, size_t bytes) {
+        std::vector<uint8_t> ha(bytes), hb(bytes);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(ha.data(), a, bytes, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hb.data(), b, bytes, hipMemcpyDeviceToHost));
+        printf("%-40s == product: %s\n", nm, memcmp(ha.data(), hb.data(), bytes) == 0 ? "yes" : "NO");
+    };
+    p_mask();
+    p_sel();
+    p_dec(0)();
+    v_mask(k_ms_mask_fast<32, 0, 2, MSV_PERTHREAD>, mw2)();
+    cmp("mask PERTHREAD", mw, mw2, (size_t)Mm * 4);
+    v_sel(k_ms_select_fast<10, 0, 2, MSV_PERTHREAD>, wq2)();
+    cmp("select PERTHREAD", wq, wq2, (size_t)Mq * 4);
+    v_dec(k_ms_decode_fast<10, 0, 2, MSV_PERTHREAD>, out2)();
+    cmp("decode order 0 PERTHREAD", out, out2, n * 4);
+
+    // ---- settled interleaved A/B ----
+    Timer T;
+    const double xb = 4.0 * n, mb = 4.0 * Mm, qb = 4.0 * Mq;
+    float tot = 0;
+    while (tot < 300.0f)
+        tot += 50 * T.run([&] { p_mask(); p_sel(); p_dec(0)(); }, 50);
+    struct V {
+        const char *name;
+        std::function<void()> f;
+        double bytes;
+        std::vector<float> t;
+    };
+    std::vector<V> vs;
+    vs.push_back({"roof: read x (NT)", [&] {
+                      hipLaunchKernelGGL(k_read_nt, dim3(4096), dim3(256), 0, 0, (const float4 *)x, n / 4, scratch);
+                  }, xb, {}});
+    vs.push_back({"roof: 10 planes -> words (select pattern)", [&] {
+                      hipLaunchKernelGGL(k_rw_planar<10>, dim3(grid(Mq / 4)), dim3(256), 0, 0, x, Mq, wq2);
+                  }, xb + qb, {}});
+    vs.push_back({"roof: 32 planes -> words (mask pattern)", [&] {
+                      hipLaunchKernelGGL(k_rw_planar<32>, dim3(grid(Mm / 4)), dim3(256), 0, 0, x, Mm, mw2);
+                  }, xb + mb, {}});
+    vs.push_back({"roof: words -> 10 planes (decode pattern)", [&] {
+                      hipLaunchKernelGGL(k_wr_planar<10>, dim3(grid(Mq / 4)), dim3(256), 0, 0, wq, Mq, out2);
+                  }, xb + qb, {}});
+    vs.push_back({"product mask encode", p_mask, xb + mb, {}});
+    vs.push_back({"lab mask split", v_mask64(k_ms_mask_fast<32, 0, 2, 0>, mw2), xb + mb, {}});
+    vs.push_back({"lab mask split NORNG", v_mask64(k_ms_mask_fast<32, 0, 2, MSV_NORNG>, mw2), xb + mb, {}});
+    vs.push_back({"lab mask split NOSLOW", v_mask64(k_ms_mask_fast<32, 0, 2, MSV_NOSLOW>, mw2), xb + mb, {}});
+    vs.push_back({"lab mask split NORNG|NOSLOW", v_mask64(k_ms_mask_fast<32, 0, 2, MSV_NORNG | MSV_NOSLOW>, mw2), xb + mb, {}});
+    vs.push_back({"lab mask PERTHREAD", v_mask(k_ms_mask_fast<32, 0, 2, MSV_PERTHREAD>, mw2), xb + mb, {}});
+    vs.push_back({"product select encode", p_sel, xb + mb + qb, {}});
+    vs.push_back({"lab select split NORNG", v_sel64(k_ms_select_fast<10, 0, 2, MSV_NORNG>, wq2), xb + mb + qb, {}});
+    vs.push_back({"lab select split NOSLOW", v_sel64(k_ms_select_fast<10, 0, 2, MSV_NOSLOW>, wq2), xb + mb + qb, {}});
+    vs.push_back({"lab select split NORNG|NOSLOW", v_sel64(k_ms_select_fast<10, 0, 2, MSV_NORNG | MSV_NOSLOW>, wq2), xb + mb + qb, {}});
+    vs.push_back({"lab select PERTHREAD", v_sel(k_ms_select_fast<10, 0, 2, MSV_PERTHREAD>, wq2), xb + mb + qb, {}});
+    vs.push_back({"product decode order 0", p_dec(0), xb + mb + qb, {}});
+    vs.push_back({"product decode order 1", p_dec(1), xb + mb + qb, {}});
+    vs.push_back({"product absmax", [&] { gc_absmax_f32(x, nullptr, n, norm, nullptr, nullptr); }, xb, {}});
+    for (int rep = 0; rep < 5; ++rep)
+        for (auto &v : vs)
+            v.t.push_back(T.run(v.f, 30));
+    for (auto &v : vs) {
+        std::sort(v.t.begin(), v.t.end());
+        row(v.name, v.t[v.t.size() / 2], v.bytes);
+    }
+    return 0;
+}
