@@ -148,9 +148,27 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
             holder["d"] = ms.decode(nrm, w, m, n3, world, 1.0 / world)
 
         t = sync_ms(ms_step)
+        # per kernel (HIP events, W = this rank's lane sizing), algorithmic bytes per
+        # mask 4n + mask words, select 4n + mask + words, decode words + mask + 4n
+        ql, ml = codec.ms_layouts(n3, [2, 4], world)
+        mwords = codec.mask_words_total(ml, [2, 4])
+        m_ = ms.encode_mask(nrm, x3, world)
+        w_ = ms.encode(nrm, x3, m_, world)
+        d_ = torch.empty(n3, device=dev)
+        kt = {
+            "absmax": (_events(torch, lambda: codec.absmax(x3, out=nrm), reps), 4 * n3),
+            "mask_encode": (_events(torch, lambda: ms.encode_mask(nrm, x3, world), reps), 4 * n3 + 4 * mwords),
+            "select_encode": (_events(torch, lambda: ms.encode(nrm, x3, m_, world), reps),
+                              4 * n3 + 4 * mwords + 4 * ql.plane_words),
+            "decode": (_events(torch, lambda: ms.decode(nrm, w_, m_, n3, world, 1.0 / world, out=d_), reps),
+                       4 * n3 + 4 * mwords + 4 * ql.plane_words),
+        }
         res[f"config3_{tag}"] = {
             "n": n3, "ms_per_step": t, "grad_floats_per_s": world * n3 / (t * 1e-3),
-            "step": "absmax, MAX, mask encode, SUM(mask lanes), select encode, SUM(words), decode"}
+            "step": "absmax, MAX, mask encode, SUM(mask lanes), select encode, SUM(words), decode",
+            "kernels": {k: {"us": ms_ * 1e3, "gbs": b / (ms_ * 1e-3) / 1e9,
+                            "frac_hbm_peak": b / (ms_ * 1e-3) / 1e9 / HBM_PEAK_GBS} for k, (ms_, b) in kt.items()}}
+        del m_, w_, d_
     del x3
 
     # fused TensorBuffer / setgrad on the ResNet50 list (161 tensors)
@@ -202,8 +220,16 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
         comp.decode(nrm, w, K4, world, 1.0, idx=idx, out=x4)
 
     t = sync_ms(rk_step, reps=max(20, reps))
+    w4 = comp.encode(nrm, x4, world, idx=idx)
+    kt4 = {
+        "gather_absmax": _events(torch, lambda: codec.absmax(x4, idx=idx, out=nrm), max(20, reps)),
+        "gather_encode": _events(torch, lambda: comp.encode(nrm, x4, world, idx=idx), max(20, reps)),
+        "decode_scatter": _events(torch, lambda: comp.decode(nrm, w4, K4, world, 1.0, idx=idx, out=x4), max(20, reps)),
+    }
     res["config4_grandk_k10000"] = {"n": n4, "K": K4, "us_per_step": t * 1e3,
-                                    "step": "gather-absmax, MAX, gather-encode, SUM(words), decode-scatter"}
+                                    "step": "gather-absmax, MAX, gather-encode, SUM(words), decode-scatter",
+                                    "kernels_us": {k: v * 1e3 for k, v in kt4.items()},
+                                    "bound": "launch latency (K = 10,000 elements, 12 B each)"}
     del x4
 
     # config 5: 1B fp32, 8-bit, chunked encode | RCCL SUM | decode on separate streams
@@ -303,12 +329,25 @@ def main():
     ms_step = el / K * 1e3
     value = world * n * K / el
 
-    # ---- per-kernel HIP-event timing (same stream the kernels launch on) ----
+    # ---- per-kernel HIP-event timing: the timed loop replayed once more with
+    # events bracketing every absmax and encode launch (on the current stream,
+    # the one the codec launches on), so each kernel runs in the state it runs
+    # in inside a step; the timed loop itself stays free of event markers
+    # (4 markers per step cost ~14 us of step time, profiles/r01r_*)
     reps = max(K, 10)
-    ms_absmax = _events(torch, lambda: codec.absmax(x, out=norm), reps)
-    if world > 1:
-        dist.all_reduce(norm, op=dist.ReduceOp.MAX)
-    ms_encode = _events(torch, encode_step, reps)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(reps)]
+    for e in ev:
+        e[0].record()
+        codec.absmax(x, out=norm)
+        e[1].record()
+        if world > 1:
+            dist.all_reduce(norm, op=dist.ReduceOp.MAX)
+        e[2].record()
+        encode_step()
+        e[3].record()
+    torch.cuda.synchronize()
+    ms_absmax = sum(e[0].elapsed_time(e[1]) for e in ev) / reps
+    ms_encode = sum(e[2].elapsed_time(e[3]) for e in ev) / reps
     enc_bytes = 4 * n + 4 * M  # read x once, write the packed words
     achieved = enc_bytes / (ms_encode * 1e-3) / 1e9
     step_bytes = 8 * n + 4 * M  # + the max-norm read of x

@@ -19,9 +19,10 @@ run() {  # name, timeout, cmd...
   return 0
 }
 [ -x tools/lab2 ] && run lab_$TAG 200 tools/lab2
+[ -x tools/lab_ms ] && run labms_$TAG 200 tools/lab_ms
 [ "$MODE" = "lab" ] && exit 0
 run smoke_$TAG 400 python -c "import __graft_entry__ as g; g.smoke()"
 run pytest_gpu_$TAG 900 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider
-run bench_$TAG 600 python bench.py --steps 20 --warmup 5
+run bench_$TAG 600 python bench.py
 run profile_$TAG 1000 bash tools/profile.sh $TAG
 echo ALL DONE
