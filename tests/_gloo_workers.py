@@ -114,3 +114,57 @@ def hip_pipeline_world(rank, world, init_file, out_dir, n, bits, chunks):
              bounds=np.array(pipe.bounds, dtype=np.int64))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def ddp_hook_world(rank, world, init_file, out_dir, use_gpu):
+    """torch DDP with gcodec.ddp_hook.qsgd_hook on a small MLP, several buckets,
+    three steps; records every hook call's input bucket, RNG offset and result."""
+    import gcodec
+    from gcodec.ddp_hook import QSGDHookState, qsgd_hook
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    if use_gpu:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        codec = None
+    else:
+        import oracle_codec as codec
+
+        dev = torch.device("cpu")
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    torch.manual_seed(0)  # same initial weights on every rank
+    model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.Tanh(), torch.nn.Linear(64, 64), torch.nn.Tanh(),
+                                torch.nn.Linear(64, 8)).to(dev)
+    ddp = DDP(model, bucket_cap_mb=0.008)  # ~2k floats per bucket -> several buckets per step
+    state = QSGDHookState(bits=4, generator=gcodec.Generator(100 + rank, "philox"), codec=codec)
+    rec = []
+
+    def hook(st, bucket):
+        x_in = bucket.buffer().detach().cpu().numpy().copy()
+        off = st.gen.offset
+        fut = qsgd_hook(st, bucket)
+
+        def keep(f):
+            out = f.value()
+            rec.append((x_in, off, out.detach().cpu().numpy().copy()))
+            return out
+
+        return fut.then(keep)
+
+    ddp.register_comm_hook(state, hook)
+    g = torch.Generator().manual_seed(1000 + rank)
+    for _ in range(3):
+        inp = torch.randn(16, 32, generator=g).to(dev)
+        ddp.zero_grad()
+        ddp(inp).square().sum().backward()
+    if use_gpu:
+        torch.cuda.synchronize()
+    res = {"calls": np.int64(len(rec))}
+    for i, (x_in, off, out) in enumerate(rec):
+        res[f"c{i}/x"] = x_in
+        res[f"c{i}/off"] = np.int64(off)
+        res[f"c{i}/out"] = out
+    res["grad0"] = model[0].weight.grad.detach().cpu().numpy()
+    np.savez(os.path.join(out_dir, f"h{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -65,3 +65,15 @@ def test_chunked_pipeline_multirank(world, chunks):
         off += e - s
     for r in range(world):
         assert outs[r]["out"].tobytes() == exp.tobytes(), f"rank {r}"
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_ddp_qsgd_hook_on_gpu(world):
+    """gcodec.ddp_hook on cuda:0 (HIP codec), DDP over gloo with CUDA tensors:
+    every bucket's result equals the oracle's reduction of the ranks' inputs."""
+    from test_ddp_hook_gloo import check_hook_records
+
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(W.ddp_hook_world, args=(world, os.path.join(td, "init"), td, True), nprocs=world, join=True)
+        recs = [np.load(os.path.join(td, f"h{r}.npz"), allow_pickle=False) for r in range(world)]
+        check_hook_records(recs, world)
