@@ -229,7 +229,24 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     res["config4_grandk_k10000"] = {"n": n4, "K": K4, "us_per_step": t * 1e3,
                                     "step": "gather-absmax, MAX, gather-encode, SUM(words), decode-scatter",
                                     "kernels_us": {k: v * 1e3 for k, v in kt4.items()},
-                                    "bound": "launch latency (K = 10,000 elements, 12 B each)"}
+                                    "bound": "host issue + launch latency (K = 10,000 elements, 12 B each)"}
+    if world == 1:
+        # the same step captured once in a HIP graph and replayed: the C ABI
+        # enqueues on the caller's stream with no allocation or host sync, so
+        # the three launches capture as-is; a replay reuses the captured draw
+        # offset (timing only)
+        try:
+            graph = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                rk_step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            with torch.cuda.graph(graph):
+                rk_step()
+            res["config4_grandk_k10000"]["hipgraph_us_per_step"] = _events(torch, graph.replay, max(50, reps)) * 1e3
+        except Exception as e:  # capture unsupported on this runtime: report, do not fail the bench
+            res["config4_grandk_k10000"]["hipgraph_us_per_step"] = f"capture failed: {type(e).__name__}: {e}"
     del x4
 
     # config 5: 1B fp32, 8-bit, chunked encode | RCCL SUM | decode on separate streams
