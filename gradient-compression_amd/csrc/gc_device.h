@@ -286,6 +286,44 @@ __device__ __forceinline__ void st_nt4(float *p, const float4 &v)
 }
 
 // ---------------------------------------------------------------------------
+// GlobalRandK gathers / scatters (MODE 2).  A thread's quads in C planes
+// (elements k*M + i0 .. +3, k = k0 .. k0+C-1): every index load is issued
+// before any value load, so the thread waits two dependent round trips
+// instead of 2C.  Addresses past n are clamped to n-1 (always valid, n > 0)
+// so the loads stay unconditional and issue back to back; the caller masks
+// those lanes.
+// ---------------------------------------------------------------------------
+// planes per gather batch: up to 8 (8 x 4 int64 indices = 64 VGPRs)
+constexpr int gather_chunk(int L) { return L < 8 ? L : 8; }
+
+template <int C>
+__device__ __forceinline__ void gather_idx(const int64_t *__restrict__ idx, uint64_t n, uint64_t M, uint64_t i0,
+                                           int k0, int64_t (&id)[C][4])
+{
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            id[c][e] = idx[min((uint64_t)(k0 + c) * M + i0 + e, n - 1)];
+}
+
+template <int C>
+__device__ __forceinline__ void gather_planes(const float *__restrict__ x, const int64_t *__restrict__ idx,
+                                              uint64_t n, uint64_t M, uint64_t i0, int k0, float4 (&v)[C])
+{
+    int64_t id[C][4];
+    gather_idx<C>(idx, n, M, i0, k0, id);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint64_t b = (uint64_t)(k0 + c) * M + i0;
+        v[c].x = b + 0 < n ? x[id[c][0]] : 0.0f;
+        v[c].y = b + 1 < n ? x[id[c][1]] : 0.0f;
+        v[c].z = b + 2 < n ? x[id[c][2]] : 0.0f;
+        v[c].w = b + 3 < n ? x[id[c][3]] : 0.0f;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // wave64 / block reductions
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)

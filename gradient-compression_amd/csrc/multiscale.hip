@@ -31,20 +31,28 @@ __global__ __launch_bounds__(kBlock) void k_ms_mask_encode(const float *__restri
 #pragma unroll
         for (int f = 0; f < GC_MAX_LEVELS - 1; ++f)
             acc[f] = make_uint4(0u, 0u, 0u, 0u);
+        constexpr int C = gather_chunk(LM);
 #pragma unroll
-        for (int j = 0; j < LM; ++j) {
-            const uint64_t i0 = (uint64_t)j * M + 4 * t;
-            if (i0 < n) {
-                const float4 v = load4m<MODE>(x, idx, i0, n);
-                const uint4 m = ms_levels4<KIND>(quot4_exact(v, dv), lv, rng, i0);
-                const uint32_t sh = (uint32_t)j * w;
+        for (int j0 = 0; j0 < LM; j0 += C) {
+            float4 g[C];
+            if constexpr (MODE == 2)  // GRandK: all index loads, then all value loads
+                gather_planes<C>(x, idx, n, M, 4 * t, j0, g);
 #pragma unroll
-                for (int f = 0; f < GC_MAX_LEVELS - 1; ++f) {
-                    if ((uint32_t)f < fields) {
-                        acc[f].x |= (uint32_t)(m.x > (uint32_t)f) << sh;
-                        acc[f].y |= (uint32_t)(m.y > (uint32_t)f && i0 + 1 < n) << sh;
-                        acc[f].z |= (uint32_t)(m.z > (uint32_t)f && i0 + 2 < n) << sh;
-                        acc[f].w |= (uint32_t)(m.w > (uint32_t)f && i0 + 3 < n) << sh;
+            for (int c = 0; c < C; ++c) {
+                const int j = j0 + c;
+                const uint64_t i0 = (uint64_t)j * M + 4 * t;
+                if (j < LM && i0 < n) {
+                    const float4 v = MODE == 2 ? g[c] : load4m<MODE>(x, idx, i0, n);
+                    const uint4 m = ms_levels4<KIND>(quot4_exact(v, dv), lv, rng, i0);
+                    const uint32_t sh = (uint32_t)j * w;
+#pragma unroll
+                    for (int f = 0; f < GC_MAX_LEVELS - 1; ++f) {
+                        if ((uint32_t)f < fields) {
+                            acc[f].x |= (uint32_t)(m.x > (uint32_t)f) << sh;
+                            acc[f].y |= (uint32_t)(m.y > (uint32_t)f && i0 + 1 < n) << sh;
+                            acc[f].z |= (uint32_t)(m.z > (uint32_t)f && i0 + 2 < n) << sh;
+                            acc[f].w |= (uint32_t)(m.w > (uint32_t)f && i0 + 3 < n) << sh;
+                        }
                     }
                 }
             }
@@ -68,18 +76,26 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_encode(const float *__rest
     const uint64_t quads = Mq >> 2;
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+        constexpr int C = gather_chunk(LQ);
 #pragma unroll
-        for (int k = 0; k < LQ; ++k) {
-            const uint64_t i0 = (uint64_t)k * Mq + 4 * t;
-            if (i0 < n) {
-                const float4 v = load4m<MODE>(x, idx, i0, n);
-                const uint4 m = mask_levels4(mk, i0);
-                const int4 q = ms_select4<KIND>(v, quot4_exact(v, dv), lv, rng, i0, m);
-                const uint32_t sh = (uint32_t)k * wq;
-                acc.x |= (uint32_t)(min(max(q.x, -qmax), qmax) + qmax) << sh;
-                acc.y |= (i0 + 1 < n ? (uint32_t)(min(max(q.y, -qmax), qmax) + qmax) : 0u) << sh;
-                acc.z |= (i0 + 2 < n ? (uint32_t)(min(max(q.z, -qmax), qmax) + qmax) : 0u) << sh;
-                acc.w |= (i0 + 3 < n ? (uint32_t)(min(max(q.w, -qmax), qmax) + qmax) : 0u) << sh;
+        for (int k0 = 0; k0 < LQ; k0 += C) {
+            float4 g[C];
+            if constexpr (MODE == 2)
+                gather_planes<C>(x, idx, n, Mq, 4 * t, k0, g);
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int k = k0 + c;
+                const uint64_t i0 = (uint64_t)k * Mq + 4 * t;
+                if (k < LQ && i0 < n) {
+                    const float4 v = MODE == 2 ? g[c] : load4m<MODE>(x, idx, i0, n);
+                    const uint4 m = mask_levels4(mk, i0);
+                    const int4 q = ms_select4<KIND>(v, quot4_exact(v, dv), lv, rng, i0, m);
+                    const uint32_t sh = (uint32_t)k * wq;
+                    acc.x |= (uint32_t)(min(max(q.x, -qmax), qmax) + qmax) << sh;
+                    acc.y |= (i0 + 1 < n ? (uint32_t)(min(max(q.y, -qmax), qmax) + qmax) : 0u) << sh;
+                    acc.z |= (i0 + 2 < n ? (uint32_t)(min(max(q.z, -qmax), qmax) + qmax) : 0u) << sh;
+                    acc.w |= (i0 + 3 < n ? (uint32_t)(min(max(q.w, -qmax), qmax) + qmax) : 0u) << sh;
+                }
             }
         }
         *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
@@ -104,10 +120,17 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode(const uint32_t *__restrict
     const uint64_t quads = Mq >> 2;
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
         const uint4 wd = *reinterpret_cast<const uint4 *>(words + 4 * t);
+        constexpr int C = gather_chunk(LQ);
 #pragma unroll
-        for (int k = 0; k < LQ; ++k) {
+        for (int k0 = 0; k0 < LQ; k0 += C) {
+          int64_t id[C][4];
+          if constexpr (MODE == 2)  // GRandK scatter: the chunk's index loads together
+              gather_idx<C>(idx, n, Mq, 4 * t, k0, id);
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            const int k = k0 + c;
             const uint64_t i0 = (uint64_t)k * Mq + 4 * t;
-            if (i0 < n) {
+            if (k < LQ && i0 < n) {
                 const uint4 m = mask_levels4(mk, i0);
                 const uint32_t sh = (uint32_t)k * wq;
                 float4 o;
@@ -122,9 +145,10 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode(const uint32_t *__restrict
                 } else {
                     for (int e = 0; e < 4; ++e)
                         if (i0 + e < n)
-                            out[MODE == 2 ? idx[i0 + e] : i0 + e] = pickf(o, e);
+                            out[MODE == 2 ? id[c][e] : i0 + e] = pickf(o, e);
                 }
             }
+          }
         }
     }
 }

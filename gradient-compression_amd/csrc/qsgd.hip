@@ -88,6 +88,30 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_decode(const uint32_t *__restri
     const float c = *normp / s;
     const uint32_t mask = w >= 32 ? 0xffffffffu : ((1u << w) - 1u);
     const uint64_t quads = M >> 2;
+    if constexpr (MODE == 2) {
+        // GlobalRandK scatter: each chunk's index loads issue together with
+        // the word load (gather_idx), then the stores
+        constexpr int C = L < 8 ? L : 8;
+        for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
+            const uint4 wd = *reinterpret_cast<const uint4 *>(words + 4 * t);
+#pragma unroll
+            for (int k0 = 0; k0 < L; k0 += C) {
+                int64_t id[C][4];
+                gather_idx<C>(idx, n, M, 4 * t, k0, id);
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    const int k = k0 + j;
+                    const uint64_t i0 = (uint64_t)k * M + 4 * t;
+                    const uint32_t sh = (uint32_t)k * w;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (k < L && i0 + e < n)
+                            out[id[j][e]] = dq(pick(wd, e), sh, mask, sub, c, alpha);
+                }
+            }
+        }
+        return;
+    }
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
         const uint4 wd = *reinterpret_cast<const uint4 *>(words + 4 * t);
 #pragma unroll

@@ -387,7 +387,40 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
         }
         *reinterpret_cast<uint4 *>(words + t4) = acc;
     }
-    // generic body: tail quads (partial planes), gathers, unaligned x, odd norms
+    if constexpr (MODE == 2) {
+        // GlobalRandK gathers: planes in chunks of up to 8, all index loads
+        // then all value loads per chunk (gather_planes)
+        constexpr int C = L < 8 ? L : 8;
+        for (; t < quads; t += stride) {
+            uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int k0 = 0; k0 < L; k0 += C) {
+                float4 v[C];
+                gather_planes<C>(x, idx, n, M, 4 * t, k0, v);
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    const int k = k0 + j;
+                    const uint64_t i0 = (uint64_t)k * M + 4 * t;
+                    if (k < L && i0 < n) {
+                        const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
+                        Range rg;
+                        rg.add4(v[j]);
+                        const float4 q = fast && ((ABL & ENC_ABL_NODIV) != 0 || !rg.slow(dv))
+                                             ? quot4_fast<ABL>(v[j], dv)
+                                             : quot4_ieee(v[j], norm);
+                        const uint32_t sh = (uint32_t)k * w;
+                        acc.x |= enc_lane<ABL>(v[j].x, q.x, s, qmax, r.x) << sh;
+                        acc.y |= (i0 + 1 < n ? enc_lane<ABL>(v[j].y, q.y, s, qmax, r.y) : 0u) << sh;
+                        acc.z |= (i0 + 2 < n ? enc_lane<ABL>(v[j].z, q.z, s, qmax, r.z) : 0u) << sh;
+                        acc.w |= (i0 + 3 < n ? enc_lane<ABL>(v[j].w, q.w, s, qmax, r.w) : 0u) << sh;
+                    }
+                }
+            }
+            *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
+        }
+        return;
+    }
+    // generic body: tail quads (partial planes), unaligned x, odd norms
     for (; t < quads; t += stride) {
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll

@@ -99,6 +99,60 @@ def test_encode_unaligned_and_gather():
     assert bits_eq(u32(out), exp.view(np.uint32))
 
 
+@pytest.mark.parametrize("bits,world", [(1, 1), (2, 8), (4, 2), (8, 1), (8, 8)])
+@pytest.mark.parametrize("K", [1, 7, 10_000, 100_003])
+def test_grandk_batched_gather_scatter(bits, world, K):
+    """GRandK gather encode / scatter decode (gather_planes, gather_idx: index
+    loads batched per chunk of <= 8 planes).  1-bit lanes at W=1 give 16 planes
+    per word (two chunks); ragged K leaves partial last planes; K=1 a single
+    element.  Non-selected elements keep their value (reducer.py:754)."""
+    n = 200_003
+    x = O.gen_input(n, seed=K + bits, kind=1)
+    idx = np.random.default_rng(K + world).permutation(n)[:K].astype(np.int64)
+    xd, idd = dev(x), dev(idx)
+    normk = O.absmax(x[idx])
+    assert codec.absmax(xd, idx=idd).item() == float(normk)
+    r = gcodec.rng.Reservation(0, 11, K, None, K, 1)
+    wk = codec.qsgd_encode(xd, float(normk), bits, r, world, idx=idd)
+    refk = O.qsgd_encode(x[idx], normk, bits, world, O.philox_rng(11, K))
+    assert bits_eq(u32(wk), refk)
+    alpha = np.float32(1.0 / world)
+    out = dev(x)
+    codec.qsgd_decode(wk, K, float(normk), bits, world, float(alpha), idx=idd, out=out)
+    exp = x.copy()
+    exp[idx] = O.qsgd_decode(refk, K, normk, bits, world, alpha)
+    assert bits_eq(u32(out), exp.view(np.uint32))
+
+
+@pytest.mark.parametrize("levels", [(2, 4), (1, 2, 3, 4, 5, 6, 7, 8)])
+@pytest.mark.parametrize("K", [3, 10_001])
+def test_ms_grandk_gather_scatter(levels, K):
+    """multi-scale mask / select / decode through idx (GRandK two-scale,
+    reducer.py:1568-1621): batched gathers vs the oracle on x[idx]."""
+    n, world = 50_021, 2
+    x = O.gen_input(n, seed=K, kind=1)
+    idx = np.random.default_rng(K).permutation(n)[:K].astype(np.int64)
+    xk = x[idx]
+    norm = O.absmax(xk)
+    L = len(levels)
+    r = gcodec.rng.Reservation(0, 5, 1, None, K, L)
+    xd, idd = dev(x), dev(idx)
+    mw = codec.ms_mask_encode(xd, float(norm), levels, r, world, idx=idd)
+    assert bits_eq(u32(mw), u32(codec.ms_mask_encode(dev(xk), float(norm), levels, r, world)))
+    mw_sum = (mw.to(torch.int64) * world).to(torch.int32)
+    m_ref = O.ms_mask(xk, norm, levels, O.philox_rng(5, 1))
+    words = codec.ms_select_encode(xd, float(norm), levels, r, mw_sum, world, idx=idd)
+    q_ref = O.ms_select(xk, norm, levels, O.philox_rng(5, 1), m_ref)
+    ql, _ = codec.ms_layouts(K, levels, world)
+    assert bits_eq(u32(words), O.lane_pack(q_ref, ql.offset, ql.bits, ql.per_word, ql.plane_words))
+    wsum = (words.to(torch.int64) * world).to(torch.int32)
+    out = dev(x)
+    codec.ms_decode(wsum, mw_sum, K, float(norm), levels, world, 0, 0.5, idx=idd, out=out)
+    exp = x.copy()
+    exp[idx] = O.ms_dequantize(q_ref * world, norm, levels, m_ref, 0, np.float32(0.5))
+    assert bits_eq(u32(out), exp.view(np.uint32))
+
+
 @pytest.mark.parametrize("world", [1, 4])
 def test_encode_non_finite_and_tiny_inputs(world):
     """NaN -> 0, +/-inf and |x| > norm saturate at +/-s, subnormal and
