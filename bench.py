@@ -131,7 +131,9 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     x3 = torch.randn(n3, device=dev, generator=g).mul_(0.01)
     gen = gcodec.Generator(5 + rank, "philox")
     for tag, ms in (("twoscale_2_4", gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen)),
-                    ("multiscale_2_4", gcodec.QSGDMaxNormMultiScaleCompressor(dev, [2, 4], generator=gen))):
+                    ("multiscale_2_4", gcodec.QSGDMaxNormMultiScaleCompressor(dev, [2, 4], generator=gen)),
+                    ("twoscale_2_4_no_q_cache",
+                     gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen, q_cache=False))):
         nrm = torch.empty(1, device=dev)
         holder = {}
 
@@ -149,22 +151,25 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
 
         t = sync_ms(ms_step)
         # per kernel (HIP events, W = this rank's lane sizing), algorithmic bytes per
-        # mask 4n + mask words, select 4n + mask + words, decode words + mask + 4n
+        # mask 4n + mask words (+ q cache cells), select 4n + mask + words
+        # (from the cache: cells + mask + words), decode words + mask + 4n
         ql, ml = codec.ms_layouts(n3, [2, 4], world)
         mwords = codec.mask_words_total(ml, [2, 4])
         m_ = ms.encode_mask(nrm, x3, world)
+        cached = ms._cache_key is not None
+        cell = codec.ms_cache_bytes(n3, [2, 4]) * n3 if cached else 0
         w_ = ms.encode(nrm, x3, m_, world)
         d_ = torch.empty(n3, device=dev)
         kt = {
             "absmax": (_events(torch, lambda: codec.absmax(x3, out=nrm), reps), 4 * n3),
-            "mask_encode": (_events(torch, lambda: ms.encode_mask(nrm, x3, world), reps), 4 * n3 + 4 * mwords),
+            "mask_encode": (_events(torch, lambda: ms.encode_mask(nrm, x3, world), reps), 4 * n3 + 4 * mwords + cell),
             "select_encode": (_events(torch, lambda: ms.encode(nrm, x3, m_, world), reps),
-                              4 * n3 + 4 * mwords + 4 * ql.plane_words),
+                              (cell if cached else 4 * n3) + 4 * mwords + 4 * ql.plane_words),
             "decode": (_events(torch, lambda: ms.decode(nrm, w_, m_, n3, world, 1.0 / world, out=d_), reps),
                        4 * n3 + 4 * mwords + 4 * ql.plane_words),
         }
         res[f"config3_{tag}"] = {
-            "n": n3, "ms_per_step": t, "grad_floats_per_s": world * n3 / (t * 1e-3),
+            "n": n3, "ms_per_step": t, "grad_floats_per_s": world * n3 / (t * 1e-3), "q_cache": cached,
             "step": "absmax, MAX, mask encode, SUM(mask lanes), select encode, SUM(words), decode",
             "kernels": {k: {"us": ms_ * 1e3, "gbs": b / (ms_ * 1e-3) / 1e9,
                             "frac_hbm_peak": b / (ms_ * 1e-3) / 1e9 / HBM_PEAK_GBS} for k, (ms_, b) in kt.items()}}

@@ -154,20 +154,92 @@ __device__ __forceinline__ void st_nt4u(uint32_t *p, const uint4 &v)
     __builtin_nontemporal_store(r, reinterpret_cast<u4v *>(p));
 }
 
+// lane value qmax + clamp(q, +-qmax): from T of the integer rounding (fast
+// path; T >> 24 = -xi) or from q itself (generic path)
+__device__ __forceinline__ uint32_t lane_of_t(float x, int32_t T, int32_t qmax)
+{
+    const int32_t nq = __mul24(T >> 24, med3_i32(__float_as_int(x), -1, 1));  // -q
+    return (uint32_t)(qmax - min(max(nq, -qmax), qmax));
+}
+__device__ __forceinline__ uint32_t lane_of_q(int32_t q, int32_t qmax)
+{
+    return (uint32_t)(min(max(q, -qmax), qmax) + qmax);
+}
+
+// ---------------------------------------------------------------------------
+// q cache: the reference's compress_cache (compressors.py:778-797, every
+// level's sign*xi as an L x n float32 tensor) in packed form.  Element i
+// owns one CBY-byte cell; field l (cb bits at l*cb) = the select's lane value
+// at level l, qmax + clamp(q_l, +-qmax).  The mask kernel rounds every level
+// anyway except level 0; with the cache it rounds level 0 too and writes the
+// cell, and the select reads the cell at the common level instead of x and
+// the draws (ms_cache_bytes in multiscale.hip says when the fields fit).
+// ---------------------------------------------------------------------------
+template <int CBY>
+struct CacheCell {
+    typedef uint8_t T;
+};
+template <>
+struct CacheCell<2> {
+    typedef uint16_t T;
+};
+
+template <int CBY>
+__device__ __forceinline__ void cache_store(void *__restrict__ cache, uint32_t i0, uint32_t n, const uint4 &c)
+{
+    typedef typename CacheCell<CBY>::T T;
+    T *p = reinterpret_cast<T *>(cache) + i0;
+    if (i0 + 4 <= n) {  // i0 % 4 == 0: 4- / 8-byte aligned
+        if constexpr (CBY == 1)
+            *reinterpret_cast<uint32_t *>(p) = c.x | (c.y << 8) | (c.z << 16) | (c.w << 24);
+        else
+            *reinterpret_cast<uint2 *>(p) = make_uint2(c.x | (c.y << 16), c.z | (c.w << 16));
+        return;
+    }
+    p[0] = (T)c.x;
+    if (i0 + 1 < n)
+        p[1] = (T)c.y;
+    if (i0 + 2 < n)
+        p[2] = (T)c.z;
+}
+
+// the cells of elements i0..i0+3 (0 past n)
+template <int CBY>
+__device__ __forceinline__ uint4 cache_load(const void *__restrict__ cache, uint32_t i0, uint32_t n)
+{
+    typedef typename CacheCell<CBY>::T T;
+    const T *p = reinterpret_cast<const T *>(cache) + i0;
+    if (i0 + 4 <= n) {
+        if constexpr (CBY == 1) {
+            const uint32_t u = *reinterpret_cast<const uint32_t *>(p);
+            return make_uint4(u & 0xffu, (u >> 8) & 0xffu, (u >> 16) & 0xffu, u >> 24);
+        } else {
+            const uint2 u = *reinterpret_cast<const uint2 *>(p);
+            return make_uint4(u.x & 0xffffu, u.x >> 16, u.y & 0xffffu, u.y >> 16);
+        }
+    }
+    return make_uint4(p[0], i0 + 1 < n ? p[1] : 0u, i0 + 2 < n ? p[2] : 0u, 0u);
+}
+
 // ---------------------------------------------------------------------------
 // per-plane work (4 elements i0..i0+3 of one plane)
 // ---------------------------------------------------------------------------
-// resolution levels (0 past n)
-template <int KIND, int NL, int VAR = 0>
+// resolution levels (0 past n).  CACHE: also every level's lane value into
+// *cv (field l at bit l*cb, clamped to +-cq), from the same draws and the same
+// fast / generic decision as select_plane, so a cell field equals the lane
+// the select would compute at that level.
+template <int KIND, int NL, int VAR = 0, bool CACHE = false>
 __device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_t n, uint32_t i0, const DivNorm &dv,
                                             uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
-                                            const RngArgs &rng)
+                                            const RngArgs &rng, int32_t cq = 0, uint32_t cb = 0,
+                                            uint4 *cv = nullptr)
 {
     const float4 v = load4_nt_tail<0>(x, i0, n);
     RangeI rg;
     rg.add4(v);
     const bool fast = (VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2));
     uint4 m = make_uint4(0u, 0u, 0u, 0u);
+    uint4 c = make_uint4(0u, 0u, 0u, 0u);
     gc_f2 q01, q23;
     float4 ql;
     if (fast) {
@@ -177,21 +249,41 @@ __device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_
         ql = quot4_exact(v, dv);
     }
 #pragma unroll
-    for (int l = 1; l < NL; ++l) {
+    for (int l = CACHE ? 0 : 1; l < NL; ++l) {
         const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);  // one draw block per level, either path
+        const uint32_t sh = (uint32_t)l * cb;
         if (fast) {
             const gc_f2 S = {fa.S24[l], fa.S24[l]};
             const gc_f2 a = q01 * S, b = q23 * S;
-            m.x = ms_t(a.x, r.x) >= fa.thr ? (uint32_t)l : m.x;
-            m.y = ms_t(a.y, r.y) >= fa.thr ? (uint32_t)l : m.y;
-            m.z = ms_t(b.x, r.z) >= fa.thr ? (uint32_t)l : m.z;
-            m.w = ms_t(b.y, r.w) >= fa.thr ? (uint32_t)l : m.w;
+            const int32_t t0 = ms_t(a.x, r.x), t1 = ms_t(a.y, r.y), t2 = ms_t(b.x, r.z), t3 = ms_t(b.y, r.w);
+            if (l > 0) {
+                m.x = t0 >= fa.thr ? (uint32_t)l : m.x;
+                m.y = t1 >= fa.thr ? (uint32_t)l : m.y;
+                m.z = t2 >= fa.thr ? (uint32_t)l : m.z;
+                m.w = t3 >= fa.thr ? (uint32_t)l : m.w;
+            }
+            if constexpr (CACHE) {
+                c.x |= lane_of_t(v.x, t0, cq) << sh;
+                c.y |= lane_of_t(v.y, t1, cq) << sh;
+                c.z |= lane_of_t(v.z, t2, cq) << sh;
+                c.w |= lane_of_t(v.w, t3, cq) << sh;
+            }
         } else {
             const float s = lv.s[l];
-            m.x = xi_from_q(ql.x, s, r.x) <= lv.maxv ? (uint32_t)l : m.x;
-            m.y = xi_from_q(ql.y, s, r.y) <= lv.maxv ? (uint32_t)l : m.y;
-            m.z = xi_from_q(ql.z, s, r.z) <= lv.maxv ? (uint32_t)l : m.z;
-            m.w = xi_from_q(ql.w, s, r.w) <= lv.maxv ? (uint32_t)l : m.w;
+            const int32_t x0 = xi_from_q(ql.x, s, r.x), x1 = xi_from_q(ql.y, s, r.y);
+            const int32_t x2 = xi_from_q(ql.z, s, r.z), x3 = xi_from_q(ql.w, s, r.w);
+            if (l > 0) {
+                m.x = x0 <= lv.maxv ? (uint32_t)l : m.x;
+                m.y = x1 <= lv.maxv ? (uint32_t)l : m.y;
+                m.z = x2 <= lv.maxv ? (uint32_t)l : m.z;
+                m.w = x3 <= lv.maxv ? (uint32_t)l : m.w;
+            }
+            if constexpr (CACHE) {
+                c.x |= lane_of_q(sgn_of(v.x) * x0, cq) << sh;
+                c.y |= lane_of_q(sgn_of(v.y) * x1, cq) << sh;
+                c.z |= lane_of_q(sgn_of(v.z) * x2, cq) << sh;
+                c.w |= lane_of_q(sgn_of(v.w) * x3, cq) << sh;
+            }
         }
     }
     if (i0 + 4 > n) {
@@ -199,6 +291,8 @@ __device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_
         m.z = i0 + 2 < n ? m.z : 0u;
         m.w = i0 + 3 < n ? m.w : 0u;
     }
+    if constexpr (CACHE)
+        *cv = c;
     return m;
 }
 
@@ -245,8 +339,7 @@ __device__ __forceinline__ float pick_level(const float (&a)[GC_MAX_LEVELS], uin
 // lane value q + qmax of one fast-path element at scale S (q clamped to +-qmax)
 __device__ __forceinline__ uint32_t ms_lane(float x, float Ls, uint32_t r, int32_t qmax)
 {
-    const int32_t nq = __mul24(ms_t(Ls, r) >> 24, med3_i32(__float_as_int(x), -1, 1));  // -q
-    return (uint32_t)(qmax - min(max(nq, -qmax), qmax));
+    return lane_of_t(x, ms_t(Ls, r), qmax);
 }
 
 // lane values of 4 elements at their common levels (0 past n)
@@ -334,12 +427,15 @@ constexpr uint32_t kMsQuadsPerBlock = 64;  // word quads per block (one per lane
 // ---------------------------------------------------------------------------
 // mask encode: thermometer fields of the resolution level (compressors.py:799-807)
 // ---------------------------------------------------------------------------
-template <int LM, int KIND, int NL, int VAR = 0>
+// CBY = 0: mask only; 1 / 2: also the q cache cells (CBY bytes per element)
+template <int LM, int KIND, int NL, int VAR = 0, int CBY = 0>
 __global__ __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict__ x, uint32_t n,
                                                          const float *__restrict__ normp, LevelsArg lv, MsFastArg fa,
                                                          RngArgs rng, uint32_t M, uint32_t w, uint32_t fields,
-                                                         uint32_t *__restrict__ mask_words)
+                                                         uint32_t *__restrict__ mask_words, void *__restrict__ cache = nullptr,
+                                                         int32_t cq = 0, uint32_t cb = 0)
 {
+    static_assert(CBY == 0 || (VAR & MSV_PERTHREAD) == 0, "the q cache is written by the wave-split kernel only");
     const float norm = *normp;
     const DivNorm dv = make_div(norm);
     const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
@@ -375,7 +471,14 @@ __global__ __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict
                 const uint32_t i0 = p * M + 4u * t;
                 if (i0 >= n)
                     break;
-                mask_bits<NL>(acc, mask_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng), p * w);
+                if constexpr (CBY != 0) {
+                    uint4 cv;
+                    const uint4 m = mask_plane<KIND, NL, VAR, true>(x, n, i0, dv, lo2, hi2, lv, fa, rng, cq, cb, &cv);
+                    cache_store<CBY>(cache, i0, n, cv);
+                    mask_bits<NL>(acc, m, p * w);
+                } else {
+                    mask_bits<NL>(acc, mask_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng), p * w);
+                }
             }
         }
 #pragma unroll
@@ -443,6 +546,62 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_fast(const float *__restri
                 if (i0 >= n)
                     break;
                 const uint4 ln = select_plane<KIND, NL, VAR>(x, n, i0, mk, fd, dv, lo2, hi2, lv, fa, rng, qmax);
+                const uint32_t sh = p * wq;
+                acc.x += ln.x << sh;
+                acc.y += ln.y << sh;
+                acc.z += ln.z << sh;
+                acc.w += ln.w << sh;
+            }
+        }
+        if (wave)
+            part[wave - 1][lane] = acc;
+        __syncthreads();
+        if (wave == 0 && t < quads) {
+            const uint4 a = part[0][lane], b = part[1][lane], c = part[2][lane];
+            st_nt4u(words + 4u * t, make_uint4(acc.x + a.x + b.x + c.x, acc.y + a.y + b.y + c.y,
+                                               acc.z + a.z + b.z + c.z, acc.w + a.w + b.w + c.w));
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// select from the q cache (compressors.py:809-817 compress(mask): q[m==i] =
+// cache[i][m==i]): per element one cell and the common level, no x, no draws
+// ---------------------------------------------------------------------------
+template <int NL, int CBY>
+__device__ __forceinline__ uint4 cache_plane(const void *__restrict__ cache, uint32_t n, uint32_t i0, const MaskArg &mk,
+                                             const FastDiv &fd, uint32_t cb, uint32_t cm)
+{
+    const uint4 c = cache_load<CBY>(cache, i0, n);  // 0 past n -> lane 0
+    const uint4 m = mask_levels4_fast<NL>(mk, fd, i0);
+    return make_uint4((c.x >> (m.x * cb)) & cm, (c.y >> (m.y * cb)) & cm, (c.z >> (m.z * cb)) & cm,
+                      (c.w >> (m.w * cb)) & cm);
+}
+
+template <int LQ, int NL, int CBY>
+__global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restrict__ cache, uint32_t n, MaskArg mk,
+                                                            FastDiv fd, uint32_t Mq, uint32_t wq, uint32_t cb,
+                                                            uint32_t *__restrict__ words)
+{
+    const uint32_t cm = (1u << cb) - 1u;
+    const uint32_t quads = Mq >> 2;
+    constexpr int PW = (LQ + 3) / 4;
+    __shared__ uint4 part[3][kMsQuadsPerBlock];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
+        const uint32_t t = tb + lane;
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+        if (t < quads) {
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                const uint32_t p = wave + 4u * j;
+                if (p >= (uint32_t)LQ)
+                    break;
+                const uint32_t i0 = p * Mq + 4u * t;
+                if (i0 >= n)
+                    break;
+                const uint4 ln = cache_plane<NL, CBY>(cache, n, i0, mk, fd, cb, cm);
                 const uint32_t sh = p * wq;
                 acc.x += ln.x << sh;
                 acc.y += ln.y << sh;

@@ -4,12 +4,14 @@
 //
 // The reference materialises an L x n float32 cache of every level's
 // quantisation (compress_cache, 778-797), then a resolution mask (799-807), a
-// MIN all-reduce of the int8 mask, and a select (809-817).  Here there is no
-// cache: the mask kernel quantises every level on the fly and emits the mask
-// as thermometer lanes (field k = [m >= k], k = 1..L-1), which a SUM
-// all-reduce turns into the MIN over ranks (m = #fields whose sum == W); the
-// select kernel recomputes only the chosen level with the SAME counter-based
-// draw, so nothing but x is read twice.
+// MIN all-reduce of the int8 mask, and a select (809-817).  Here the mask
+// kernel quantises every level on the fly and emits the mask as thermometer
+// lanes (field k = [m >= k], k = 1..L-1), which a SUM all-reduce turns into
+// the MIN over ranks (m = #fields whose sum == W).  The select then either
+// recomputes the chosen level with the SAME counter-based draw (x read
+// twice), or — gc_ms_*_cached, dense fast path — reads the cache the mask
+// kernel wrote as one 1-2 byte cell per element (every level's lane value):
+// 40 + 16 us instead of 24 + 36 us at 23.5M floats (profiles/r01s_lab_ms.log).
 #include "gc_device.h"
 #include "gc_host.h"
 #include "segments.h"
@@ -311,6 +313,30 @@ static unsigned ms_grid(uint64_t quads)
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, 65535));
 }
 
+// q cache geometry (ms_fast.h): cell bytes per element (0 = not supported:
+// outside the dense fast path, or the count fields of cb bits exceed 16 bits)
+struct CacheGeom {
+    uint32_t bytes, cb;
+    int32_t qmax;
+};
+
+static CacheGeom ms_cache_geom(uint64_t n, const gc_levels *lv)
+{
+    CacheGeom g{0, 0, 0};
+    gc_lanes ql;
+    if (!ms_fast_ok(0, n, lv) || gc_ms_layout(n, lv, 1, &ql) != GC_OK)
+        return g;
+    const uint64_t span = 2ull * ql.offset;  // lane values 0 .. 2 qmax
+    uint32_t cb = 0;
+    while ((span >> cb) != 0)
+        ++cb;
+    const uint32_t bits = cb * lv->count;
+    g.bytes = bits <= 8 ? 1u : (bits <= 16 ? 2u : 0u);
+    g.cb = cb;
+    g.qmax = (int32_t)ql.offset;
+    return g;
+}
+
 #define GC_DISPATCH_L2(L, ...)                                                   \
     switch (L) {                                                                 \
     case 1: { constexpr int LL = 1; __VA_ARGS__; } break;                        \
@@ -360,7 +386,7 @@ int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const floa
 #define GC_MF(KIND_, NL_)                                                                                            \
     GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_fast<LL, KIND_, NL_>), dim3(g), dim3(kBlock), 0, \
                                                             st, x, (uint32_t)n, norm, la, fa, ra, (uint32_t)M, w,  \
-                                                            fields, mask_words))
+                                                            fields, mask_words, (void *)nullptr, 0, 0u))
         if (levels->count == 2) {
             if (rng->kind == GC_RNG_PHILOX) { GC_MF(0, 2); } else { GC_MF(1, 2); }
         } else {
@@ -423,6 +449,88 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
     }
 #undef GC_SE
     return launch_status("gc_ms_select_encode");
+}
+
+int gc_ms_cache_bytes(uint64_t n, const gc_levels *levels, uint32_t *bytes_per_element)
+{
+    int rc = check_levels(levels, "gc_ms_cache_bytes");
+    if (rc)
+        return rc;
+    GC_REQUIRE(bytes_per_element, "gc_ms_cache_bytes: null output");
+    *bytes_per_element = levels->count >= 2 ? ms_cache_geom(n, levels).bytes : 0u;
+    return GC_OK;
+}
+
+int gc_ms_mask_encode_cached(const float *x, uint64_t n, const float *norm, const gc_levels *levels,
+                             const gc_rng *rng, const gc_lanes *mask_lanes, uint32_t *mask_words, void *cache,
+                             gc_stream_t stream)
+{
+    const char *what = "gc_ms_mask_encode_cached";
+    int rc;
+    if ((rc = check_levels(levels, what)) || (rc = check_rng_ms(rng, what)) ||
+        (rc = check_mask_lanes(mask_lanes, levels, n, what)))
+        return rc;
+    const CacheGeom cg = ms_cache_geom(n, levels);
+    GC_REQUIRE(cg.bytes, "%s: no q cache for these levels / n (gc_ms_cache_bytes == 0)", what);
+    GC_REQUIRE(norm && mask_words && (n == 0 || (x && cache)), "%s: null pointer", what);
+    GC_REQUIRE(aligned16(mask_words) && (n == 0 || (aligned16(x) && aligned16(cache))),
+               "%s: x, mask_words and cache must be 16-byte aligned", what);
+    if (mask_lanes->plane_words == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const LevelsArg la = levels_arg(levels);
+    const RngArgs ra = rng_args_ms(rng, n);
+    const MsFastArg fa = ms_fast_arg(levels);
+    const uint32_t M = (uint32_t)mask_lanes->plane_words, w = mask_lanes->bits, fields = levels->count - 1;
+    const unsigned g = ms_grid(M >> 2);
+#define GC_MFC(KIND_, NL_, CBY_)                                                                                      \
+    GC_DISPATCH_L2(mask_lanes->per_word,                                                                             \
+                   hipLaunchKernelGGL((k_ms_mask_fast<LL, KIND_, NL_, 0, CBY_>), dim3(g), dim3(kBlock), 0, st, x,     \
+                                      (uint32_t)n, norm, la, fa, ra, M, w, fields, mask_words, cache, cg.qmax, cg.cb))
+#define GC_MFC_K(NL_, CBY_) \
+    if (rng->kind == GC_RNG_PHILOX) { GC_MFC(0, NL_, CBY_); } else { GC_MFC(1, NL_, CBY_); }
+    if (levels->count == 2) {
+        if (cg.bytes == 1) { GC_MFC_K(2, 1) } else { GC_MFC_K(2, 2) }
+    } else {
+        if (cg.bytes == 1) { GC_MFC_K(3, 1) } else { GC_MFC_K(3, 2) }
+    }
+#undef GC_MFC_K
+#undef GC_MFC
+    return launch_status(what);
+}
+
+int gc_ms_select_cached(const void *cache, uint64_t n, const gc_levels *levels, const uint32_t *mask_words,
+                        const gc_lanes *mask_lanes, const gc_lanes *q_lanes, uint32_t *words, gc_stream_t stream)
+{
+    const char *what = "gc_ms_select_cached";
+    int rc;
+    if ((rc = check_levels(levels, what)) || (rc = check_mask_lanes(mask_lanes, levels, n, what)) ||
+        (rc = check_q_lanes(q_lanes, levels, n, what)))
+        return rc;
+    const CacheGeom cg = ms_cache_geom(n, levels);
+    GC_REQUIRE(cg.bytes, "%s: no q cache for these levels / n (gc_ms_cache_bytes == 0)", what);
+    GC_REQUIRE(mask_words && words && (n == 0 || cache), "%s: null pointer", what);
+    GC_REQUIRE(aligned16(words) && aligned16(mask_words) && (n == 0 || aligned16(cache)),
+               "%s: words, mask_words and cache must be 16-byte aligned", what);
+    if (q_lanes->plane_words == 0)
+        return GC_OK;
+    GC_REQUIRE(mask_lanes->plane_words >= 2 && mask_lanes->plane_words < (1ull << 32), "%s: mask stream size", what);
+    hipStream_t st = as_stream(stream);
+    const MaskArg mk = mask_arg(mask_words, mask_lanes, levels->count);
+    const FastDiv fd = make_fastdiv((uint32_t)mask_lanes->plane_words);
+    const uint32_t Mq = (uint32_t)q_lanes->plane_words;
+    const unsigned g = ms_grid(Mq >> 2);
+#define GC_SC(NL_, CBY_)                                                                                            \
+    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_cache<LL, NL_, CBY_>), dim3(g), dim3(kBlock), 0, \
+                                                         st, cache, (uint32_t)n, mk, fd, Mq, q_lanes->bits, cg.cb,    \
+                                                         words))
+    if (levels->count == 2) {
+        if (cg.bytes == 1) { GC_SC(2, 1); } else { GC_SC(2, 2); }
+    } else {
+        if (cg.bytes == 1) { GC_SC(3, 1); } else { GC_SC(3, 2); }
+    }
+#undef GC_SC
+    return launch_status(what);
 }
 
 static int ms_decode(const char *what, const uint32_t *words, const uint32_t *mask_words, const int64_t *idx,

@@ -302,7 +302,17 @@ def lane_unpack(words, lanes, out=None):
 # ---------------------------------------------------------------------------
 # multi-scale packed
 # ---------------------------------------------------------------------------
-def ms_mask_encode(x, norm, levels, rng, world=1, idx=None, out=None):
+def ms_cache_bytes(n: int, levels) -> int:
+    """Bytes per element of the packed q cache for these levels (0: none)."""
+    lv = levels_struct(levels)
+    b = C.c_uint32(0)
+    check(_lib.load().gc_ms_cache_bytes(n, C.byref(lv), C.byref(b)), "gc_ms_cache_bytes")
+    return int(b.value)
+
+
+def ms_mask_encode(x, norm, levels, rng, world=1, idx=None, out=None, cache=None):
+    """Thermometer mask lanes; with `cache` (uint8, n * ms_cache_bytes) also the
+    packed q cache that ms_select_encode(..., cache=cache) reads instead of x."""
     dev = _dev(x)
     x = _f32(x, "ms_mask_encode")
     idx = _idx(idx, dev)
@@ -313,21 +323,35 @@ def ms_mask_encode(x, norm, levels, rng, world=1, idx=None, out=None):
     if out is None:
         out = torch.empty(mask_words_total(ml, levels), dtype=torch.int32, device=dev)
     r = rng.struct()
+    if cache is not None:
+        if idx is not None:
+            raise _lib.GCodecError(_lib.GC_EINVAL, "ms_mask_encode: the q cache needs a dense x (no idx)")
+        check(_lib.load().gc_ms_mask_encode_cached(_p(x), n, _p(nt), C.byref(lv), C.byref(r), C.byref(ml), _p(out),
+                                                   _p(cache), _stream(dev)), "gc_ms_mask_encode_cached")
+        return out
     check(_lib.load().gc_ms_mask_encode(_p(x), _p(idx), n, _p(nt), C.byref(lv), C.byref(r), C.byref(ml), _p(out),
                                         _stream(dev)), "gc_ms_mask_encode")
     return out
 
 
-def ms_select_encode(x, norm, levels, rng, mask_words, world=1, idx=None, out=None):
+def ms_select_encode(x, norm, levels, rng, mask_words, world=1, idx=None, out=None, cache=None):
+    """Packed q at the common levels of the W-summed mask; with `cache` (written
+    by ms_mask_encode for this x, norm and rng) from the cache cells."""
     dev = _dev(x)
     x = _f32(x, "ms_select_encode")
     idx = _idx(idx, dev)
     n = idx.numel() if idx is not None else x.numel()
     ql, ml = ms_layouts(n, levels, world)
     lv = levels_struct(levels)
-    nt = norm_tensor(norm, dev)
     if out is None:
         out = torch.empty(ql.plane_words, dtype=torch.int32, device=dev)
+    if cache is not None:
+        if idx is not None:
+            raise _lib.GCodecError(_lib.GC_EINVAL, "ms_select_encode: the q cache needs a dense x (no idx)")
+        check(_lib.load().gc_ms_select_cached(_p(cache), n, C.byref(lv), _p(mask_words), C.byref(ml), C.byref(ql),
+                                              _p(out), _stream(dev)), "gc_ms_select_cached")
+        return out
+    nt = norm_tensor(norm, dev)
     r = rng.struct()
     check(_lib.load().gc_ms_select_encode(_p(x), _p(idx), n, _p(nt), C.byref(lv), C.byref(r), _p(mask_words),
                                           C.byref(ml), C.byref(ql), _p(out), _stream(dev)), "gc_ms_select_encode")

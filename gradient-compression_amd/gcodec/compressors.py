@@ -77,20 +77,77 @@ class GlobalRandKMaxNormCompressor(QSGDMaxNormCompressor):
     """compressors.py:419-456 — the same arithmetic applied to the K-subset."""
 
 
-class QSGDMaxNormTwoScaleCompressor(_Base):
+class _MultiScalePacked(_Base):
+    """Packed mask + select of the two-scale and multi-scale classes.
+
+    The reference splits the work as compress_cache (every level's sign*xi
+    into an L x n float32 cache) -> compress_mask -> MIN all-reduce ->
+    compress(mask), which reads the cache (compressors.py:778-817).  Here
+    encode_mask writes the thermometer mask lanes and, when the backend has a
+    packed form of the cache for these levels (codec.ms_cache_bytes > 0: dense
+    x, 2-3 levels of <= 7 bits), the cache as one 1-2 byte cell per element;
+    encode then reads the cells at the common level instead of x and the
+    draws.  Without a cache encode recomputes the chosen level from the same
+    reserved draws.  Either way the words are identical."""
+
+    def __init__(self, device, generator=None, q_cache=True):
+        super().__init__(device, generator)
+        self.q_cache = q_cache
+        self._rng = None
+        self._cache = None
+        self._cache_key = None
+
+    def _packed_levels(self):
+        raise NotImplementedError
+
+    def _cache_buffer(self, tensor, n, idx, levels):
+        nbytes = getattr(self.backend, "ms_cache_bytes", None)
+        if not self.q_cache or nbytes is None or idx is not None or tensor.data_ptr() % 16:
+            return None
+        nb = nbytes(n, levels)
+        if not nb:
+            return None
+        if self._cache is None or self._cache.numel() < n * nb or self._cache.device != tensor.device:
+            self._cache = torch.empty(n * nb, dtype=torch.uint8, device=tensor.device)
+        return self._cache
+
+    def encode_mask(self, norm, tensor, world=1, idx=None):
+        levels = self._packed_levels()
+        n = idx.numel() if idx is not None else tensor.numel()
+        self._rng = self._reserve(n, len(levels), tensor.device)
+        self._cache_key = None
+        cache = self._cache_buffer(tensor, n, idx, levels)
+        if cache is None:
+            return self.backend.ms_mask_encode(tensor, norm, levels, self._rng, world, idx)
+        self._cache_key = (tensor.data_ptr(), n)
+        return self.backend.ms_mask_encode(tensor, norm, levels, self._rng, world, cache=cache)
+
+    def encode(self, norm, tensor, mask_words, world=1, idx=None):
+        levels = self._packed_levels()
+        n = idx.numel() if idx is not None else tensor.numel()
+        if idx is None and self._cache_key == (tensor.data_ptr(), n):
+            return self.backend.ms_select_encode(tensor, norm, levels, self._rng, mask_words, world,
+                                                 cache=self._cache)
+        return self.backend.ms_select_encode(tensor, norm, levels, self._rng, mask_words, world, idx)
+
+
+class QSGDMaxNormTwoScaleCompressor(_MultiScalePacked):
     """compressors.py:612-680.  compress_lower consumes draws [0, n) and
     compress_higher [n, 2n) of one reservation (level 0 / level 1)."""
 
-    def __init__(self, device, lower_quantization_level=6, higher_quantization_level=10, generator=None):
-        super().__init__(device, generator)
+    def __init__(self, device, lower_quantization_level=6, higher_quantization_level=10, generator=None,
+                 q_cache=True):
+        super().__init__(device, generator, q_cache)
         self._lower_quantization_level = lower_quantization_level
         self._higher_quantization_level = higher_quantization_level
         self._dtype = _qdtype(lower_quantization_level)
-        self._rng = None
 
     @property
     def levels(self):
         return [self._lower_quantization_level, self._higher_quantization_level]
+
+    def _packed_levels(self):
+        return self.levels
 
     def compress_lower(self, norm, tensor):
         self._rng = self._reserve(tensor.numel(), 2, tensor.device)
@@ -107,15 +164,7 @@ class QSGDMaxNormTwoScaleCompressor(_Base):
     def decompress(self, norm, sign_xi_array, higher_resolution_mask):
         return self.backend.ms_dequantize(sign_xi_array, higher_resolution_mask, norm, self.levels, order=1)
 
-    # packed: mask + select over the two levels (thermometer mask lanes)
-    def encode_mask(self, norm, tensor, world=1, idx=None):
-        n = idx.numel() if idx is not None else tensor.numel()
-        self._rng = self._reserve(n, 2, tensor.device)
-        return self.backend.ms_mask_encode(tensor, norm, self.levels, self._rng, world, idx)
-
-    def encode(self, norm, tensor, mask_words, world=1, idx=None):
-        return self.backend.ms_select_encode(tensor, norm, self.levels, self._rng, mask_words, world, idx)
-
+    # packed: encode_mask / encode (_MultiScalePacked) over the two levels
     def decode(self, norm, words, mask_words, n, world=1, alpha=1.0, idx=None, out=None):
         return self.backend.ms_decode(words, mask_words, n, norm, self.levels, world, 1, alpha, idx, out)
 
@@ -127,19 +176,23 @@ class GlobalRandKMaxNormTwoScaleCompressor(QSGDMaxNormTwoScaleCompressor):
     """compressors.py:683-751 — identical arithmetic on the K-subset."""
 
 
-class QSGDMaxNormMultiScaleCompressor(_Base):
-    """compressors.py:754-826.  No L x n float cache: the select pass
-    recomputes the chosen level from the same reserved draws."""
+class QSGDMaxNormMultiScaleCompressor(_MultiScalePacked):
+    """compressors.py:754-826.  Unpacked forms: no L x n float cache, the
+    select pass recomputes the chosen level from the same reserved draws.
+    Packed forms: the cache as 1-2 byte cells where the levels allow it
+    (_MultiScalePacked)."""
 
-    def __init__(self, device, quantization_levels=None, generator=None):
-        super().__init__(device, generator)
+    def __init__(self, device, quantization_levels=None, generator=None, q_cache=True):
+        super().__init__(device, generator, q_cache)
         if not quantization_levels:
             quantization_levels = [6, 10]
         self._quantization_levels = sorted(quantization_levels)
         self._dtype = _qdtype(self._quantization_levels[0])
-        self._rng = None
         self._x = None
         self._norm = None
+
+    def _packed_levels(self):
+        return self._quantization_levels
 
     def compress_cache(self, norm, tensor):
         self._rng = self._reserve(tensor.numel(), len(self._quantization_levels), tensor.device)
@@ -156,16 +209,7 @@ class QSGDMaxNormMultiScaleCompressor(_Base):
     def decompress(self, norm, sign_xi_array, resolution_mask):
         return self.backend.ms_dequantize(sign_xi_array, resolution_mask, norm, self._quantization_levels, order=0)
 
-    # packed
-    def encode_mask(self, norm, tensor, world=1, idx=None):
-        n = idx.numel() if idx is not None else tensor.numel()
-        self._rng = self._reserve(n, len(self._quantization_levels), tensor.device)
-        return self.backend.ms_mask_encode(tensor, norm, self._quantization_levels, self._rng, world, idx)
-
-    def encode(self, norm, tensor, mask_words, world=1, idx=None):
-        return self.backend.ms_select_encode(tensor, norm, self._quantization_levels, self._rng, mask_words, world,
-                                             idx)
-
+    # packed: encode_mask / encode (_MultiScalePacked)
     def decode(self, norm, words, mask_words, n, world=1, alpha=1.0, idx=None, out=None):
         return self.backend.ms_decode(words, mask_words, n, norm, self._quantization_levels, world, 0, alpha, idx,
                                       out)

@@ -25,6 +25,7 @@
  *   gc_ms_mask_encode ........ compressors.py:778-807 compress_cache + compress_mask
  *                              (= TwoScale compress_lower/compress_higher 630-666 for 2 levels)
  *   gc_ms_select_encode ...... compressors.py:809-817 compress(mask) (+ reducer.py:1503-1505 blend)
+ *   gc_ms_*_cached ........... the same pair with compressors.py:778-797's cache kept (packed cells)
  *   gc_ms_decode ............. compressors.py:819-826 (order 0) / 668-680 (order 1)
  *   gc_mt19937_seed/_generate  seed.py:6-11 torch.manual_seed + torch CPU generator stream
  *                              consumed by torch.bernoulli (compressors.py:310)
@@ -214,6 +215,21 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
                         const gc_levels *levels, const gc_rng *rng, const uint32_t *mask_words,
                         const gc_lanes *mask_lanes, const gc_lanes *q_lanes, uint32_t *words,
                         gc_stream_t stream);
+/* q cache — compressors.py:778-797 compress_cache (every level's sign*xi, kept
+ * between compress_mask and compress) in packed form: one cell of
+ * *bytes_per_element (1 or 2) bytes per element holding every level's select
+ * lane.  0 when these levels / n have no cache form (dense fast path only: 2 or
+ * 3 levels of <= 7 bits, n < 2^32, count * bit_length(2 qmax) <= 16). */
+int gc_ms_cache_bytes(uint64_t n, const gc_levels *levels, uint32_t *bytes_per_element);
+/* gc_ms_mask_encode (dense, 16-byte aligned x) that also writes the cells into
+ * cache[n * bytes_per_element] (16-byte aligned) */
+int gc_ms_mask_encode_cached(const float *x, uint64_t n, const float *norm, const gc_levels *levels,
+                             const gc_rng *rng, const gc_lanes *mask_lanes, uint32_t *mask_words, void *cache,
+                             gc_stream_t stream);
+/* gc_ms_select_encode from the cells instead of x and the draws: the same words
+ * bit for bit for the x / norm / rng the cache was written with */
+int gc_ms_select_cached(const void *cache, uint64_t n, const gc_levels *levels, const uint32_t *mask_words,
+                        const gc_lanes *mask_lanes, const gc_lanes *q_lanes, uint32_t *words, gc_stream_t stream);
 /* order 0: RN(RN(Q*norm)/s_m) (multi-scale); order 1: RN(RN(norm/s_m)*Q) (two-scale); then *alpha */
 int gc_ms_decode(const uint32_t *words, const uint32_t *mask_words, const int64_t *idx, uint64_t n,
                  const float *norm, const gc_levels *levels, const gc_lanes *mask_lanes,

@@ -404,8 +404,68 @@ def test_ms_fast_path_edges_vs_oracle(levels, world):
             assert bits_eq(u32(d), ref.view(np.uint32)), (order, float(norm))
 
 
+@pytest.mark.parametrize("levels,cell", [((2, 4), 1), ((1, 3), 1), ((3, 7), 1), ((1, 2, 3), 2), ((2, 4, 6), 2),
+                                         ((4, 7), 2), ((3, 4, 5), 2), ((5, 6, 7), 0), ((2, 8), 0)])
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_ms_q_cache_vs_oracle(levels, cell, world):
+    """q cache (compress_cache kept as packed cells): the cached mask kernel
+    writes the same mask words, and the select from the cells equals the oracle
+    at a COMMON mask below this rank's own levels (other ranks' inputs force
+    lower levels), on level-boundary values, +-norm, zeros and subnormal tiles,
+    inside and outside the Markstein range."""
+    n = 3 * 4 * 4096 + 7
+    assert codec.ms_cache_bytes(n, levels) == cell
+    if not cell:
+        return
+    L = len(levels)
+    for norm0 in (np.float32(0.05), np.float32(3.0), np.float32(2.0**-110)):
+        s = (1 << levels[-1]) - 1
+        x = _int_path_input(n, norm0, s, seed=world + 5 * L)
+        s0 = (1 << levels[0]) - 1
+        k = np.random.default_rng(L).integers(-s0, s0 + 1, n // 3).astype(np.float32)
+        x[: n // 3] = np.clip((k * np.float32(norm0)) / np.float32(s0), -norm0, norm0)
+        other = np.random.default_rng(world).permutation(x)  # another rank's bucket
+        norm = max(O.absmax(x), O.absmax(other))
+        r = gcodec.rng.Reservation(0, 71 + L, 4, None, n, L)
+        r2 = gcodec.rng.Reservation(0, 72 + L, 4, None, n, L)
+        xd = dev(x)
+        cache = torch.empty(n * cell, dtype=torch.uint8, device=DEV)
+        mw = codec.ms_mask_encode(xd, float(norm), levels, r, world, cache=cache)
+        assert bits_eq(u32(mw), u32(codec.ms_mask_encode(xd, float(norm), levels, r, world)))
+        mw_other = codec.ms_mask_encode(dev(other), float(norm), levels, r2, world)
+        mw_sum = (mw.to(torch.int64) + mw_other.to(torch.int64) * (world - 1)).to(torch.int32)
+        m_common = codec.ms_mask_unpack(mw_sum, n, levels, world).cpu().numpy().astype(np.uint8)
+        m_own = O.ms_mask(x, norm, levels, O.philox_rng(71 + L, 4))
+        assert np.all(m_common <= m_own)
+        if world > 1:
+            assert np.any(m_common < m_own)
+        words = codec.ms_select_encode(xd, float(norm), levels, r, mw_sum, world, cache=cache)
+        q_ref = O.ms_select(x, norm, levels, O.philox_rng(71 + L, 4), m_common)
+        ql, _ = codec.ms_layouts(n, levels, world)
+        assert bits_eq(u32(words), O.lane_pack(q_ref, ql.offset, ql.bits, ql.per_word, ql.plane_words))
+        assert bits_eq(u32(words), u32(codec.ms_select_encode(xd, float(norm), levels, r, mw_sum, world)))
+
+
+def test_ms_compressor_uses_q_cache():
+    """the packed compressors take the cache path for cacheable levels and
+    give the same words as with q_cache=False."""
+    n = 100_003
+    x = dev(O.gen_input(n, seed=3, kind=1))
+    for cls, kw in ((gcodec.QSGDMaxNormTwoScaleCompressor, dict(lower_quantization_level=2,
+                                                                 higher_quantization_level=4)),
+                    (gcodec.QSGDMaxNormMultiScaleCompressor, dict(quantization_levels=[4, 2]))):
+        out = []
+        for qc in (True, False):
+            c = cls(DEV, generator=gcodec.Generator(9, "philox"), q_cache=qc, **kw)
+            norm = codec.absmax(x)
+            m = c.encode_mask(norm, x, 2)
+            assert (c._cache_key is not None) == qc
+            out.append((u32(m), u32(c.encode(norm, x, (m.to(torch.int64) * 2).to(torch.int32), 2))))
+        assert bits_eq(out[0][0], out[1][0]) and bits_eq(out[0][1], out[1][1])
+
+
 # --------------------------------------------------------------------------- GRandK
-@pytest.mark.parametrize("case", ["n20011_k1000", "n5000_k5000", "n3001_k1000"])
+@pytest.mark.parametrize("case",["n20011_k1000", "n5000_k5000", "n3001_k1000"])
 def test_grandk_torch_mode_matches_reference(case):
     z = gz("randk.npz")
     buf, idx, norm, q = (z[f"{case}/{k}"] for k in ("buf", "idx", "norm", "q"))

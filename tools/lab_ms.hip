@@ -126,6 +126,47 @@ static unsigned grid(uint64_t quads, unsigned cap = 16384)
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, cap));
 }
 
+// select from the q cache without the mask words (every element at level 1):
+// the cost of the W-summed mask reads in k_ms_select_cache
+__global__ __launch_bounds__(256) void k_sel_cache_nomask(const uint8_t *__restrict__ cache, uint32_t n, uint32_t Mq,
+                                                          uint32_t wq, uint32_t cb, uint32_t *__restrict__ words)
+{
+    const uint32_t cm = (1u << cb) - 1u, quads = Mq >> 2;
+    __shared__ uint4 part[3][64];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (uint32_t tb = blockIdx.x * 64; tb < quads; tb += gridDim.x * 64) {
+        const uint32_t t = tb + lane;
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+        if (t < quads) {
+            for (int j = 0; j < 3; ++j) {
+                const uint32_t p = wave + 4u * j;
+                if (p >= 10u)
+                    break;
+                const uint32_t i0 = p * Mq + 4u * t;
+                if (i0 >= n)
+                    break;
+                const uint4 c = cache_load<1>(cache, i0, n);
+                const uint32_t sh = p * wq;
+                acc.x += ((c.x >> cb) & cm) << sh;
+                acc.y += ((c.y >> cb) & cm) << sh;
+                acc.z += ((c.z >> cb) & cm) << sh;
+                acc.w += ((c.w >> cb) & cm) << sh;
+            }
+        }
+        if (wave)
+            part[wave - 1][lane] = acc;
+        __syncthreads();
+        if (wave == 0 && t < quads) {
+            const uint4 a = part[0][lane], b = part[1][lane], c = part[2][lane];
+            words[4 * t] = acc.x + a.x + b.x + c.x;
+            words[4 * t + 1] = acc.y + a.y + b.y + c.y;
+            words[4 * t + 2] = acc.z + a.z + b.z + c.z;
+            words[4 * t + 3] = acc.w + a.w + b.w + c.w;
+        }
+        __syncthreads();
+    }
+}
+
 int main(int argc, char **argv)
 {
     const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 23520842ull;
@@ -187,7 +228,7 @@ int main(int argc, char **argv)
     auto v_mask = [&](auto kern, uint32_t *dst) {
         return [=] {
             hipLaunchKernelGGL(kern, dim3(grid(Mm / 4)), dim3(256), 0, 0, x, n32, norm, la, fa, ra, Mm, ml.bits,
-                               lv.count - 1, dst);
+                               lv.count - 1, dst, (void *)nullptr, 0, 0u);
         };
     };
     auto v_sel = [&](auto kern, uint32_t *dst) {
@@ -199,7 +240,7 @@ int main(int argc, char **argv)
     auto v_mask64 = [&](auto kern, uint32_t *dst) {
         return [=] {
             hipLaunchKernelGGL(kern, dim3((Mm / 4 + 63) / 64), dim3(256), 0, 0, x, n32, norm, la, fa, ra, Mm, ml.bits,
-                               lv.count - 1, dst);
+                               lv.count - 1, dst, (void *)nullptr, 0, 0u);
         };
     };
     auto v_sel64 = [&](auto kern, uint32_t *dst) {
@@ -269,6 +310,33 @@ int main(int argc, char **argv)
     vs.push_back({"lab select split NOSLOW", v_sel64(k_ms_select_fast<10, 0, 2, MSV_NOSLOW>, wq2), xb + mb + qb, {}});
     vs.push_back({"lab select split NORNG|NOSLOW", v_sel64(k_ms_select_fast<10, 0, 2, MSV_NORNG | MSV_NOSLOW>, wq2), xb + mb + qb, {}});
     vs.push_back({"lab select PERTHREAD", v_sel(k_ms_select_fast<10, 0, 2, MSV_PERTHREAD>, wq2), xb + mb + qb, {}});
+    // q cache (1 byte per element for [2, 4])
+    uint32_t cby = 0;
+    GK(gc_ms_cache_bytes(n, &lv, &cby));
+    uint8_t *cache;
+    CK(hipMalloc(&cache, n * cby + 64));
+    const double cbytes = (double)n * cby;
+    auto p_maskc = [&] { GK(gc_ms_mask_encode_cached(x, n, norm, &lv, &rng, &ml, mw2, cache, nullptr)); };
+    auto p_selc = [&] { GK(gc_ms_select_cached(cache, n, &lv, mw, &ml, &ql, wq2, nullptr)); };
+    p_maskc();
+    cmp("cached mask", mw, mw2, (size_t)Mm * 4);
+    p_selc();
+    cmp("select from cache", wq, wq2, (size_t)Mq * 4);
+    auto v_maskc = [&](auto kern) {
+        return [=] {
+            hipLaunchKernelGGL(kern, dim3((Mm / 4 + 63) / 64), dim3(256), 0, 0, x, n32, norm, la, fa, ra, Mm, ml.bits,
+                               lv.count - 1, mw2, (void *)cache, qmax, 3u);
+        };
+    };
+    vs.push_back({"product mask encode + cache", p_maskc, xb + mb + cbytes, {}});
+    vs.push_back({"lab mask + cache NORNG", v_maskc(k_ms_mask_fast<32, 0, 2, MSV_NORNG, 1>), xb + mb + cbytes, {}});
+    vs.push_back({"lab mask + cache NORNG|NOSLOW", v_maskc(k_ms_mask_fast<32, 0, 2, MSV_NORNG | MSV_NOSLOW, 1>),
+                  xb + mb + cbytes, {}});
+    vs.push_back({"product select from cache", p_selc, cbytes + mb + qb, {}});
+    vs.push_back({"lab select from cache, no mask reads", [&] {
+                      hipLaunchKernelGGL(k_sel_cache_nomask, dim3((Mq / 4 + 63) / 64), dim3(256), 0, 0, cache, n32, Mq,
+                                         ql.bits, 3u, wq2);
+                  }, cbytes + qb, {}});
     vs.push_back({"product decode order 0", p_dec(0), xb + mb + qb, {}});
     vs.push_back({"product decode order 1", p_dec(1), xb + mb + qb, {}});
     vs.push_back({"product absmax", [&] { gc_absmax_f32(x, nullptr, n, norm, nullptr, nullptr); }, xb, {}});
