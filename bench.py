@@ -132,8 +132,8 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     gen = gcodec.Generator(5 + rank, "philox")
     for tag, ms in (("twoscale_2_4", gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen)),
                     ("multiscale_2_4", gcodec.QSGDMaxNormMultiScaleCompressor(dev, [2, 4], generator=gen)),
-                    ("twoscale_2_4_no_q_cache",
-                     gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen, q_cache=False))):
+                    ("twoscale_2_4_q_cache",
+                     gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen, q_cache=True))):
         nrm = torch.empty(1, device=dev)
         holder = {}
 

@@ -569,16 +569,6 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_fast(const float *__restri
 // select from the q cache (compressors.py:809-817 compress(mask): q[m==i] =
 // cache[i][m==i]): per element one cell and the common level, no x, no draws
 // ---------------------------------------------------------------------------
-template <int NL, int CBY>
-__device__ __forceinline__ uint4 cache_plane(const void *__restrict__ cache, uint32_t n, uint32_t i0, const MaskArg &mk,
-                                             const FastDiv &fd, uint32_t cb, uint32_t cm)
-{
-    const uint4 c = cache_load<CBY>(cache, i0, n);  // 0 past n -> lane 0
-    const uint4 m = mask_levels4_fast<NL>(mk, fd, i0);
-    return make_uint4((c.x >> (m.x * cb)) & cm, (c.y >> (m.y * cb)) & cm, (c.z >> (m.z * cb)) & cm,
-                      (c.w >> (m.w * cb)) & cm);
-}
-
 template <int LQ, int NL, int CBY>
 __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restrict__ cache, uint32_t n, MaskArg mk,
                                                             FastDiv fd, uint32_t Mq, uint32_t wq, uint32_t cb,
@@ -593,20 +583,46 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
         const uint32_t t = tb + lane;
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
         if (t < quads) {
+            // every plane's cells and mask words are loaded before any is used
+            // (short, latency-bound planes: no load -> use -> load chains)
+            uint4 c[PW], mw[PW][NL - 1];
+            uint32_t shm[PW];
 #pragma unroll
             for (int j = 0; j < PW; ++j) {
                 const uint32_t p = wave + 4u * j;
-                if (p >= (uint32_t)LQ)
-                    break;
                 const uint32_t i0 = p * Mq + 4u * t;
-                if (i0 >= n)
-                    break;
-                const uint4 ln = cache_plane<NL, CBY>(cache, n, i0, mk, fd, cb, cm);
-                const uint32_t sh = p * wq;
-                acc.x += ln.x << sh;
-                acc.y += ln.y << sh;
-                acc.z += ln.z << sh;
-                acc.w += ln.w << sh;
+                c[j] = make_uint4(0u, 0u, 0u, 0u);
+                shm[j] = 0;
+#pragma unroll
+                for (int f = 0; f < NL - 1; ++f)
+                    mw[j][f] = make_uint4(0u, 0u, 0u, 0u);
+                if (p < (uint32_t)LQ && i0 < n) {
+                    c[j] = cache_load<CBY>(cache, i0, n);
+                    const uint32_t plane = fdiv(i0, fd);
+                    const uint32_t pos = i0 - plane * fd.d;
+                    shm[j] = plane * mk.w;
+#pragma unroll
+                    for (int f = 0; f < NL - 1; ++f)
+                        mw[j][f] = *reinterpret_cast<const uint4 *>(mk.words + (uint64_t)f * mk.M + pos);
+                }
+            }
+            const uint32_t msk = (1u << mk.w) - 1u;
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                uint4 m = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+                for (int f = 0; f < NL - 1; ++f) {  // common level = #fields whose W-sum == W (mask_levels4_fast)
+                    m.x += ((mw[j][f].x >> shm[j]) & msk) == mk.world;
+                    m.y += ((mw[j][f].y >> shm[j]) & msk) == mk.world;
+                    m.z += ((mw[j][f].z >> shm[j]) & msk) == mk.world;
+                    m.w += ((mw[j][f].w >> shm[j]) & msk) == mk.world;
+                }
+                const uint32_t p = wave + 4u * j;  // planes past LQ / n contribute c = 0
+                const uint32_t sh = p < (uint32_t)LQ ? p * wq : 0u;
+                acc.x += ((c[j].x >> (m.x * cb)) & cm) << sh;
+                acc.y += ((c[j].y >> (m.y * cb)) & cm) << sh;
+                acc.z += ((c[j].z >> (m.z * cb)) & cm) << sh;
+                acc.w += ((c[j].w >> (m.w * cb)) & cm) << sh;
             }
         }
         if (wave)

@@ -11,7 +11,8 @@
 // recomputes the chosen level with the SAME counter-based draw (x read
 // twice), or — gc_ms_*_cached, dense fast path — reads the cache the mask
 // kernel wrote as one 1-2 byte cell per element (every level's lane value):
-// 40 + 16 us instead of 24 + 36 us at 23.5M floats (profiles/r01s_lab_ms.log).
+// 43 + 15 us instead of 24 + 36 us at 23.5M floats, the same total: both
+// kernels are bound by the Philox draws (profiles/r01s_lab_ms.log); opt-in.
 #include "gc_device.h"
 #include "gc_host.h"
 #include "segments.h"

@@ -88,9 +88,13 @@ class _MultiScalePacked(_Base):
     x, 2-3 levels of <= 7 bits), the cache as one 1-2 byte cell per element;
     encode then reads the cells at the common level instead of x and the
     draws.  Without a cache encode recomputes the chosen level from the same
-    reserved draws.  Either way the words are identical."""
+    reserved draws.  Either way the words are identical.  Off by default
+    (q_cache=False): on MI355X both splits cost the same, because the two
+    kernels are bound by the Philox draws, not by reading x twice (config 3:
+    mask 25 + select 38 us vs 46 + 16 us with the cache, 112 us per step
+    either way; profiles/r01s_bench_cache.log, r01s_lab_ms.log)."""
 
-    def __init__(self, device, generator=None, q_cache=True):
+    def __init__(self, device, generator=None, q_cache=False):
         super().__init__(device, generator)
         self.q_cache = q_cache
         self._rng = None
@@ -136,7 +140,7 @@ class QSGDMaxNormTwoScaleCompressor(_MultiScalePacked):
     compress_higher [n, 2n) of one reservation (level 0 / level 1)."""
 
     def __init__(self, device, lower_quantization_level=6, higher_quantization_level=10, generator=None,
-                 q_cache=True):
+                 q_cache=False):
         super().__init__(device, generator, q_cache)
         self._lower_quantization_level = lower_quantization_level
         self._higher_quantization_level = higher_quantization_level
@@ -179,10 +183,10 @@ class GlobalRandKMaxNormTwoScaleCompressor(QSGDMaxNormTwoScaleCompressor):
 class QSGDMaxNormMultiScaleCompressor(_MultiScalePacked):
     """compressors.py:754-826.  Unpacked forms: no L x n float cache, the
     select pass recomputes the chosen level from the same reserved draws.
-    Packed forms: the cache as 1-2 byte cells where the levels allow it
-    (_MultiScalePacked)."""
+    Packed forms: optionally the cache as 1-2 byte cells where the levels
+    allow it (_MultiScalePacked, q_cache=True)."""
 
-    def __init__(self, device, quantization_levels=None, generator=None, q_cache=True):
+    def __init__(self, device, quantization_levels=None, generator=None, q_cache=False):
         super().__init__(device, generator, q_cache)
         if not quantization_levels:
             quantization_levels = [6, 10]
