@@ -436,6 +436,43 @@ def main():
                               "packed_bytes_per_rank": 4 * M,
                               "steps": "absmax, all_reduce MAX, encode, all_reduce SUM (RCCL), decode + 1/W"}
 
+        if world >= 4 and world % 2 == 0:
+            # the same path through gcodec.NodeTopology as if the node were 2 nodes of
+            # world/2 GPUs (intra reduce-scatter, "inter-node" all-reduce of 1/L of the
+            # words, intra all-gather): the multi-node code path on one node
+            try:
+                from gcodec.topology import NodeTopology
+                topo = NodeTopology(world // 2)
+
+                def hpath():
+                    step()
+                    topo.all_reduce(words)
+                    codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
+
+                for _ in range(2):
+                    hpath()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(K):
+                    hpath()
+                torch.cuda.synchronize()
+                dist.barrier()
+                hel = time.perf_counter() - t0
+                t = torch.tensor([hel], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                # flat vs hierarchical sum of the same encoded words
+                step()
+                a = words.clone()
+                dist.all_reduce(a)
+                step_b = words.clone()
+                topo.all_reduce(step_b)
+                hier_ok = bool(torch.equal(a, step_b))
+                out["reduce_path_2x_nodes"] = {"ms_per_step": t.item() / K * 1e3, "local_size": world // 2,
+                                               "bit_identical_to_flat": hier_ok}
+            except Exception as e:  # noqa: BLE001 — report, never fail the headline bench
+                out["reduce_path_2x_nodes"] = f"failed: {type(e).__name__}: {e}"
+
         # PCIe-inclusive: the reference's path starts and ends in host memory;
         # pinned buffers, hipMemcpyAsync (torch non_blocking copies) on the same stream
         xh = torch.empty(n, dtype=torch.float32, pin_memory=True)

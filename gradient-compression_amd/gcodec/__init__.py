@@ -26,6 +26,7 @@ from .reducer import (  # noqa: F401
 from .ddp_hook import QSGDHookState, qsgd_hook  # noqa: F401
 from .pipeline import ChunkedQSGDAllReduce  # noqa: F401
 from .rng import Generator, default_generator, manual_seed, set_mode  # noqa: F401
+from .topology import NodeTopology  # noqa: F401
 
 set_rng_mode = set_mode
 

@@ -36,9 +36,10 @@ class QSGDHookState:
     """State of qsgd_hook: quantization bits, process group, RNG, codec."""
 
     def __init__(self, bits: int = 4, process_group=None, generator: Generator | None = None, codec=None,
-                 seed: int = 42):
+                 seed: int = 42, topology=None):
         self.bits = int(bits)
         self.group = process_group
+        self.topology = topology  # NodeTopology (multi-node): two-level collectives, lanes sized for the world
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         rank = dist.get_rank(process_group) if dist.is_initialized() else 0
         self.gen = generator or Generator(seed + rank, "philox")
@@ -54,14 +55,22 @@ def qsgd_hook(state: QSGDHookState, bucket) -> torch.futures.Future:
     n = x.numel()
     codec, W = state.codec, state.world
     norm = codec.absmax(x)
+    topo = state.topology
     if W > 1:
-        dist.all_reduce(norm, op=dist.ReduceOp.MAX, group=state.group)
+        if topo is not None:
+            topo.all_reduce(norm, dist.ReduceOp.MAX)
+        else:
+            dist.all_reduce(norm, op=dist.ReduceOp.MAX, group=state.group)
     rng = state.gen.reserve(n, 1, device=x.device, backend=codec)
     words = codec.qsgd_encode(x, norm, state.bits, rng, W)
     state.buckets += 1
     state.bits_sent += 32 + 32 * words.numel()
-    if W > 1:
+    if W > 1 and topo is None:
         fut = dist.all_reduce(words, group=state.group, async_op=True).get_future()
+    elif W > 1:  # reduce-scatter / inter-node all-reduce / all-gather, enqueued in order
+        topo.all_reduce(words)
+        fut = torch.futures.Future()
+        fut.set_result([words])
     else:
         fut = torch.futures.Future()
         fut.set_result([words])

@@ -50,7 +50,7 @@ def set_seed(seed: int, generator=None):
 class Reducer:
     """reducer.py:26-43."""
 
-    def __init__(self, device, timer=None, codec=None, generator=None, group=None, fused=True):
+    def __init__(self, device, timer=None, codec=None, generator=None, group=None, fused=True, topology=None):
         if dist.is_available() and dist.is_initialized():
             self.n_workers = dist.get_world_size(group)
             self.rank = dist.get_rank(group)
@@ -62,6 +62,9 @@ class Reducer:
         self._codec = codec or _hip_codec
         self._gen = generator or default_generator
         self._group = group
+        self._topology = topology  # NodeTopology: two-level (xGMI / network) collectives
+        if topology is not None and group is not None:
+            raise ValueError("topology spans the default process group; pass one or the other")
         self._fused = fused
         self._seg_cache = {}
 
@@ -71,6 +74,8 @@ class Reducer:
     # -- collectives (RCCL over xGMI when the group is "nccl") -------------
     def _all_reduce(self, t, op=dist.ReduceOp.SUM):
         if self.n_workers > 1:
+            if self._topology is not None:  # multi-node: reduce-scatter / all-reduce / all-gather
+                return self._topology.all_reduce(t, op)
             dist.all_reduce(t, op=op, group=self._group)
         return t
 

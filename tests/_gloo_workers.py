@@ -168,3 +168,81 @@ def ddp_hook_world(rank, world, init_file, out_dir, use_gpu):
     np.savez(os.path.join(out_dir, f"h{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def topology_world(rank, world, init_file, out_dir, local_size):
+    """NodeTopology (world = nodes x local_size) against flat all-reduces:
+    int32 word sums (wrapping past 2^31, ragged lengths), MAX, and every
+    reducer with the oracle codec, hierarchical vs flat, step by step."""
+    import gcodec
+    import oracle_codec
+    from gcodec.topology import NodeTopology
+
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    topo = NodeTopology(local_size)
+    res = {}
+    g = torch.Generator().manual_seed(100 + rank)
+    for n in (1, 3, 7, 64, 1001, 4099):
+        w = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, generator=g)
+        flat = w.clone()
+        dist.all_reduce(flat)
+        hier = topo.all_reduce(w.clone())
+        res[f"sum{n}"] = np.int64((hier == flat).all().item())
+        m = torch.rand(n, generator=g)
+        mf = m.clone()
+        dist.all_reduce(mf, op=dist.ReduceOp.MAX)
+        res[f"max{n}"] = np.int64((topo.all_reduce(m.clone(), dist.ReduceOp.MAX) == mf).all().item())
+    for name in REDUCERS:
+        outs = []
+        for use_topo in (False, True):
+            gen = gcodec.Generator(0, "torch")
+            red = make_reducer(name, codec=oracle_codec, generator=gen, topology=topo if use_topo else None)
+            torch.manual_seed(SEED + rank)
+            gen.manual_seed(SEED + rank)
+            got = []
+            for step in range(2):
+                gin = [torch.randn(s, generator=torch.Generator().manual_seed(1000 * step + 10 * rank + i))
+                       for i, s in enumerate((37, 500, 1999))]
+                gout = [torch.empty_like(t) for t in gin]
+                red.reduce(gin, gout)
+                got += [t.numpy().copy() for t in gout]
+            outs.append(got)
+        res[f"red_{name}"] = np.int64(all(a.tobytes() == b.tobytes() for a, b in zip(*outs)))
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def hip_topology_world(rank, world, init_file, out_dir, local_size):
+    """NodeTopology with the HIP codec (gloo over CUDA tensors, one GPU):
+    reducers through the two-level collectives vs flat, bit for bit."""
+    import gcodec
+    from gcodec.topology import NodeTopology
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    topo = NodeTopology(local_size)
+    from gcodec import reducer as R
+
+    res = {}
+    for name, mk in (("qsgd", lambda **kw: R.QSGDMaxNormReducer(dev, None, quantization_level=4, **kw)),
+                     ("ts", lambda **kw: R.QSGDMaxNormTwoScaleReducer(dev, None, 2, 4, **kw)),
+                     ("randk", lambda **kw: R.GlobalRandKMaxNormReducer(dev, None, SEED, K=1000,
+                                                                        quantization_level=4, **kw))):
+        outs = []
+        for use_topo in (False, True):
+            gen = gcodec.Generator(SEED + rank, "philox")
+            red = mk(generator=gen, topology=topo if use_topo else None)
+            got = []
+            for step in range(2):
+                gin = [torch.randn(s, generator=torch.Generator().manual_seed(1000 * step + 10 * rank + i)).to(dev)
+                       for i, s in enumerate((37, 5000, 70001))]
+                gout = [torch.empty_like(t) for t in gin]
+                red.reduce(gin, gout)
+                got += [t.cpu().numpy() for t in gout]
+            outs.append(got)
+        res[name] = np.int64(all(a.tobytes() == b.tobytes() for a, b in zip(*outs)))
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()

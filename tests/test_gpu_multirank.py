@@ -77,3 +77,15 @@ def test_ddp_qsgd_hook_on_gpu(world):
         mp.spawn(W.ddp_hook_world, args=(world, os.path.join(td, "init"), td, True), nprocs=world, join=True)
         recs = [np.load(os.path.join(td, f"h{r}.npz"), allow_pickle=False) for r in range(world)]
         check_hook_records(recs, world)
+
+
+@pytest.mark.parametrize("world,local_size", [(2, 1), (2, 2)])
+def test_hip_reducers_through_node_topology(world, local_size):
+    """gcodec.NodeTopology (two-level collectives) with the HIP codec: the
+    reducers' gradients equal the flat all-reduce's bit for bit."""
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(W.hip_topology_world, args=(world, os.path.join(td, "init"), td, local_size), nprocs=world,
+                 join=True)
+        for r in range(world):
+            got = np.load(os.path.join(td, f"r{r}.npz"), allow_pickle=False)
+            assert got.files and all(int(got[k]) == 1 for k in got.files), (r, {k: int(got[k]) for k in got.files})
