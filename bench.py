@@ -133,7 +133,10 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     for tag, ms in (("twoscale_2_4", gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen)),
                     ("multiscale_2_4", gcodec.QSGDMaxNormMultiScaleCompressor(dev, [2, 4], generator=gen)),
                     ("twoscale_2_4_q_cache",
-                     gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen, q_cache=True))):
+                     gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen, q_cache=True)),
+                    # the (4, 8) pair of the reference's logged runs; 8 bits take the
+                    # generic kernels (the fast path needs every level <= 7 bits)
+                    ("twoscale_4_8", gcodec.QSGDMaxNormTwoScaleCompressor(dev, 4, 8, generator=gen))):
         nrm = torch.empty(1, device=dev)
         holder = {}
 
@@ -153,11 +156,12 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
         # per kernel (HIP events, W = this rank's lane sizing), algorithmic bytes per
         # mask 4n + mask words (+ q cache cells), select 4n + mask + words
         # (from the cache: cells + mask + words), decode words + mask + 4n
-        ql, ml = codec.ms_layouts(n3, [2, 4], world)
-        mwords = codec.mask_words_total(ml, [2, 4])
+        lvls = ms._packed_levels()
+        ql, ml = codec.ms_layouts(n3, lvls, world)
+        mwords = codec.mask_words_total(ml, lvls)
         m_ = ms.encode_mask(nrm, x3, world)
         cached = ms._cache_key is not None
-        cell = codec.ms_cache_bytes(n3, [2, 4]) * n3 if cached else 0
+        cell = codec.ms_cache_bytes(n3, lvls) * n3 if cached else 0
         w_ = ms.encode(nrm, x3, m_, world)
         d_ = torch.empty(n3, device=dev)
         kt = {
@@ -408,6 +412,13 @@ def main():
                                                            lanes=lanes), reps)
         out["kernels_ms"]["k_qsgd_decode"] = ms_dec
         out["decode_gbs"] = (4 * M + 4 * n) / (ms_dec * 1e-3) / 1e9
+
+        # achievable-bandwidth reference: a STREAM-style device copy of
+        # the bucket (read 4n + write 4n) through the runtime's own copy kernel
+        ms_copy = _events(torch, lambda: dec.copy_(x), reps)
+        copy_gbs = 8 * n / (ms_copy * 1e-3) / 1e9
+        out["roofline"]["achievable_copy_gbs"] = copy_gbs
+        out["roofline"]["frac_of_copy"] = out["roofline"]["achieved"] / copy_gbs
 
         # full DP path: norm -> encode -> all_reduce(SUM words) -> decode
         def path():

@@ -295,6 +295,14 @@ static bool ms_fast_ok(int mode, uint64_t n, const gc_levels *lv)
     return mode == 0 && n < (1ull << 32) && (lv->count == 2 || lv->count == 3) && lv->bits[lv->count - 1] <= 7;
 }
 
+// dense fast decode (k_ms_decode_fast): no rounding, so no 7-bit limit; the
+// order-0 Markstein quotient by s = 2^b - 1 is exhaustively checked for
+// b = 1..16 (profiles/r01q_divcheck_levels.log)
+static bool ms_fast_decode_ok(int mode, uint64_t n, const gc_levels *lv)
+{
+    return mode == 0 && n < (1ull << 32) && (lv->count == 2 || lv->count == 3) && lv->bits[lv->count - 1] <= 16;
+}
+
 static MsFastArg ms_fast_arg(const gc_levels *lv)
 {
     MsFastArg a;
@@ -562,7 +570,7 @@ static int ms_decode(const char *what, const uint32_t *words, const uint32_t *ma
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_decode<LL, MODE_>), dim3(grid), dim3(kBlock), 0, st, \
                                                          words, mk, idx, n, norm, la, q_lanes->plane_words,        \
                                                          q_lanes->bits, sub, order, alpha, out, sg))
-    if (ms_fast_ok(mode, n, levels) && mask_lanes->plane_words >= 2 && mask_lanes->plane_words < (1ull << 32)) {
+    if (ms_fast_decode_ok(mode, n, levels) && mask_lanes->plane_words >= 2 && mask_lanes->plane_words < (1ull << 32)) {
         const MsFastArg fa = ms_fast_arg(levels);
         const FastDiv fd = make_fastdiv((uint32_t)mask_lanes->plane_words);
         const unsigned g = ms_grid(q_lanes->plane_words >> 2);

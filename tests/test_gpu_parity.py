@@ -369,7 +369,7 @@ def test_ms_packed_vs_oracle(levels, world, n):
         assert bits_eq(u32(d), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("levels", [(2, 4), (1, 3), (3, 7), (2, 4, 6), (1, 2, 3, 4, 5, 6, 7)])
+@pytest.mark.parametrize("levels", [(2, 4), (1, 3), (3, 7), (2, 4, 6), (1, 2, 3, 4, 5, 6, 7), (4, 8), (3, 10, 16)])
 @pytest.mark.parametrize("world", [1, 2, 8])
 def test_ms_fast_path_edges_vs_oracle(levels, world):
     """ms_fast.h (dense, levels <= 7 bits): integer rounding per level,
