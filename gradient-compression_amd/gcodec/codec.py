@@ -8,6 +8,7 @@ SUM); the bits are the uint32 lane words of include/gcodec.h.
 from __future__ import annotations
 
 import ctypes as C
+import functools
 
 import numpy as np
 import torch
@@ -26,7 +27,15 @@ def _dev(t: torch.Tensor) -> torch.device:
     return t.device
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(device) -> C.c_void_p:
+    """The current HIP stream of `device` as a raw pointer.  The raw accessor
+    skips the Stream object torch.cuda.current_stream builds (~4 us per call,
+    tools/host_overhead.py)."""
+    if _raw_stream is not None:
+        return C.c_void_p(_raw_stream(device.index if device.index is not None else torch.cuda.current_device()))
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
@@ -57,6 +66,8 @@ def _idx(idx, device):
 def norm_tensor(norm, device) -> torch.Tensor:
     """The max-norm as a device float32 scalar tensor (no host sync)."""
     if isinstance(norm, torch.Tensor):
+        if norm.dtype == torch.float32 and norm.device == device:
+            return norm  # the kernels read element 0 through the data pointer
         t = norm.detach()
         if t.dtype != torch.float32:
             t = t.float()
@@ -69,7 +80,10 @@ def norm_tensor(norm, device) -> torch.Tensor:
 # ---------------------------------------------------------------------------
 # layouts
 # ---------------------------------------------------------------------------
+@functools.lru_cache(maxsize=512)
 def qsgd_layout(n: int, bits: int, world: int = 1) -> _lib.gc_lanes:
+    """Lane layout (cached: a per-call ctypes round trip on every encode;
+    callers treat the struct as read-only)."""
     ln = _lib.gc_lanes()
     check(_lib.load().gc_qsgd_layout(n, bits, world, C.byref(ln)), "gc_qsgd_layout")
     return ln
