@@ -55,11 +55,14 @@ inline FastDiv make_fastdiv(uint32_t d)
     return f;
 }
 
-// lab variants (tools/lab_ms.hip); the product uses VAR = 0
+// kernel variants: the product uses VAR = 0 (levels <= 7 bits) or MSV_WIDE;
+// the others are lab variants (tools/lab_ms.hip)
 enum : int {
     MSV_PERTHREAD = 1,  // one thread walks all planes of its word quad (no wave split)
     MSV_NORNG = 2,      // measurement only: draws = a hash of the element index (no Philox)
     MSV_NOSLOW = 4,     // measurement only: no generic fallback (assumes every quad is fast)
+    MSV_WIDE = 8,       // levels of 8-24 bits (s * 2^24 >= 2^31): the wave-split kernels with the
+                        // generic per-element rounding (quot4_exact + xi_from_q) on every quad
 };
 
 template <int KIND, int VAR>
@@ -235,10 +238,11 @@ __device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_
                                             const RngArgs &rng, int32_t cq = 0, uint32_t cb = 0,
                                             uint4 *cv = nullptr)
 {
+    static_assert(!CACHE || (VAR & MSV_WIDE) == 0, "no q cache for wide levels");
     const float4 v = load4_nt_tail<0>(x, i0, n);
     RangeI rg;
     rg.add4(v);
-    const bool fast = (VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2));
+    const bool fast = (VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)));
     uint4 m = make_uint4(0u, 0u, 0u, 0u);
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
     gc_f2 q01, q23;
@@ -356,7 +360,7 @@ __device__ __forceinline__ uint4 select_plane(const float *__restrict__ x, uint3
     rg.add4(v);
     const uint4 r = draws_at<KIND, NL, VAR>(rng, i0, m);  // the selected level's draw, either path
     uint4 ln;
-    if ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2))) {
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
         const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
         const gc_f2 S01 = {pick_level<NL>(fa.S24, m.x), pick_level<NL>(fa.S24, m.y)};
         const gc_f2 S23 = {pick_level<NL>(fa.S24, m.z), pick_level<NL>(fa.S24, m.w)};

@@ -295,6 +295,12 @@ static bool ms_fast_ok(int mode, uint64_t n, const gc_levels *lv)
     return mode == 0 && n < (1ull << 32) && (lv->count == 2 || lv->count == 3) && lv->bits[lv->count - 1] <= 7;
 }
 
+// levels of 8-24 bits: the same wave-split kernels with generic rounding (MSV_WIDE)
+static bool ms_fast_wide_ok(int mode, uint64_t n, const gc_levels *lv)
+{
+    return mode == 0 && n < (1ull << 32) && (lv->count == 2 || lv->count == 3) && lv->bits[lv->count - 1] <= 24;
+}
+
 // dense fast decode (k_ms_decode_fast): no rounding, so no 7-bit limit; the
 // order-0 Markstein quotient by s = 2^b - 1 is exhaustively checked for
 // b = 1..16 (profiles/r01q_divcheck_levels.log)
@@ -389,10 +395,17 @@ int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const floa
     GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_encode<LL, KIND_, MODE_>), dim3(grid),    \
                                                             dim3(kBlock), 0, st, x, idx, n, norm, la, ra, M, w,  \
                                                             fields, mask_words))
-    if (ms_fast_ok(mode, n, levels)) {
+    if (ms_fast_wide_ok(mode, n, levels)) {
         const MsFastArg fa = ms_fast_arg(levels);
         const unsigned g = ms_grid(M >> 2);
-#define GC_MF(KIND_, NL_)                                                                                            \
+        const bool wide = !ms_fast_ok(mode, n, levels);
+#define GC_MF(KIND_, NL_)                                                                                         \
+    if (wide)                                                                                                     \
+        GC_DISPATCH_L2(mask_lanes->per_word,                                                                      \
+                       hipLaunchKernelGGL((k_ms_mask_fast<LL, KIND_, NL_, MSV_WIDE>), dim3(g), dim3(kBlock), 0, st, \
+                                          x, (uint32_t)n, norm, la, fa, ra, (uint32_t)M, w, fields, mask_words,   \
+                                          (void *)nullptr, 0, 0u))                                                \
+    else                                                                                                          \
     GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_fast<LL, KIND_, NL_>), dim3(g), dim3(kBlock), 0, \
                                                             st, x, (uint32_t)n, norm, la, fa, ra, (uint32_t)M, w,  \
                                                             fields, mask_words, (void *)nullptr, 0, 0u))
@@ -437,11 +450,17 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_encode<LL, KIND_, MODE_>), dim3(grid),       \
                                                          dim3(kBlock), 0, st, x, idx, n, norm, la, ra, mk, Mq, wq, \
                                                          qmax, words))
-    if (ms_fast_ok(mode, n, levels) && mask_lanes->plane_words >= 2 && mask_lanes->plane_words < (1ull << 32)) {
+    if (ms_fast_wide_ok(mode, n, levels) && mask_lanes->plane_words >= 2 && mask_lanes->plane_words < (1ull << 32)) {
         const MsFastArg fa = ms_fast_arg(levels);
         const FastDiv fd = make_fastdiv((uint32_t)mask_lanes->plane_words);
         const unsigned g = ms_grid(Mq >> 2);
+        const bool wide = !ms_fast_ok(mode, n, levels);
 #define GC_SF(KIND_, NL_)                                                                                             \
+    if (wide)                                                                                                         \
+        GC_DISPATCH_L2(q_lanes->per_word,                                                                             \
+                       hipLaunchKernelGGL((k_ms_select_fast<LL, KIND_, NL_, MSV_WIDE>), dim3(g), dim3(kBlock), 0, st,   \
+                                          x, (uint32_t)n, norm, la, fa, ra, mk, fd, (uint32_t)Mq, wq, qmax, words))  \
+    else                                                                                                              \
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_fast<LL, KIND_, NL_>), dim3(g), dim3(kBlock), 0,   \
                                                          st, x, (uint32_t)n, norm, la, fa, ra, mk, fd, (uint32_t)Mq, \
                                                          wq, qmax, words))
