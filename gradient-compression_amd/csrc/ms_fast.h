@@ -20,9 +20,10 @@
 // Taken when: dense aligned x (MODE 0), n < 2^32, 2 or 3 levels (NL, a
 // template argument: level tables and mask fields resolve at compile time),
 // every level <= 7 bits (s * 2^24 < 2^31; the decode, which does no rounding,
-// up to 16 bits).  Anything else, and any quad whose |x| fail the
-// RangeI check (or whose norm is outside the Markstein range), runs the
-// generic per-element code.
+// up to 16 bits).  Levels of 8-24 bits run the same kernels with MSV_WIDE:
+// the wave split and the streaming, with the generic per-element rounding.
+// Anything else, and any quad whose |x| fail the RangeI check (or whose norm
+// is outside the Markstein range), runs the generic per-element code.
 #pragma once
 
 #include "gc_device.h"
