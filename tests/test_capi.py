@@ -195,3 +195,23 @@ def test_ms_cache_bytes():
         assert codec.ms_cache_bytes(n, levels) == cell, levels
     assert codec.ms_cache_bytes(1 << 32, (2, 4)) == 0  # beyond the fast path's 32-bit indices
     assert codec.ms_cache_bytes(0, (2, 4)) == 1
+
+
+def test_product_package_never_reaches_the_oracle():
+    """The shipped package (gcodec/ + csrc/) must not import, load or link
+    anything under oracle/: the oracle is the test checker only."""
+    import re
+
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "gradient-compression_amd")
+    pat = re.compile(r"(import\s+oracle|from\s+oracle|liboracle|oracle/_ref)")
+    offenders = []
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")) or f == "Makefile":
+                p = os.path.join(dirpath, f)
+                with open(p, encoding="utf-8", errors="replace") as fh:
+                    for i, line in enumerate(fh, 1):
+                        if pat.search(line):
+                            offenders.append(f"{p}:{i}: {line.strip()}")
+    assert not offenders, "\n".join(offenders)
