@@ -60,18 +60,21 @@ def _events(torch, fn, reps):
 
 
 def _traffic(kernel: str, n: int, bits: int):
-    """HBM bytes per launch from the committed PMC profile (profiles/), if it
-    was collected for this exact workload; else None."""
+    """HBM bytes per launch of `kernel` from the committed PMC profile
+    (profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+    over this same workload, collected by tools/profile.sh on an earlier run)
+    -> (bytes, source) or (None, None).  Not measured by this run: PMC
+    counters need their own rocprofv3 pass."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
         k = d["kernels"][kernel]
         if d.get("n") == n and d.get("bits") == bits:
-            return k["hbm_bytes_per_launch"]
+            return k["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json (rocprofv3 --pmc, tag {d.get('tag')})"
     except Exception:
         pass
-    return None
+    return None, None
 
 
 def cpu_baseline(n: int, bits: int, budget_s: float):
@@ -400,7 +403,8 @@ def main():
         "pct_hbm_peak_step": 100.0 * step_bytes * K / el / 1e9 / HBM_PEAK_GBS,
         "roofline": {"bound": "hbm", "kernel": "k_qsgd_encode", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": _traffic("k_qsgd_encode", n, bits),
+                     "traffic": _traffic("k_qsgd_encode", n, bits)[0],
+                     "traffic_source": _traffic("k_qsgd_encode", n, bits)[1],
                      "bytes_per_launch": enc_bytes, "ms_per_launch": ms_encode},
         "kernels_ms": {"k_absmax": ms_absmax, "k_qsgd_encode": ms_encode},
     }

@@ -183,8 +183,10 @@ class Segments:
     """gc_segments for a list of contiguous fp32 tensors on one device: the
     reference's TensorBuffer (reducer.py:46-68) as a device table, so flatten,
     max-norm, decode and setgrad address the tensors in place.  Built once per
-    parameter list (one small H2D copy) and reused; it keeps the tensors alive
-    because the table holds their raw pointers."""
+    parameter list (one small H2D copy) and reused.  It holds NO reference to
+    the tensors: a table is valid for any list whose key_of (data pointers,
+    sizes, dtype, device) equals self.key, which callers check on every use —
+    so a cached table never pins freed gradients in device memory."""
 
     CHUNK_SHIFT = 12
 
@@ -212,7 +214,6 @@ class Segments:
         self.device = dev
         self.n = n
         self.count = count
-        self.tensors = tensors
         self.key = Segments.key_of(tensors)
         self._seg = torch.from_numpy(seg_host.view(np.int64)).to(dev)
         self._chunk = torch.from_numpy(chunk_host.view(np.int32)).to(dev)

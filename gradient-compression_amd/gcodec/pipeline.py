@@ -7,6 +7,14 @@ per chunk:
     all_reduce(c)   on RCCL's stream, after encode(c)    (int32 SUM of packed lanes)
     decode(c)       on a decode stream, after all_reduce(c)
 so encode(c+1) runs while chunk c is on the wire and chunk c-1 decodes.
+
+Stream dependencies (nothing waits on a whole stream inside a call):
+    decode stream  <- event after the norm is final (absmax + MAX)
+    decode(c)      <- the RCCL work handle of chunk c (W > 1), or an event
+                      recorded right after encode(c) (W = 1)
+    compute stream <- the decode stream, once, at the end of the call (the next
+                      call's encode(c) must not overwrite chunk c's words
+                      before this call's decode(c) has read them)
 With the generator in torch mode the packed integers equal the unchunked
 encode's (draws are consumed chunk by chunk, in element order).
 
@@ -23,13 +31,18 @@ from .rng import default_generator
 
 
 class ChunkedQSGDAllReduce:
-    def __init__(self, n: int, bits: int, device, chunks: int = 4, group=None, generator=None, codec=None):
+    """reduce(x) = decode(SUM over ranks of encode(x)) * 1/W, chunk-pipelined.
+
+    world: the W the lanes are sized for; defaults to the group's size.
+    """
+
+    def __init__(self, n: int, bits: int, device, chunks: int = 4, group=None, generator=None, codec=None,
+                 world: int | None = None):
         self.n, self.bits, self.device = n, bits, torch.device(device)
         self.group = group
-        if dist.is_available() and dist.is_initialized():
-            self.world = dist.get_world_size(group)
-        else:
-            self.world = 1
+        if world is None:
+            world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.world = int(world)
         self.codec = codec or _hip_codec
         self.gen = generator or default_generator
         chunks = max(1, min(chunks, n))
@@ -44,25 +57,40 @@ class ChunkedQSGDAllReduce:
     def bits_per_step(self) -> int:
         return 32 + sum(32 * w.numel() for w in self.words)
 
+    def _max(self, norm: torch.Tensor):
+        """MAX of the local norms (enqueued in line: every encode needs it)."""
+        if self.world > 1:
+            dist.all_reduce(norm, op=dist.ReduceOp.MAX, group=self.group)
+
+    def _reduce(self, words: torch.Tensor):
+        """Asynchronous SUM of one chunk's packed words; the work handle, or
+        None when the words are final on the compute stream."""
+        if self.world > 1:
+            return dist.all_reduce(words, group=self.group, async_op=True)
+        return None
+
     def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         if out is None:
             out = torch.empty_like(x)
         W = self.world
         compute = torch.cuda.current_stream(self.device)
         self.codec.absmax(x, out=self.norm)
-        if W > 1:
-            dist.all_reduce(self.norm, op=dist.ReduceOp.MAX, group=self.group)
-        works = []
+        self._max(self.norm)
+        norm_ready = torch.cuda.Event()
+        norm_ready.record(compute)
+        self.dec_stream.wait_event(norm_ready)
         for (s, e), ln, wd in zip(self.bounds, self.lanes, self.words):
             rng = self.gen.reserve(e - s, 1, device=self.device, backend=self.codec)
             self.codec.qsgd_encode(x[s:e], self.norm, self.bits, rng, W, out=wd, lanes=ln)
-            works.append(dist.all_reduce(wd, group=self.group, async_op=True) if W > 1 else None)
-        # decode stream: starts after the norm is final, then each chunk after its all-reduce
-        self.dec_stream.wait_stream(compute)
-        with torch.cuda.stream(self.dec_stream):
-            for (s, e), ln, wd, wk in zip(self.bounds, self.lanes, self.words, works):
-                if wk is not None:
-                    wk.wait()  # the decode stream waits for RCCL, the host does not block
+            work = self._reduce(wd)
+            if work is None:
+                encoded = torch.cuda.Event()
+                encoded.record(compute)
+            with torch.cuda.stream(self.dec_stream):
+                if work is not None:
+                    work.wait()  # the decode stream waits for this chunk's RCCL SUM; the host does not block
+                else:
+                    self.dec_stream.wait_event(encoded)
                 self.codec.qsgd_decode(wd, e - s, self.norm, self.bits, W, 1.0 / W, out=out[s:e], lanes=ln)
         compute.wait_stream(self.dec_stream)
         for t in [x, out, self.norm, *self.words]:

@@ -20,6 +20,7 @@ reference does not overflow.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import random
 
@@ -50,6 +51,8 @@ def set_seed(seed: int, generator=None):
 class Reducer:
     """reducer.py:26-43."""
 
+    SEG_CACHE = 8  # gc_segments tables kept (grad_in + grad_out lists of a few recent steps)
+
     def __init__(self, device, timer=None, codec=None, generator=None, group=None, fused=True, topology=None):
         if dist.is_available() and dist.is_initialized():
             self.n_workers = dist.get_world_size(group)
@@ -66,7 +69,7 @@ class Reducer:
         if topology is not None and group is not None:
             raise ValueError("topology spans the default process group; pass one or the other")
         self._fused = fused
-        self._seg_cache = {}
+        self._seg_cache = collections.OrderedDict()  # LRU of gc_segments tables by tensor-list key
 
     def reduce(self, grad_in, grad_out):
         raise NotImplementedError()
@@ -114,12 +117,18 @@ class Reducer:
             return None
         if any(not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous() for t in tensors):
             return None
+        # keyed by the tensors' data pointers and sizes: a table stays valid while
+        # the list it describes lives at the same addresses (the caching
+        # allocator usually hands a re-created p.grad the same block every step);
+        # LRU, so the stable send-buffer entry survives reallocated grad lists
         key = make.key_of(tensors)
         segs = self._seg_cache.get(key)
         if segs is None:
-            if len(self._seg_cache) >= 4:
-                self._seg_cache.pop(next(iter(self._seg_cache)))
+            if len(self._seg_cache) >= self.SEG_CACHE:
+                self._seg_cache.popitem(last=False)
             segs = self._seg_cache[key] = make(tensors)
+        else:
+            self._seg_cache.move_to_end(key)
         return segs
 
     def _flat_pack(self, grad_in):

@@ -66,8 +66,24 @@ class Reservation:
         return None if self.stream is None else self.stream.cpu().numpy().view(np.uint32)
 
 
+def _process_rank() -> int:
+    import torch.distributed as dist
+
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
 class Generator:
-    def __init__(self, seed: int = 42, mode: str = "philox"):
+    """Draw allocator of one codec stream.
+
+    per_rank=True keys the Philox stream by seed + the process's global rank
+    (read at every reservation), so ranks that share one Generator object by
+    default still draw independent uniforms — the reference seeds every rank's
+    torch generator with seed + rank (model_dispatcher.py:59, trainer.py:158).
+    Identical draws on every rank would correlate the ranks' rounding errors
+    instead of averaging them down with W."""
+
+    def __init__(self, seed: int = 42, mode: str = "philox", per_rank: bool = False):
+        self.per_rank = per_rank
         self.set_mode(mode)
         self.manual_seed(seed)
 
@@ -85,7 +101,8 @@ class Generator:
         """Reserve n*levels draws (advances the stream like torch's generator)."""
         count = n * levels
         if self.mode == "philox":
-            r = Reservation(_lib.GC_RNG_PHILOX, self.seed, self.offset, None, n, levels)
+            key = self.seed + (_process_rank() if self.per_rank else 0)
+            r = Reservation(_lib.GC_RNG_PHILOX, key, self.offset, None, n, levels)
             self.offset += count
             return r
         if backend is None:
@@ -94,7 +111,9 @@ class Generator:
         return Reservation(_lib.GC_RNG_STREAM, 0, 0, stream, n, levels)
 
 
-default_generator = Generator()
+# the stream every compressor / reducer / pipeline uses when none is passed:
+# one object per process, keyed per rank (see Generator)
+default_generator = Generator(per_rank=True)
 
 
 def manual_seed(seed: int, mode: str | None = None) -> Generator:

@@ -36,8 +36,9 @@ def make_reducer(name, **kw):
     raise KeyError(name)
 
 
-def reducer_vs_reference(rank, world, init_file, fixture, out_dir):
-    """Run our reducers (oracle codec, torch-mode RNG) on the golden grads."""
+def reducer_vs_reference(rank, world, init_file, fixture, out_dir, local_size=None):
+    """Run our reducers (oracle codec, torch-mode RNG) on the golden grads
+    (local_size: through gcodec.NodeTopology's two-level collectives)."""
     import gcodec
     import oracle_codec
 
@@ -45,8 +46,13 @@ def reducer_vs_reference(rank, world, init_file, fixture, out_dir):
     z = np.load(fixture, allow_pickle=False)
     gen = gcodec.Generator(0, "torch")
     res = {}
+    topo = None
+    if local_size is not None:
+        from gcodec.topology import NodeTopology
+
+        topo = NodeTopology(local_size)
     for name in REDUCERS:
-        red = make_reducer(name, codec=oracle_codec, generator=gen)
+        red = make_reducer(name, codec=oracle_codec, generator=gen, topology=topo)
         torch.manual_seed(SEED + rank)
         for step in range(2):
             gin = []
@@ -64,8 +70,10 @@ def reducer_vs_reference(rank, world, init_file, fixture, out_dir):
     dist.destroy_process_group()
 
 
-def hip_reducer_vs_reference(rank, world, init_file, fixture, out_dir):
-    """Our reducers on the GPU (HIP codec, torch-mode RNG), gloo over CUDA tensors."""
+def hip_reducer_vs_reference(rank, world, init_file, fixture, out_dir, local_size=None):
+    """Our reducers on the GPU (HIP codec, torch-mode RNG), gloo over CUDA
+    tensors; local_size: every collective through gcodec.NodeTopology (the
+    multi-node two-level path, nodes of local_size ranks)."""
     import gcodec
 
     dev = torch.device("cuda", 0)
@@ -74,10 +82,14 @@ def hip_reducer_vs_reference(rank, world, init_file, fixture, out_dir):
     z = np.load(fixture, allow_pickle=False)
     gen = gcodec.Generator(0, "torch")
     res = {}
-    from gcodec import reducer as R
+    topo = None
+    if local_size is not None:
+        from gcodec.topology import NodeTopology
+
+        topo = NodeTopology(local_size)
 
     for name in REDUCERS:
-        red = make_reducer(name, generator=gen)
+        red = make_reducer(name, generator=gen, topology=topo)
         red._device = dev
         torch.manual_seed(SEED + rank)
         for step in range(2):
@@ -116,9 +128,10 @@ def hip_pipeline_world(rank, world, init_file, out_dir, n, bits, chunks):
     dist.destroy_process_group()
 
 
-def ddp_hook_world(rank, world, init_file, out_dir, use_gpu):
+def ddp_hook_world(rank, world, init_file, out_dir, use_gpu, levels=None, two_scale=False):
     """torch DDP with gcodec.ddp_hook.qsgd_hook on a small MLP, several buckets,
-    three steps; records every hook call's input bucket, RNG offset and result."""
+    three steps; records every hook call's input bucket, RNG offset and result
+    (levels: the two-/multi-scale form of the hook)."""
     import gcodec
     from gcodec.ddp_hook import QSGDHookState, qsgd_hook
     from torch.nn.parallel import DistributedDataParallel as DDP
@@ -136,7 +149,8 @@ def ddp_hook_world(rank, world, init_file, out_dir, use_gpu):
     model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.Tanh(), torch.nn.Linear(64, 64), torch.nn.Tanh(),
                                 torch.nn.Linear(64, 8)).to(dev)
     ddp = DDP(model, bucket_cap_mb=0.008)  # ~2k floats per bucket -> several buckets per step
-    state = QSGDHookState(bits=4, generator=gcodec.Generator(100 + rank, "philox"), codec=codec)
+    state = QSGDHookState(bits=4, generator=gcodec.Generator(100 + rank, "philox"), codec=codec, levels=levels,
+                          two_scale=two_scale)
     rec = []
 
     def hook(st, bucket):
@@ -213,36 +227,23 @@ def topology_world(rank, world, init_file, out_dir, local_size):
     dist.destroy_process_group()
 
 
-def hip_topology_world(rank, world, init_file, out_dir, local_size):
-    """NodeTopology with the HIP codec (gloo over CUDA tensors, one GPU):
-    reducers through the two-level collectives vs flat, bit for bit."""
+
+def default_generator_world(rank, world, init_file, out_dir):
+    """QSGDMaxNormCompressor.encode with NO generator argument on identical
+    inputs on every rank (oracle codec on CPU)."""
     import gcodec
-    from gcodec.topology import NodeTopology
+    import oracle_codec
+    from oracle import oracle as O
 
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
-    topo = NodeTopology(local_size)
-    from gcodec import reducer as R
-
-    res = {}
-    for name, mk in (("qsgd", lambda **kw: R.QSGDMaxNormReducer(dev, None, quantization_level=4, **kw)),
-                     ("ts", lambda **kw: R.QSGDMaxNormTwoScaleReducer(dev, None, 2, 4, **kw)),
-                     ("randk", lambda **kw: R.GlobalRandKMaxNormReducer(dev, None, SEED, K=1000,
-                                                                        quantization_level=4, **kw))):
-        outs = []
-        for use_topo in (False, True):
-            gen = gcodec.Generator(SEED + rank, "philox")
-            red = mk(generator=gen, topology=topo if use_topo else None)
-            got = []
-            for step in range(2):
-                gin = [torch.randn(s, generator=torch.Generator().manual_seed(1000 * step + 10 * rank + i)).to(dev)
-                       for i, s in enumerate((37, 5000, 70001))]
-                gout = [torch.empty_like(t) for t in gin]
-                red.reduce(gin, gout)
-                got += [t.cpu().numpy() for t in gout]
-            outs.append(got)
-        res[name] = np.int64(all(a.tobytes() == b.tobytes() for a, b in zip(*outs)))
-    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
+    x = O.gen_input(10_001, seed=3)
+    comp = gcodec.QSGDMaxNormCompressor(torch.device("cpu"), 4)
+    comp.backend = oracle_codec
+    r = gcodec.rng.default_generator.reserve(0)  # the key this rank's default stream uses
+    off = gcodec.rng.default_generator.offset
+    words = comp.encode(torch.tensor([O.absmax(x)]), torch.from_numpy(x), world=world)
+    ref = O.qsgd_encode(x, O.absmax(x), 4, world, O.philox_rng(r.seed, off))
+    np.savez(os.path.join(out_dir, f"g{rank}.npz"), words=words.numpy(), key=np.int64(r.seed),
+             oracle=ref.view(np.int32))
     dist.barrier()
     dist.destroy_process_group()

@@ -16,7 +16,26 @@ import torch.multiprocessing as mp  # noqa: E402
 import _gloo_workers as W  # noqa: E402
 
 
-def check_hook_records(recs, world, bits=4):
+def _expected_bucket(O, xs, offs, world, bits, levels, order):
+    n = xs[0].size
+    norm = max(O.absmax(x) for x in xs)
+    alpha = np.float32(1.0 / world)
+    if levels is None:
+        tot = None
+        for rk in range(world):
+            w = O.qsgd_encode(xs[rk], norm, bits, world, O.philox_rng(100 + rk, offs[rk]))
+            tot = w.astype(np.uint64) if tot is None else tot + w
+        return O.qsgd_decode(tot.astype(np.uint32), n, norm, bits, world, alpha)
+    # common resolution level = MIN over ranks (reducer.py:1680-1685; the AND of
+    # two-scale, 1494-1499), every rank's q at it, summed, decoded
+    masks = [O.ms_mask(xs[rk], norm, levels, O.philox_rng(100 + rk, offs[rk])) for rk in range(world)]
+    common = np.minimum.reduce(masks)
+    qsum = sum(O.ms_select(xs[rk], norm, levels, O.philox_rng(100 + rk, offs[rk]), common).astype(np.int64)
+               for rk in range(world)).astype(np.int32)
+    return O.ms_dequantize(qsum, norm, levels, common, order, alpha)
+
+
+def check_hook_records(recs, world, bits=4, levels=None, order=0):
     from oracle import oracle as O
 
     calls = int(recs[0]["calls"])
@@ -24,13 +43,8 @@ def check_hook_records(recs, world, bits=4):
     assert all(int(r["calls"]) == calls for r in recs)
     for c in range(calls):
         xs = [r[f"c{c}/x"] for r in recs]
-        n = xs[0].size
-        norm = max(O.absmax(x) for x in xs)
-        tot = None
-        for rk in range(world):
-            w = O.qsgd_encode(xs[rk], norm, bits, world, O.philox_rng(100 + rk, int(recs[rk][f"c{c}/off"])))
-            tot = w.astype(np.uint64) if tot is None else tot + w
-        exp = O.qsgd_decode(tot.astype(np.uint32), n, norm, bits, world, np.float32(1.0 / world))
+        offs = [int(r[f"c{c}/off"]) for r in recs]
+        exp = _expected_bucket(O, xs, offs, world, bits, levels, order)
         for rk in range(world):
             assert recs[rk][f"c{c}/out"].tobytes() == exp.tobytes(), f"call {c} rank {rk}"
     # every rank ends with the same averaged gradients
@@ -44,3 +58,15 @@ def test_ddp_qsgd_hook_matches_oracle(world):
         mp.spawn(W.ddp_hook_world, args=(world, os.path.join(td, "init"), td, False), nprocs=world, join=True)
         recs = [np.load(os.path.join(td, f"h{r}.npz"), allow_pickle=False) for r in range(world)]
         check_hook_records(recs, world)
+
+
+@pytest.mark.parametrize("levels,two_scale", [((2, 4), True), ((2, 4, 6), False)])
+@pytest.mark.parametrize("world", [1, 2])
+def test_ddp_multiscale_hook_matches_oracle(world, levels, two_scale):
+    """The two-/multi-scale hook: mask lanes SUM (= MIN of the levels) in one
+    future, select + words SUM + decode in its callback, vs the oracle."""
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(W.ddp_hook_world, args=(world, os.path.join(td, "init"), td, False, list(levels), two_scale),
+                 nprocs=world, join=True)
+        recs = [np.load(os.path.join(td, f"h{r}.npz"), allow_pickle=False) for r in range(world)]
+        check_hook_records(recs, world, levels=list(levels), order=1 if two_scale else 0)

@@ -568,3 +568,180 @@ def test_chunked_pipeline_world1(chunks):
         w = O.qsgd_encode(x[s:e], nh, bits, 1, O.philox_rng(99, off))
         assert bits_eq(got[s:e], O.qsgd_decode(w, e - s, nh, bits, 1))
         off += e - s
+
+
+# --------------------------------------------------------------------------- config 5: 8-bit chunked, full size
+class _IdenticalRanks(gcodec.ChunkedQSGDAllReduce):
+    """W identical ranks on one GPU: the SUM of W equal packed streams is W
+    times the stream (the lanes are sized for W, so nothing carries), and the
+    MAX of W equal norms is the norm.  Exercises the W-dependent lane layout
+    (8-bit at W = 8: 12-bit lanes, 2 per word) through the product pipeline."""
+
+    def _max(self, norm):
+        pass
+
+    def _reduce(self, words):
+        words.mul_(self.world)
+        return None
+
+
+def _unchunked_reduce(x, bits, world, rng):
+    """encode the whole bucket, SUM of `world` identical ranks, decode * 1/W"""
+    n = x.numel()
+    norm = codec.absmax(x)
+    w = codec.qsgd_encode(x, norm, bits, rng, world)
+    w.mul_(world)
+    return codec.qsgd_decode(w, n, norm, bits, world, 1.0 / world)
+
+
+def _check_chunk_heads(pipe, x, out, bits, world, seed, k=1 << 16):
+    """Philox mode: chunk c draws at offset = its start; the head of every
+    chunk equals the oracle's quantize -> W-sum -> dequantize bit for bit."""
+    s_ = (1 << bits) - 1
+    norm = np.float32(codec.absmax(x).item())
+    alpha = np.float32(1.0 / world)
+    for s, e in pipe.bounds:
+        m = min(k, e - s)
+        xs = x[s:s + m].cpu().numpy()
+        q = O.qsgd_quantize(xs, norm, bits, O.philox_rng(seed, s))
+        assert np.all(np.abs(q) <= s_)
+        exp = O.qsgd_dequantize(q * world, norm, bits, alpha)
+        assert bits_eq(u32(out[s:s + m]), exp.view(np.uint32)), (s, e)
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_config5_chunked_8bit_1e8(world):
+    """BASELINE config 5's pipeline (8-bit, 8 chunks) at n = 1e8 + 3 with the
+    lane layouts of W = 1 (9-bit lanes x3) and W = 8 (12-bit lanes x2):
+    torch mode: chunked == unchunked bit for bit (draws consumed in element
+    order); Philox mode: every chunk's head == the oracle."""
+    n, bits, chunks = 100_000_003, 8, 8
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(n, device=DEV, generator=g).mul_(0.01)
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(17)
+        ref = _unchunked_reduce(x, bits, world, gcodec.rng.default_generator.reserve(n, 1, device=DEV))
+        torch.manual_seed(17)
+        pipe = _IdenticalRanks(n, bits, DEV, chunks=chunks, world=world)
+        assert pipe.lanes[0].bits == (9 if world == 1 else 12)
+        got = pipe(x)
+        torch.cuda.synchronize()
+        assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+    finally:
+        gcodec.set_rng_mode("philox")
+    pipe = _IdenticalRanks(n, bits, DEV, chunks=chunks, world=world, generator=gcodec.Generator(99, "philox"))
+    out = pipe(x)
+    torch.cuda.synchronize()
+    _check_chunk_heads(pipe, x, out, bits, world, 99)
+
+
+def test_config5_chunked_8bit_1e9_properties():
+    """config 5 at its full size, 1e9 fp32, 8-bit, W = 8 lanes, 8 chunks:
+    size-independent properties (|dec - x| <= norm/s, unbiased, launch
+    invariant) plus every chunk's head vs the oracle."""
+    n, bits, world = 1_000_000_000, 8, 8
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn(n, device=DEV, generator=g).mul_(0.01)
+    pipe = _IdenticalRanks(n, bits, DEV, chunks=8, world=world, generator=gcodec.Generator(7, "philox"))
+    out = pipe(x)
+    pipe2 = _IdenticalRanks(n, bits, DEV, chunks=8, world=world, generator=gcodec.Generator(7, "philox"))
+    assert torch.equal(pipe2(x), out)
+    del pipe2
+    torch.cuda.synchronize()
+    step = codec.absmax(x).item() / 255
+    d = out - x
+    assert d.abs().max().item() <= step * (1 + 1e-6)
+    assert abs(d.double().mean().item()) < 5 * step / np.sqrt(n)
+    del d
+    _check_chunk_heads(pipe, x, out, bits, world, 7, k=1 << 14)
+
+
+# --------------------------------------------------------------------------- multi-scale large-plane layout
+@pytest.mark.parametrize("name", ["ms_2_4_1e6", "ms_4_8_1e6"])
+def test_ms_large_digest_torch_mode(name):
+    """The reference's 1e6-element multi-scale digests (q planes of >= 65536
+    words: the 64-word plane alignment) through the unpacked facade AND the
+    packed mask -> select -> decode path, torch-mode draws."""
+    import hashlib
+
+    def sha(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    meta = json.load(open(os.path.join(GOLD, "golden.json")))["digests"][name]
+    lv = meta["levels"]
+    x = O.gen_input(meta["n"], seed=42, kind=meta["kind"])
+    xd = dev(x)
+    qdt = np.int8 if lv[0] < 8 else np.int32
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(42)
+        norm = codec.absmax(xd)
+        assert norm.item() == meta["norm"]
+        c = gcodec.QSGDMaxNormMultiScaleCompressor(DEV, list(lv))
+        mask = c.compress_mask(norm, xd)
+        assert sha(mask.cpu().numpy()) == meta["mask"]
+        q = c.compress(mask)
+        assert sha(q.cpu().numpy()) == meta["q"]
+        assert sha(c.decompress(norm, q, mask).cpu().numpy()) == meta["dec"]
+        # packed: thermometer mask lanes, planar q lanes, fused decode
+        torch.manual_seed(42)
+        cp = gcodec.QSGDMaxNormMultiScaleCompressor(DEV, list(lv))
+        mw = cp.encode_mask(norm, xd)
+        ql, ml = codec.ms_layouts(x.size, lv, 1)
+        assert ql.plane_words % 64 == 0 and -(-x.size // ql.per_word) >= 65536
+        assert sha(codec.ms_mask_unpack(mw, x.size, lv).cpu().numpy()) == meta["mask"]
+        words = cp.encode(norm, xd, mw)
+        qp = codec.lane_unpack(words, ql).cpu().numpy().astype(qdt)
+        assert sha(qp) == meta["q"]
+        assert sha(cp.decode(norm, words, mw, x.size).cpu().numpy()) == meta["dec"]
+    finally:
+        gcodec.set_rng_mode("philox")
+
+
+@pytest.mark.parametrize("levels", [(2, 4), (4, 8)])
+@pytest.mark.parametrize("world", [1, 2])
+def test_ms_resnet50_bucket_vs_oracle(levels, world):
+    """BASELINE config 3's bucket (n = 23,520,842, planes of 64-word
+    alignment, mask planes > 65536 words) with Philox draws: mask, select at
+    the common levels of two ranks (W = 2), and both decode orders (two-scale
+    order 1, multi-scale order 0) vs the oracle, bit for bit."""
+    n = 23_520_842
+    L = len(levels)
+    x = O.gen_input(n, seed=L + world, kind=1)
+    xs = [x] + [np.random.default_rng(world).permutation(x) for _ in range(world - 1)]
+    norm = max(O.absmax(v) for v in xs)
+    rngs = [gcodec.rng.Reservation(0, 31 + r, 3, None, n, L) for r in range(world)]
+    ql, ml = codec.ms_layouts(n, levels, world)
+    assert ql.plane_words % 64 == 0
+    mws = [codec.ms_mask_encode(dev(v), float(norm), levels, rngs[r], world) for r, v in enumerate(xs)]
+    masks = [O.ms_mask(v, norm, levels, O.philox_rng(31 + r, 3)) for r, v in enumerate(xs)]
+    for r in range(world):  # each rank's own levels (its lanes times W: W identical ranks)
+        own = codec.ms_mask_unpack((mws[r].to(torch.int64) * world).to(torch.int32), n, levels, world)
+        assert bits_eq(own.cpu().numpy().astype(np.uint8), masks[r])
+    mw_sum = sum(m.to(torch.int64) for m in mws).to(torch.int32)
+    common = np.minimum.reduce(masks)
+    assert bits_eq(codec.ms_mask_unpack(mw_sum, n, levels, world).cpu().numpy().astype(np.uint8), common)
+    words = [codec.ms_select_encode(dev(v), float(norm), levels, rngs[r], mw_sum, world) for r, v in enumerate(xs)]
+    qs = [O.ms_select(v, norm, levels, O.philox_rng(31 + r, 3), common) for r, v in enumerate(xs)]
+    assert bits_eq(u32(words[0]), O.lane_pack(qs[0], ql.offset, ql.bits, ql.per_word, ql.plane_words))
+    wsum = sum(w.to(torch.int64) for w in words).to(torch.int32)
+    qsum = sum(q.astype(np.int64) for q in qs).astype(np.int32)
+    alpha = np.float32(1.0 / world)
+    for order in (0, 1):
+        d = codec.ms_decode(wsum, mw_sum, n, float(norm), levels, world, order, float(alpha))
+        assert bits_eq(u32(d), O.ms_dequantize(qsum, norm, levels, common, order, alpha).view(np.uint32)), order
+
+
+@pytest.mark.parametrize("n", [1, 1000, 300_007, 4_000_037, 26_000_011])
+def test_absmax_workspace_reuse_many_grids(n):
+    """The last-block hand-off of k_absmax (sc1 partials + agent-scope ticket,
+    include/gcodec.h) over grids of 1 to 256 blocks, the self-resetting
+    workspace reused 50 times on one stream, every result vs the oracle."""
+    x = O.gen_input(n, seed=n, kind=1)
+    x[(n * 7) // 11] = np.float32(-0.75)  # a unique maximum somewhere inside
+    xd = dev(x)
+    out = torch.empty(50, dtype=torch.float32, device=DEV)
+    for i in range(50):
+        codec.absmax(xd, out=out[i:i + 1])
+    assert np.all(out.cpu().numpy() == O.absmax(x))
