@@ -282,6 +282,7 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
 
 def main():
     args = _args()
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -516,19 +517,33 @@ def main():
             "note": "pinned host x -> H2D -> absmax+encode -> D2H packed words; and H2D words -> decode -> D2H floats"}
         del xh, wh, dh, xd, dec
 
-        # reference-parity mode: torch CPU-generator (MT19937) stream, generated on the GPU
-        n_mt = min(n, 10_000_000)
+        # reference-parity mode: torch CPU-generator (MT19937) stream, generated on the
+        # GPU by the jumped parallel generators, then the encode from those draws;
+        # per call: torch state read -> H2D, draws, encode, state D2H (synchronises)
         pgen = gcodec.Generator(0, "torch")
         torch.manual_seed(42)
-        xs = x[:n_mt]
-        nm = codec.absmax(xs)
-        lm = codec.qsgd_layout(n_mt, bits, 1)
+        nm = codec.absmax(x)
+        pgen.reserve(n)  # warm: builds the jump table once per process
         torch.cuda.synchronize()
+        reps_mt = 5
         t0 = time.perf_counter()
-        codec.qsgd_encode(xs, nm, bits, pgen.reserve(n_mt), 1, lanes=lm)
+        for _ in range(reps_mt):
+            codec.qsgd_encode(x, nm, bits, pgen.reserve(n), 1, out=words, lanes=lanes)
         torch.cuda.synchronize()
-        out["torch_parity_mode"] = {"n": n_mt, "grad_floats_per_s": n_mt / (time.perf_counter() - t0),
-                                    "note": "MT19937 stream generated serially by one workgroup, then encode"}
+        t_mt = (time.perf_counter() - t0) / reps_mt
+        st = codec.mt19937_seed_state(42)
+        sd = torch.from_numpy(st.view(np.int32)).to(dev)
+        draws = torch.empty(n, dtype=torch.int32, device=dev)
+        ms_gen = _events(torch, lambda: codec.mt19937_generate(sd, n, out=draws), 3)
+        ms_ser = _events(torch, lambda: codec.mt19937_generate(sd, 10_000_000, out=draws, parallel=False), 1)
+        out["torch_parity_mode"] = {
+            "n": n, "grad_floats_per_s": n / t_mt, "ms_per_call": t_mt * 1e3,
+            "mt19937_parallel_ms": ms_gen, "mt19937_parallel_draws_per_s": n / (ms_gen * 1e-3),
+            "mt19937_serial_draws_per_s": 10_000_000 / (ms_ser * 1e-3),
+            "note": "torch-CPU-generator (MT19937) draws, bit-exact with compressors.py: jump-ahead parallel "
+                    "generators (gc_mt19937_generate_jumped) -> encode from the draws; includes the torch "
+                    "state hand-off (H2D + D2H sync) per call"}
+        del draws
 
     if not args.no_extras:
         out["configs"] = other_configs(torch, dist, gcodec, codec, dev, world, rank, K)

@@ -88,6 +88,11 @@ __device__ __forceinline__ uint4 draws4(const RngArgs &r, uint32_t level, uint64
     } else {
         const uint32_t *p = r.stream + (uint64_t)level * r.n + i0;
         const uint64_t left = i0 < r.n ? r.n - i0 : 0;
+        if (left >= 4 && (reinterpret_cast<uintptr_t>(p) & 15u) == 0) {  // streamed once: one 16-byte NT load
+            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+            const u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(p));
+            return make_uint4(v.x, v.y, v.z, v.w);
+        }
         uint4 d;
         d.x = left > 0 ? p[0] : 0u;
         d.y = left > 1 ? p[1] : 0u;

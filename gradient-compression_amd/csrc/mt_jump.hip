@@ -1,0 +1,255 @@
+// mt_jump.hip — the torch CPU-generator stream (MT19937, seed.py:6-11 /
+// compressors.py:310 torch.bernoulli) generated in parallel on gfx950.
+//
+// MT19937 is serial: draw t+1 needs the state after draw t.  The parallel
+// stream cuts the `count` draws into G = ceil(count / J) generators of J =
+// GC_MT_JUMP_DRAWS (= 624 x 420) consecutive draws.  Generator g starts from
+// the 624-word window at raw position g*J of the caller's state frame (so every
+// window is aligned to the 624-word twist blocks of the serial generator, and
+// the last generator's final window IS torch's state array), with the caller's
+// read index.  Its window comes from the jump-ahead of mt_poly.cpp:
+//     x_{gJ-1+j} = XOR_{k : a_k = 1} x_{k+j},   a = x^(gJ-1) mod P,  j = 1..624
+// Three launches, all on the caller's stream, no host synchronisation:
+//   k_mt_seq    one workgroup: the first 20561 raw words x_0.. of the stream
+//               (32 twists of the state) into the workspace; window 0 = the
+//               state itself, plus the read index
+//   k_mt_jump   one workgroup per generator g >= 1: x_0..x_20560 in LDS (82 KB),
+//               624 threads, thread j accumulates the XOR over the 19937
+//               coefficient bits (uniform per block: scalar loads of the jump
+//               table; per bit a uniform 0 / ~0 mask and one xor-and)
+//   k_mt_gen    one wave per generator: its window in LDS, wave-synchronous
+//               3-phase twists, tempered draws stored coalesced; the last
+//               generator writes the advanced state back
+// Bit-exact with the serial stream (tests/test_gpu_parity.py vs the oracle's
+// MT19937 and the reference's torch-mode goldens).
+#include "gc_device.h"
+#include "gc_host.h"
+
+namespace gc {
+
+constexpr uint32_t kMtN = 624;
+constexpr uint32_t kMtM = 397;
+constexpr uint32_t kMtJ = GC_MT_JUMP_DRAWS;
+constexpr uint32_t kMtSeq = 19937 + kMtN;              // x_0 .. x_20560 (k + j <= 19936 + 624)
+constexpr uint32_t kMtSeqLds = 623 * 32 + 32 + kMtN;  // every (cw, b, j) read in bounds (pad = 0)
+constexpr uint32_t kMtSeqWs = 33 * kMtN;              // 33 twist blocks cover kMtSeq
+constexpr uint32_t kMtJumpThreads = 640;              // 10 waves; threads 0..623 own a window word
+constexpr uint32_t kMtGenWaves = 4;                   // generators per block of k_mt_gen
+
+static_assert(kMtJ % kMtN == 0, "generator windows stay aligned to the twist blocks");
+static_assert(kMtSeqWs >= kMtSeq, "sequence blocks");
+
+// workspace (uint32): [0] read index, [64 ..) sequence, then windows [G][624]
+constexpr uint64_t kWsSeq = 64;
+constexpr uint64_t kWsWin = kWsSeq + kMtSeqWs;
+
+__device__ __forceinline__ uint32_t mtj_temper(uint32_t y)
+{
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+__device__ __forceinline__ uint32_t mtj_mix(uint32_t a, uint32_t b, uint32_t c)
+{
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// compiler-level ordering of LDS accesses between the phases of a
+// wave-synchronous twist (the hardware executes one wave's DS ops in order)
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+// one in-place twist of a 624-word window by one wave (s[k] = s[k+397] ^
+// twist(s[k], s[k+1]) in k order): phase A k < 227 reads only old words,
+// B k < 454 reads s[k-227] from A, C k < 624 from B (and s[0] from A for
+// k = 623).  Every lane loads all its inputs of a phase before any store.
+__device__ __forceinline__ void twist_wave(uint32_t *s, uint32_t lane)
+{
+    constexpr uint32_t H = kMtN - kMtM;  // 227
+    uint32_t v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t k = lane + 64u * r;
+        v[r] = k < H ? mtj_mix(s[k], s[k + 1], s[k + kMtM]) : 0u;
+    }
+    lds_order();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t k = lane + 64u * r;
+        if (k < H)
+            s[k] = v[r];
+    }
+    lds_order();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t k = H + lane + 64u * r;
+        v[r] = k < 2 * H ? mtj_mix(s[k], s[k + 1], s[k - H]) : 0u;
+    }
+    lds_order();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t k = H + lane + 64u * r;
+        if (k < 2 * H)
+            s[k] = v[r];
+    }
+    lds_order();
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const uint32_t k = 2 * H + lane + 64u * r;
+        v[r] = k < kMtN - 1 ? mtj_mix(s[k], s[k + 1], s[k - H]) : (k == kMtN - 1 ? mtj_mix(s[k], s[0], s[k - H]) : 0u);
+    }
+    lds_order();
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const uint32_t k = 2 * H + lane + 64u * r;
+        if (k < kMtN)
+            s[k] = v[r];
+    }
+    lds_order();
+}
+
+// x_0 .. x_{kMtSeqWs-1} of the caller's state frame; window 0 and the read index
+__global__ __launch_bounds__(256) void k_mt_seq(const uint32_t *__restrict__ state, uint32_t *__restrict__ ws)
+{
+    __shared__ uint32_t s[kMtN];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < kMtN; i += 256) {
+        s[i] = state[i];
+        ws[kWsSeq + i] = state[i];
+        ws[kWsWin + i] = state[i];  // generator 0 starts from the state itself
+    }
+    if (tid == 0)
+        ws[0] = state[kMtN];
+    __syncthreads();
+    for (uint32_t b = 1; b < kMtSeqWs / kMtN; ++b) {
+        // block-wide twist: the three phases with barriers
+        uint32_t v = 0;
+        constexpr uint32_t H = kMtN - kMtM;
+        if (tid < H)
+            v = mtj_mix(s[tid], s[tid + 1], s[tid + kMtM]);
+        __syncthreads();
+        if (tid < H)
+            s[tid] = v;
+        __syncthreads();
+        if (tid < H)
+            v = mtj_mix(s[H + tid], s[H + tid + 1], s[tid]);
+        __syncthreads();
+        if (tid < H)
+            s[H + tid] = v;
+        __syncthreads();
+        const uint32_t k = 2 * H + tid;
+        if (k < kMtN - 1)
+            v = mtj_mix(s[k], s[k + 1], s[k - H]);
+        else if (k == kMtN - 1)
+            v = mtj_mix(s[k], s[0], s[k - H]);
+        __syncthreads();
+        if (k < kMtN)
+            s[k] = v;
+        __syncthreads();
+        for (uint32_t i = tid; i < kMtN; i += 256)
+            ws[kWsSeq + (uint64_t)b * kMtN + i] = s[i];
+        __syncthreads();
+    }
+}
+
+// window of generator g = blockIdx.x + 1: thread j-1 (j = 1..624) writes
+// x_{gJ-1+j} = XOR over the set coefficient bits k of table[g-1] of x_{k+j}
+__global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws)
+{
+    __shared__ uint32_t seq[kMtSeqLds];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < kMtSeqLds; i += kMtJumpThreads)
+        seq[i] = i < kMtSeq ? ws[kWsSeq + i] : 0u;
+    __syncthreads();
+    const uint64_t g = (uint64_t)blockIdx.x + 1;
+    const uint32_t *__restrict__ coef = table + (uint64_t)blockIdx.x * kMtN;
+    const uint32_t j = tid + 1;
+    uint32_t acc = 0;
+    if (tid < kMtN) {
+        for (uint32_t cw = 0; cw < kMtN; ++cw) {
+            const uint32_t c = __builtin_amdgcn_readfirstlane(coef[cw]);
+            const uint32_t *p = seq + cw * 32u + j;
+#pragma unroll
+            for (int b = 0; b < 32; ++b) {
+                const uint32_t m = 0u - ((c >> b) & 1u);             // uniform 0 / ~0: one s_bfe_i32
+                acc = __builtin_amdgcn_bitop3_b32(acc, p[b], m, 0x78);  // acc ^ (p & m)
+            }
+        }
+        ws[kWsWin + g * kMtN + tid] = acc;
+    }
+}
+
+// one wave per generator: draws [gJ, min((g+1)J, count)) into out
+__global__ __launch_bounds__(64 * kMtGenWaves) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t count,
+                                                             uint32_t *__restrict__ out, uint32_t *__restrict__ state)
+{
+    __shared__ uint32_t win[kMtGenWaves][kMtN];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint64_t g = (uint64_t)blockIdx.x * kMtGenWaves + wave;
+    if (g >= gens)
+        return;  // whole waves only: nothing below synchronises across waves
+    uint32_t *s = win[wave];
+    for (uint32_t i = lane; i < kMtN; i += 64)
+        s[i] = ws[kWsWin + g * kMtN + i];
+    uint32_t ptr = ws[0];
+    lds_order();
+    uint64_t pos = g * kMtJ;
+    const uint64_t end = min(pos + kMtJ, count);
+    while (pos < end) {
+        if (ptr >= kMtN) {
+            twist_wave(s, lane);
+            ptr = 0;
+        }
+        const uint32_t take = (uint32_t)min((uint64_t)(kMtN - ptr), end - pos);
+        for (uint32_t i = lane; i < take; i += 64)
+            out[pos + i] = mtj_temper(s[ptr + i]);
+        lds_order();
+        pos += take;
+        ptr += take;
+    }
+    if (g == gens - 1) {  // the advanced state: this window (aligned to the twist blocks) + read index
+        for (uint32_t i = lane; i < kMtN; i += 64)
+            state[i] = s[i];
+        if (lane == 0)
+            state[kMtN] = ptr;
+    }
+}
+
+}  // namespace gc
+
+using namespace gc;
+
+extern "C" {
+
+size_t gc_mt19937_workspace_size(uint64_t count)
+{
+    const uint64_t gens = count ? (count + kMtJ - 1) / kMtJ : 1;
+    return 4 * (kWsWin + gens * kMtN);
+}
+
+int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,
+                               uint64_t count, void *workspace, gc_stream_t stream)
+{
+    GC_REQUIRE(state_dev && workspace, "gc_mt19937_generate_jumped: null state/workspace");
+    GC_REQUIRE(count == 0 || out, "gc_mt19937_generate_jumped: null out");
+    if (count == 0)
+        return GC_OK;
+    const uint64_t gens = (count + kMtJ - 1) / kMtJ;
+    GC_REQUIRE(gens - 1 <= table_gens && (gens == 1 || table_dev),
+               "gc_mt19937_generate_jumped: jump table holds %llu generators, %llu draws need %llu",
+               (unsigned long long)table_gens, (unsigned long long)count, (unsigned long long)(gens - 1));
+    GC_REQUIRE(gens <= 0x7fffffffull, "gc_mt19937_generate_jumped: count too large");
+    hipStream_t st = as_stream(stream);
+    uint32_t *ws = reinterpret_cast<uint32_t *>(workspace);
+    hipLaunchKernelGGL(k_mt_seq, dim3(1), dim3(256), 0, st, state_dev, ws);
+    if (gens > 1)
+        hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)(gens - 1)), dim3(kMtJumpThreads), 0, st, table_dev, ws);
+    hipLaunchKernelGGL(k_mt_gen, dim3((unsigned)((gens + kMtGenWaves - 1) / kMtGenWaves)), dim3(64 * kMtGenWaves), 0,
+                       st, ws, gens, count, out, state_dev);
+    return launch_status("gc_mt19937_generate_jumped");
+}
+
+}  // extern "C"

@@ -23,6 +23,7 @@ GC_ENODEV = -5
 GC_I8, GC_I32, GC_I64 = 1, 4, 8
 GC_RNG_PHILOX, GC_RNG_STREAM = 0, 1
 GC_MAX_LEVELS = 8
+GC_MT_JUMP_DRAWS = 262080  # include/gcodec.h: draws per generator of the parallel MT19937 stream
 
 
 class GCodecError(RuntimeError):
@@ -118,6 +119,9 @@ SIGNATURES = {
     "gc_ms_dequantize": (C.c_int, [P, u32, P, u64, P, LEVP, C.c_int, f32, P, P]),
     "gc_mt19937_seed": (C.c_int, [u64, P]),
     "gc_mt19937_generate": (C.c_int, [P, P, u64, P]),
+    "gc_mt19937_jump_table": (C.c_int, [u64, u64, P]),
+    "gc_mt19937_workspace_size": (C.c_size_t, [u64]),
+    "gc_mt19937_generate_jumped": (C.c_int, [P, P, u64, P, u64, P, P]),
     "gc_greedy4_pack": (i64, [P, u64, P, u64]),
     "gc_greedy4_unpack": (i64, [P, u64, P, u64]),
     "gc_greedy4_workspace_size": (C.c_size_t, [u64]),

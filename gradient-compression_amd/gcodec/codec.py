@@ -446,11 +446,50 @@ def mt19937_seed_state(seed: int) -> np.ndarray:
     return st
 
 
-def mt19937_generate(state_dev: torch.Tensor, count: int, out=None) -> torch.Tensor:
+_MT_TABLE = {}  # device index -> (int32 tensor [gens * 624], gens): jump coefficients of generators 1..gens
+_MT_WS = {}     # (device index, stream) -> workspace tensor
+
+
+def _mt_jump_table(dev, gens: int):
+    """Device jump table covering generators 1..gens (host-computed once per
+    process and grown geometrically; it depends only on the generator index)."""
+    cur = _MT_TABLE.get(dev.index)
+    have = cur[1] if cur is not None else 0
+    if have >= gens:
+        return cur
+    total = max(gens, 2 * have, 16)
+    host = np.empty((total - have) * 624, dtype=np.uint32)
+    check(_lib.load().gc_mt19937_jump_table(have + 1, total - have, host.ctypes.data_as(C.c_void_p)),
+          "gc_mt19937_jump_table")
+    part = torch.from_numpy(host.view(np.int32)).to(dev)
+    table = part if cur is None else torch.cat([cur[0], part])
+    _MT_TABLE[dev.index] = (table, total)
+    return _MT_TABLE[dev.index]
+
+
+def mt19937_generate(state_dev: torch.Tensor, count: int, out=None, parallel: bool = True) -> torch.Tensor:
+    """The next `count` draws of the MT19937 state on the device (625 words:
+    state + read index), which advances.  parallel: the jumped multi-generator
+    kernels (gc_mt19937_generate_jumped); else one workgroup walks the stream."""
     dev = _dev(state_dev)
     if out is None:
         out = torch.empty(count, dtype=torch.int32, device=dev)
-    check(_lib.load().gc_mt19937_generate(_p(state_dev), _p(out), count, _stream(dev)), "gc_mt19937_generate")
+    st = _stream(dev)
+    lib = _lib.load()
+    if not parallel:
+        check(lib.gc_mt19937_generate(_p(state_dev), _p(out), count, st), "gc_mt19937_generate")
+        return out
+    if count == 0:
+        return out
+    gens = -(-count // _lib.GC_MT_JUMP_DRAWS)
+    table, tgens = _mt_jump_table(dev, gens - 1) if gens > 1 else (None, 0)
+    need = int(lib.gc_mt19937_workspace_size(count))
+    key = (dev.index, st.value)
+    ws = _MT_WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = _MT_WS[key] = torch.empty(need, dtype=torch.uint8, device=dev)
+    check(lib.gc_mt19937_generate_jumped(_p(state_dev), _p(table), tgens, _p(out), count, _p(ws), st),
+          "gc_mt19937_generate_jumped")
     return out
 
 

@@ -28,7 +28,8 @@
  *   gc_ms_*_cached ........... the same pair with compressors.py:778-797's cache kept (packed cells)
  *   gc_ms_decode ............. compressors.py:819-826 (order 0) / 668-680 (order 1)
  *   gc_mt19937_seed/_generate  seed.py:6-11 torch.manual_seed + torch CPU generator stream
- *                              consumed by torch.bernoulli (compressors.py:310)
+ *   gc_mt19937_*jump*          consumed by torch.bernoulli (compressors.py:310); the
+ *                              jumped form generates it in parallel
  *   gc_greedy4_pack/_unpack .. extensions/Extension CPU/bitpacking.cpp:5-124 (host, same format)
  *   gc_greedy4_*_device ...... the same format on the device (Extension GPU/gpu_bitpacking.cpp:5-125
  *                              is host code despite its name; this is the GPU drop-in)
@@ -261,8 +262,23 @@ int gc_ms_dequantize(const void *q, uint32_t q_dtype, const int8_t *mask, uint64
 /* ---- torch CPU generator stream (MT19937) -------------------------------- */
 /* state = 624 words + next index (625 uint32); index 624 = block exhausted */
 int gc_mt19937_seed(uint64_t seed, uint32_t *state_host);
-/* out[count] = next `count` draws; state_dev (625 words, device) advances */
+/* out[count] = next `count` draws; state_dev (625 words, device) advances.
+ * One workgroup walks the serial stream (reference / small counts). */
 int gc_mt19937_generate(uint32_t *state_dev, uint32_t *out, uint64_t count, gc_stream_t stream);
+
+/* Parallel form of the same stream (bit-identical draws and final state):
+ * generator g of G = ceil(count / GC_MT_JUMP_DRAWS) emits draws [g*J, (g+1)*J)
+ * from the state jumped g*J draws ahead (GF(2) jump polynomials x^(g*J-1) mod P,
+ * P the characteristic polynomial of MT19937).  The jump table depends only on
+ * g: gc_mt19937_jump_table fills table_host[count * 624] with the coefficients
+ * of generators first .. first+count-1 (first >= 1; host computation, PCLMUL
+ * when available); callers upload it once and keep it.  workspace:
+ * gc_mt19937_workspace_size(count) device bytes, no initialisation. */
+#define GC_MT_JUMP_DRAWS 262080u /* 624 x 420 draws per generator */
+int gc_mt19937_jump_table(uint64_t first, uint64_t count, uint32_t *table_host);
+size_t gc_mt19937_workspace_size(uint64_t count);
+int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,
+                               uint64_t count, void *workspace, gc_stream_t stream);
 
 /* ---- reference-compatible packers ----------------------------------------- */
 /* greedy 4-mode format of extensions/Extension CPU/bitpacking.cpp (host

@@ -277,6 +277,44 @@ def test_mt19937_kernel_matches_oracle():
     assert bits_eq(u32(b), mt.draws(123_457))
 
 
+MTJ = gcodec._lib.GC_MT_JUMP_DRAWS
+
+
+@pytest.mark.parametrize("count", [1, 1000, MTJ - 1, MTJ, MTJ + 1, 3 * MTJ + 5])
+@pytest.mark.parametrize("pre", [0, 1, 300])
+def test_mt19937_jumped_matches_serial(count, pre):
+    """The parallel (jump-ahead) MT19937 stream == the serial one: every draw
+    and the advanced state (state array + read index) bit for bit, from read
+    indices 624 (fresh seed), 1 and 300; generator boundaries at J - 1, J, J + 1."""
+    st = codec.mt19937_seed_state(42)
+    sd = torch.from_numpy(st.view(np.int32)).to(DEV)
+    if pre:
+        codec.mt19937_generate(sd, pre, parallel=False)
+    s2 = sd.clone()
+    a = codec.mt19937_generate(sd, count)
+    b = codec.mt19937_generate(s2, count, parallel=False)
+    assert torch.equal(a, b)
+    assert torch.equal(sd, s2)
+    if count <= 3 * MTJ + 5:
+        mt = O.MT19937(42)
+        mt.draws(pre)
+        assert bits_eq(u32(a), mt.draws(count))
+
+
+def test_mt19937_jumped_1e8_vs_oracle():
+    """1e8 draws (382 generators) of the parallel stream == the oracle's
+    serial MT19937, and the final state == the serial GPU kernel's."""
+    n = 100_000_000
+    st = codec.mt19937_seed_state(1234)
+    sd = torch.from_numpy(st.view(np.int32)).to(DEV)
+    s2 = sd.clone()
+    a = codec.mt19937_generate(sd, n)
+    assert bits_eq(u32(a), O.MT19937(1234).draws(n))
+    del a
+    codec.mt19937_generate(s2, n, parallel=False)
+    assert torch.equal(sd, s2)
+
+
 @pytest.mark.parametrize("name", ["qsgd_b4_1e6_k0", "qsgd_b8_1e6_k1"])
 def test_large_digest_torch_mode(name):
     import hashlib
