@@ -214,39 +214,61 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     res["epilogue_resnet50_qsgd4"] = ep
     del base, grads, segs, flat
 
-    # config 4: GRandK K=10000, 4-bit, VGG16-sized bucket: gather -> encode -> RCCL -> decode/scatter
+    # config 4: GRandK K=10000, 4-bit, VGG16-sized bucket: gather -> encode -> RCCL -> decode/scatter.
+    # codec.RandKStep: pointers and structs resolved once, one ctypes call per launch.  W = 1: gather +
+    # max-norm + encode in one launch (gc_randk_encode_w1), then the decode-scatter; W > 1: gather + local
+    # norm, MAX, dense encode of the gathered subset, SUM, decode-scatter
     n4, K4 = 14_728_266, 10_000
     g = torch.Generator(device=dev).manual_seed(12 + rank)
     x4 = torch.randn(n4, device=dev, generator=g).mul_(0.01)
     idx = torch.randperm(n4, generator=torch.Generator().manual_seed(42))[:K4].to(dev)
-    comp = gcodec.GlobalRandKMaxNormCompressor(dev, 4, generator=gen)
-    nrm = torch.empty(1, device=dev)
+    rk = codec.RandKStep(x4, K4, 4, gen, world)
 
     def rk_step():
-        codec.absmax(x4, idx=idx, out=nrm)
-        if world > 1:
+        if rk.fused:
+            w, nrm = rk.encode(idx)
+        else:
+            _, nrm = rk.gather(idx)
             dist.all_reduce(nrm, op=dist.ReduceOp.MAX)
-        w = comp.encode(nrm, x4, world, idx=idx)
+            w = rk.encode_gathered()
+            dist.all_reduce(w)
+        rk.decode(w, idx, x4, 1.0 / world)
+
+    t = sync_ms(rk_step, reps=max(200, reps))
+    kr = max(200, reps)
+    if rk.fused:
+        kt4 = {"gather_absmax_encode (one launch)": _events(torch, lambda: rk.encode(idx), kr)}
+    else:
+        kt4 = {"gather_absmax": _events(torch, lambda: rk.gather(idx), kr),
+               "encode_gathered": _events(torch, rk.encode_gathered, kr)}
+    kt4["decode_scatter"] = _events(torch, lambda: rk.decode(rk.words, idx, x4, 1.0 / world), kr)
+    # the previous round's three-launch form (gather-absmax, gather-encode, decode-scatter), for comparison
+    nrm4 = torch.empty(1, device=dev)
+    comp = gcodec.GlobalRandKMaxNormCompressor(dev, 4, generator=gen)
+
+    def rk_step_3():
+        codec.absmax(x4, idx=idx, out=nrm4)
+        if world > 1:
+            dist.all_reduce(nrm4, op=dist.ReduceOp.MAX)
+        w = comp.encode(nrm4, x4, world, idx=idx)
         if world > 1:
             dist.all_reduce(w)
-        comp.decode(nrm, w, K4, world, 1.0, idx=idx, out=x4)
+        comp.decode(nrm4, w, K4, world, 1.0 / world, idx=idx, out=x4)
 
-    t = sync_ms(rk_step, reps=max(20, reps))
-    w4 = comp.encode(nrm, x4, world, idx=idx)
-    kt4 = {
-        "gather_absmax": _events(torch, lambda: codec.absmax(x4, idx=idx, out=nrm), max(20, reps)),
-        "gather_encode": _events(torch, lambda: comp.encode(nrm, x4, world, idx=idx), max(20, reps)),
-        "decode_scatter": _events(torch, lambda: comp.decode(nrm, w4, K4, world, 1.0, idx=idx, out=x4), max(20, reps)),
-    }
-    res["config4_grandk_k10000"] = {"n": n4, "K": K4, "us_per_step": t * 1e3,
-                                    "step": "gather-absmax, MAX, gather-encode, SUM(words), decode-scatter",
-                                    "kernels_us": {k: v * 1e3 for k, v in kt4.items()},
-                                    "bound": "host issue + launch latency (K = 10,000 elements, 12 B each)"}
+    t3 = sync_ms(rk_step_3, reps=max(200, reps))
+    gpu_us = sum(kt4.values()) * 1e3
+    res["config4_grandk_k10000"] = {
+        "n": n4, "K": K4, "us_per_step": t * 1e3, "us_per_step_three_launch_codec_calls": t3 * 1e3,
+        "step": ("gather+absmax+encode (1 launch), decode-scatter" if rk.fused else
+                 "gather+absmax, MAX, encode(gathered), SUM(words), decode-scatter"),
+        "kernels_us": {k: v * 1e3 for k, v in kt4.items()},
+        "bound": ("kernel latency (the step's launches sum to %.1f us of the %.1f us step)" % (gpu_us, t * 1e3)
+                  if gpu_us > 0.8 * t * 1e3 else
+                  "host issue (launches sum to %.1f us of the %.1f us step)" % (gpu_us, t * 1e3))}
     if world == 1:
-        # the same step captured once in a HIP graph and replayed: the C ABI
-        # enqueues on the caller's stream with no allocation or host sync, so
-        # the three launches capture as-is; a replay reuses the captured draw
-        # offset (timing only)
+        # the same step captured once in a HIP graph and replayed: the C ABI enqueues on
+        # the caller's stream with no allocation or host sync, so the launches capture
+        # as-is; a replay reuses the captured draw offset (timing only)
         try:
             graph = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(dev)
@@ -256,7 +278,7 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
             torch.cuda.current_stream(dev).wait_stream(side)
             with torch.cuda.graph(graph):
                 rk_step()
-            res["config4_grandk_k10000"]["hipgraph_us_per_step"] = _events(torch, graph.replay, max(50, reps)) * 1e3
+            res["config4_grandk_k10000"]["hipgraph_us_per_step"] = _events(torch, graph.replay, max(200, reps)) * 1e3
         except Exception as e:  # capture unsupported on this runtime: report, do not fail the bench
             res["config4_grandk_k10000"]["hipgraph_us_per_step"] = f"capture failed: {type(e).__name__}: {e}"
     del x4

@@ -130,6 +130,26 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_decode(const uint32_t *__restri
     }
 }
 
+// GlobalRandK scatter for small K (reducer.py:754 buffer[idx] = dec):
+// out[idx[i]] = RN(RN(c * (lane_i - W*s)) * alpha), one element per thread
+__global__ __launch_bounds__(kBlock) void k_decode_scatter1(const uint32_t *__restrict__ words,
+                                                           const int64_t *__restrict__ idx, uint32_t n,
+                                                           const float *__restrict__ normp, float s, int32_t sub,
+                                                           uint32_t w, uint32_t M, float alpha, float *__restrict__ out)
+{
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t plane = i / M, pos = i - plane * M;
+    const uint32_t wd = words[pos];
+    const int64_t id = idx[i];
+    const float c = *normp / s;
+    const uint32_t mask = (1u << w) - 1u;
+    const int32_t Q = (int32_t)((wd >> (plane * w)) & mask) - sub;
+    const float d = c * (float)Q;
+    out[id] = d * alpha;
+}
+
 // ---------------------------------------------------------------------------
 // unpacked quantize / dequantize (the literal compress()/decompress() drop-in)
 // ---------------------------------------------------------------------------
@@ -365,7 +385,14 @@ static int qsgd_decode(const char *what, const uint32_t *words, const int64_t *i
     } else if (mode == 1) {
         GC_DEC(1);
     } else if (mode == 2) {
-        GC_DEC(2);
+        if (n < (1ull << 32) && lanes->bits < 32 && lanes->plane_words < (1ull << 32)) {
+            // one element per thread: the word and the index load in one round trip
+            hipLaunchKernelGGL(k_decode_scatter1, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                               words, idx, (uint32_t)n, norm, sf, sub, lanes->bits, (uint32_t)lanes->plane_words,
+                               alpha, out);
+        } else {
+            GC_DEC(2);
+        }
     } else {
         GC_DEC(3);
     }

@@ -122,6 +122,9 @@ SIGNATURES = {
     "gc_mt19937_jump_table": (C.c_int, [u64, u64, P]),
     "gc_mt19937_workspace_size": (C.c_size_t, [u64]),
     "gc_mt19937_generate_jumped": (C.c_int, [P, P, u64, P, u64, P, P]),
+    "gc_randk_workspace_size": (C.c_size_t, []),
+    "gc_randk_gather_absmax": (C.c_int, [P, P, u64, P, P, P, P]),
+    "gc_randk_encode_w1": (C.c_int, [P, P, u64, P, P, u32, LANESP, RNGP, P, P, P]),
     "gc_greedy4_pack": (i64, [P, u64, P, u64]),
     "gc_greedy4_unpack": (i64, [P, u64, P, u64]),
     "gc_greedy4_workspace_size": (C.c_size_t, [u64]),

@@ -177,6 +177,147 @@ def qsgd_decode(words, n, norm, bits, world=1, alpha=1.0, idx=None, out=None, la
 
 
 # ---------------------------------------------------------------------------
+# small-K GlobalRandK (reducer.py:717-754)
+# ---------------------------------------------------------------------------
+RANDK_FUSED_MAX = 16384      # K of the one-launch W = 1 encode (gc_randk_encode_w1)
+RANDK_GATHER_MAX = 256 * 1024  # K of gc_randk_gather_absmax
+
+
+def randk_gather_absmax(x, idx, xk=None, norm=None):
+    """(xk, norm): the subset x[idx] stored contiguously and its max-norm, in one
+    launch (reducer.py:722-726).  At W > 1 the encode then reads xk densely after
+    the MAX all-reduce, so the subset is gathered once."""
+    dev = _dev(x)
+    x = _f32(x, "randk_gather_absmax")
+    idx = _idx(idx, dev)
+    k = idx.numel()
+    if xk is None:
+        xk = torch.empty(k, dtype=torch.float32, device=dev)
+    if norm is None:
+        norm = torch.empty(1, dtype=torch.float32, device=dev)
+    st = _stream(dev)
+    check(_lib.load().gc_randk_gather_absmax(_p(x), _p(idx), k, _p(xk), _p(norm), _p(_absmax_ws(dev, st)), st),
+          "gc_randk_gather_absmax")
+    return xk, norm
+
+
+def randk_encode_w1(x, idx, bits, rng, xk=None, norm=None, out=None, lanes=None):
+    """(words, norm) of the W = 1 GlobalRandK step: gather + max-norm + quantize
+    + pack in one launch (the MAX over one rank is the identity); words equal
+    qsgd_encode(x, max|x[idx]|, bits, rng, 1, idx=idx)."""
+    dev = _dev(x)
+    x = _f32(x, "randk_encode_w1")
+    idx = _idx(idx, dev)
+    k = idx.numel()
+    lanes = lanes or qsgd_layout(k, bits, 1)
+    if xk is None:
+        xk = torch.empty(k, dtype=torch.float32, device=dev)
+    if norm is None:
+        norm = torch.empty(1, dtype=torch.float32, device=dev)
+    if out is None:
+        out = torch.empty(lanes.plane_words, dtype=torch.int32, device=dev)
+    r = rng.struct()
+    st = _stream(dev)
+    check(_lib.load().gc_randk_encode_w1(_p(x), _p(idx), k, _p(xk), _p(norm), bits, C.byref(lanes), C.byref(r),
+                                         _p(out), _p(_absmax_ws(dev, st)), st), "gc_randk_encode_w1")
+    return out, norm
+
+
+class RandKStep:
+    """A pre-resolved GlobalRandK encode / decode for a fixed bucket, K and lane
+    layout (BASELINE config 4: K = 10,000 of a 14.7M bucket).  At this size the
+    kernels take a few microseconds and an eager step is bound by the host work
+    of each call (argument checks, layout and workspace lookups, ctypes struct
+    building: 7-10 us per call, profiles/r01s_host_overhead.log); here every
+    pointer and struct is built once and a call is one ctypes call.  Philox
+    draws only (torch mode draws come from the host generator every call:
+    use the codec functions).
+
+        step = RandKStep(x, k, bits, generator, world)
+        words, norm = step.encode(idx)          # W = 1: one launch
+        xk, local = step.gather(idx)            # W > 1: gather + local norm,
+        step.encode_gathered()                  #   MAX all-reduce, dense encode
+        step.decode(words, idx, out, alpha)     # decode + scatter
+    """
+
+    def __init__(self, x, k: int, bits: int, generator, world: int = 1):
+        dev = _dev(x)
+        if generator.mode != "philox":
+            raise _lib.GCodecError(_lib.GC_EINVAL, "RandKStep: Philox generators only")
+        self.x = _f32(x, "RandKStep")
+        self.k, self.bits, self.world, self.gen, self.device = int(k), int(bits), int(world), generator, dev
+        self.lanes = qsgd_layout(self.k, self.bits, self.world)
+        self.words = torch.empty(self.lanes.plane_words, dtype=torch.int32, device=dev)
+        self.norm = torch.empty(1, dtype=torch.float32, device=dev)
+        self.xk = torch.empty(self.k, dtype=torch.float32, device=dev)
+        self.fused = self.world == 1 and self.k <= RANDK_FUSED_MAX
+        self._rng = _lib.gc_rng(_lib.GC_RNG_PHILOX, 0, 0, 0, None)
+        self._ws = {}
+        lib = _lib.load()
+        self._enc1, self._gather, self._enc, self._dec = (lib.gc_randk_encode_w1, lib.gc_randk_gather_absmax,
+                                                          lib.gc_qsgd_encode, lib.gc_qsgd_decode)
+        self._xp, self._xkp, self._np, self._wp = (self.x.data_ptr(), self.xk.data_ptr(), self.norm.data_ptr(),
+                                                   self.words.data_ptr())
+        self._lanes_ref = C.byref(self.lanes)
+        self._rng_ref = C.byref(self._rng)
+        self._idx = None
+        self._idxp = None
+
+    def _ws_for(self, st):
+        ws = self._ws.get(st.value)
+        if ws is None:
+            ws = self._ws[st.value] = _absmax_ws(self.device, st).data_ptr()
+        return ws
+
+    def _set_idx(self, idx):
+        if idx is not self._idx:
+            if idx.numel() != self.k or idx.dtype != torch.int64 or idx.device != self.device or not idx.is_contiguous():
+                raise _lib.GCodecError(_lib.GC_EINVAL, f"RandKStep: idx must be {self.k} contiguous int64 on "
+                                       f"{self.device}")
+            self._idx, self._idxp = idx, idx.data_ptr()
+
+    def _draws(self):
+        self._rng.seed = self.gen.reserve_key() & (2 ** 64 - 1)
+        self._rng.offset = self.gen.offset
+        self.gen.offset += self.k
+
+    def encode(self, idx):
+        """W = 1: gather + max-norm + encode in one launch -> (words, norm)."""
+        if not self.fused:
+            raise _lib.GCodecError(_lib.GC_EINVAL, "RandKStep.encode: the one-launch step needs W = 1 and "
+                                   f"K <= {RANDK_FUSED_MAX}; use gather() + encode_gathered()")
+        self._set_idx(idx)
+        self._draws()
+        st = _stream(self.device)
+        check(self._enc1(self._xp, self._idxp, self.k, self._xkp, self._np, self.bits, self._lanes_ref,
+                         self._rng_ref, self._wp, self._ws_for(st), st), "gc_randk_encode_w1")
+        return self.words, self.norm
+
+    def gather(self, idx):
+        """xk = x[idx] and its local max-norm (before the MAX all-reduce)."""
+        self._set_idx(idx)
+        st = _stream(self.device)
+        check(self._gather(self._xp, self._idxp, self.k, self._xkp, self._np, self._ws_for(st), st),
+              "gc_randk_gather_absmax")
+        return self.xk, self.norm
+
+    def encode_gathered(self):
+        """encode of the gathered subset with the (global) norm in self.norm."""
+        self._draws()
+        st = _stream(self.device)
+        check(self._enc(self._xkp, None, self.k, self._np, self.bits, self._lanes_ref, self._rng_ref, self._wp, st),
+              "gc_qsgd_encode")
+        return self.words
+
+    def decode(self, words, idx, out, alpha: float):
+        """out[idx] = decode(words) * alpha (the scatter of reducer.py:754)."""
+        self._set_idx(idx)
+        check(self._dec(words.data_ptr(), self._idxp, self.k, self._np, self.bits, self._lanes_ref, float(alpha),
+                        out.data_ptr(), _stream(self.device)), "gc_qsgd_decode")
+        return out
+
+
+# ---------------------------------------------------------------------------
 # per-parameter tensors (reducer.py:46-68 TensorBuffer, 543-549 setgrad)
 # ---------------------------------------------------------------------------
 class Segments:

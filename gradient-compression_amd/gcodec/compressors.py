@@ -76,6 +76,12 @@ class QSGDMaxNormCompressor(_Base):
 class GlobalRandKMaxNormCompressor(QSGDMaxNormCompressor):
     """compressors.py:419-456 — the same arithmetic applied to the K-subset."""
 
+    def encode_w1(self, tensor, idx, out=None):
+        """W = 1: gather + max-norm + encode of tensor[idx] in one launch ->
+        (words, norm); the same words as encode(max|tensor[idx]|, tensor, idx=idx)."""
+        rng = self._reserve(idx.numel(), 1, tensor.device)
+        return self.backend.randk_encode_w1(tensor, idx, self._quantization_level, rng, out=out)
+
 
 class _MultiScalePacked(_Base):
     """Packed mask + select of the two-scale and multi-scale classes.

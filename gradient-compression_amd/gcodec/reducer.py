@@ -246,9 +246,22 @@ class GlobalRandKMaxNormReducer(Reducer):
         n = flat.buffer.numel()
         idx = self._next_indices(n).to(flat.buffer.device, non_blocking=True)
         k = idx.numel()
-        norm = self._max_norm(flat, idx=idx)
-        with self._timer("reduce.compress", verbosity=2):
-            words = comp.encode(norm, flat.buffer, world=W, idx=idx)
+        codec = self._codec
+        if W == 1 and hasattr(codec, "randk_encode_w1") and k <= codec.RANDK_FUSED_MAX:
+            # gather + max-norm + encode in one launch (the MAX over one rank is the identity)
+            with self._timer("reduce.compress", verbosity=2):
+                words, norm = comp.encode_w1(flat.buffer, idx)
+        elif hasattr(codec, "randk_gather_absmax") and k <= codec.RANDK_GATHER_MAX:
+            # the subset gathered once (with its local norm); the encode reads it densely
+            with self._timer("reduce.norm", verbosity=2):
+                xk, local = codec.randk_gather_absmax(flat.buffer, idx)
+                norm = self._all_reduce(local, dist.ReduceOp.MAX)
+            with self._timer("reduce.compress", verbosity=2):
+                words = comp.encode(norm, xk, world=W)
+        else:
+            norm = self._max_norm(flat, idx=idx)
+            with self._timer("reduce.compress", verbosity=2):
+                words = comp.encode(norm, flat.buffer, world=W, idx=idx)
         with self._timer("reduce.reduce.vector", verbosity=2):
             self._all_reduce(words)
         bits = self.n_bits(norm) + self.n_bits(words)
@@ -275,11 +288,21 @@ class QSGDMaxNormTwoScaleReducer(Reducer):
 
     def _reduce_scales(self, comp, flat, idx, n, local=None):
         W = self.n_workers
-        norm = self._max_norm(flat, local, idx)
+        codec = self._codec
+        x = flat.buffer
+        if idx is not None and hasattr(codec, "randk_gather_absmax") and idx.numel() <= codec.RANDK_GATHER_MAX:
+            # GlobalRandK: gather the subset once (with its local norm); both
+            # multi-scale passes then read it densely
+            with self._timer("reduce.norm", verbosity=2):
+                x, local = codec.randk_gather_absmax(flat.buffer, idx)
+                norm = self._all_reduce(local, dist.ReduceOp.MAX)
+            idx = None
+        else:
+            norm = self._max_norm(flat, local, idx)
         with self._timer("reduce.compress", verbosity=2):
-            mask = comp.encode_mask(norm, flat.buffer, world=W, idx=idx)
+            mask = comp.encode_mask(norm, x, world=W, idx=idx)
             self._all_reduce(mask)
-            words = comp.encode(norm, flat.buffer, mask, world=W, idx=idx)
+            words = comp.encode(norm, x, mask, world=W, idx=idx)
         with self._timer("reduce.reduce.vector", verbosity=2):
             self._all_reduce(words)
         bits = self.n_bits(norm) + self.n_bits(mask) + self.n_bits(words)

@@ -97,12 +97,15 @@ class Generator:
         self.offset = 0
         return self
 
+    def reserve_key(self) -> int:
+        """The Philox key the next reservation uses (seed, + rank if per_rank)."""
+        return self.seed + (_process_rank() if self.per_rank else 0)
+
     def reserve(self, n: int, levels: int = 1, device=None, backend=None) -> Reservation:
         """Reserve n*levels draws (advances the stream like torch's generator)."""
         count = n * levels
         if self.mode == "philox":
-            key = self.seed + (_process_rank() if self.per_rank else 0)
-            r = Reservation(_lib.GC_RNG_PHILOX, key, self.offset, None, n, levels)
+            r = Reservation(_lib.GC_RNG_PHILOX, self.reserve_key(), self.offset, None, n, levels)
             self.offset += count
             return r
         if backend is None:

@@ -18,6 +18,8 @@
  *                              extensions/Extension CPU/bitpacking.cpp:5-61 (carry-free lanes)
  *   gc_qsgd_decode ........... compressors.py:318-321 decompress (+ reducer.py:549 alpha=1/W,
  *                              + reducer.py:754 scatter with idx)
+ *   gc_randk_* ............... reducer.py:722-735 GlobalRandK gather buffer[idx] + its max-norm
+ *                              (+ compressors.py:435-451 compress, fused at W = 1)
  *   gc_qsgd_quantize ......... compressors.py:299-316, unpacked int8/int32 output (literal drop-in)
  *   gc_qsgd_dequantize ....... compressors.py:318-321, unpacked input
  *   gc_lane_pack/_unpack ..... extensions/Extension GPU/gpu_bitpacking.cpp:5-125 intent
@@ -159,6 +161,22 @@ int gc_qsgd_dequantize(const void *q, uint32_t q_dtype, uint64_t n, const float 
 int gc_lane_pack(const void *q, uint32_t q_dtype, const gc_lanes *lanes, uint32_t *words, gc_stream_t stream);
 /* q[i] = lane - world*offset (the W-way sum) */
 int gc_lane_unpack(const uint32_t *words, const gc_lanes *lanes, int32_t *q, gc_stream_t stream);
+
+/* ---- small-K GlobalRandK (reducer.py:717-754, compressors.py:419-456) -------
+ * One element per thread over ceil(k/1024) blocks: xk[i] = x[idx[i]] (the subset,
+ * contiguous) and *norm = max |xk| in one launch (the last block to finish reduces
+ * the partials; workspace: gc_randk_workspace_size() device bytes zeroed once,
+ * self-resetting, one per stream).  k <= 262144.  At W > 1 the encode then runs
+ * on xk after the MAX all-reduce (gc_qsgd_encode, dense): the subset is gathered
+ * once.  gc_randk_encode_w1 is the W = 1 step (the MAX over one rank is the
+ * identity): gather + max-norm + quantize + pack in ONE launch, words identical to
+ * gc_qsgd_encode(x, idx, ...) with lanes = gc_qsgd_layout(k, bits, 1); k <= 16384.
+ * The decode-scatter is gc_qsgd_decode with idx. */
+size_t gc_randk_workspace_size(void);
+int gc_randk_gather_absmax(const float *x, const int64_t *idx, uint64_t k, float *xk, float *norm, void *workspace,
+                           gc_stream_t stream);
+int gc_randk_encode_w1(const float *x, const int64_t *idx, uint64_t k, float *xk, float *norm, uint32_t bits,
+                       const gc_lanes *lanes, const gc_rng *rng, uint32_t *words, void *workspace, gc_stream_t stream);
 
 /* ---- greedy 4-mode packer on the device --------------------------------------
  * The format of gc_greedy4_pack (Extension CPU/bitpacking.cpp:5-124) produced by

@@ -48,6 +48,22 @@ def absmax(x, idx=None, out=None):
     return v
 
 
+RANDK_FUSED_MAX = 16384
+RANDK_GATHER_MAX = 256 * 1024
+
+
+def randk_gather_absmax(x, idx, xk=None, norm=None):
+    xs = _gather(x, idx)
+    return torch.from_numpy(xs.copy()), torch.tensor([O.absmax(xs)], dtype=torch.float32)
+
+
+def randk_encode_w1(x, idx, bits, rng, xk=None, norm=None, out=None, lanes=None):
+    xs = _gather(x, idx)
+    nk = O.absmax(xs)
+    words = O.qsgd_encode(xs, nk, bits, 1, _rng(rng))
+    return torch.from_numpy(words.view(np.int32).copy()), torch.tensor([nk], dtype=torch.float32)
+
+
 def qsgd_encode(x, norm, bits, rng, world=1, idx=None, out=None, lanes=None):
     words = O.qsgd_encode(_gather(x, idx), _norm(norm), bits, world, _rng(rng))
     return torch.from_numpy(words.view(np.int32).copy())

@@ -783,3 +783,97 @@ def test_absmax_workspace_reuse_many_grids(n):
     for i in range(50):
         codec.absmax(xd, out=out[i:i + 1])
     assert np.all(out.cpu().numpy() == O.absmax(x))
+
+
+# --------------------------------------------------------------------------- small-K GlobalRandK (config 4)
+@pytest.mark.parametrize("bits", [1, 2, 4, 8])
+@pytest.mark.parametrize("K", [1, 3, 1000, 10_000, 16_384])
+def test_randk_fused_w1_vs_oracle(bits, K):
+    """gc_randk_encode_w1: gather + max-norm + encode in one launch (W = 1) ==
+    the oracle's encode of x[idx] with max |x[idx]|; the subset and the norm
+    are written too."""
+    n = 300_007
+    x = O.gen_input(n, seed=K + 17 * bits, kind=K % 2)
+    idx = np.random.default_rng(K).permutation(n)[:K].astype(np.int64)
+    r = gcodec.rng.Reservation(0, 23 + bits, 7 * K, None, K, 1)
+    xk = torch.empty(K, dtype=torch.float32, device=DEV)
+    words, norm = codec.randk_encode_w1(dev(x), dev(idx), bits, r, xk=xk)
+    nk = O.absmax(x[idx])
+    assert norm.item() == float(nk)
+    assert bits_eq(u32(xk), x[idx].view(np.uint32))
+    assert bits_eq(u32(words), O.qsgd_encode(x[idx], nk, bits, 1, O.philox_rng(23 + bits, 7 * K)))
+
+
+def test_randk_fused_w1_torch_stream_and_edges():
+    """the fused kernel with caller draws (torch-mode stream), NaN / +-inf /
+    zero subsets vs the oracle, and the ticket re-armed across many calls"""
+    n, K, bits = 50_021, 10_000, 4
+    x = O.gen_input(n, seed=5, kind=1)
+    idx = np.random.default_rng(2).permutation(n)[:K].astype(np.int64)
+    draws = O.MT19937(9).draws(K)
+    rs = gcodec.rng.Reservation(1, 0, 0, dev(draws.view(np.int32)), K, 1)
+    words, norm = codec.randk_encode_w1(dev(x), dev(idx), bits, rs)
+    nk = O.absmax(x[idx])
+    assert bits_eq(u32(words), O.qsgd_encode(x[idx], nk, bits, 1, O.stream_rng(draws)))
+    xz = np.zeros(n, np.float32)
+    w0, n0 = codec.randk_encode_w1(dev(xz), dev(idx), bits, gcodec.rng.Reservation(0, 1, 0, None, K, 1))
+    assert n0.item() == 0.0
+    assert bits_eq(u32(w0), O.qsgd_encode(xz[idx], np.float32(0), bits, 1, O.philox_rng(1, 0)))
+    x2 = x.copy()
+    x2[idx[17]] = np.inf
+    x2[idx[9000]] = np.nan
+    for i in range(30):  # many launches on one workspace (self-resetting ticket)
+        w2, n2 = codec.randk_encode_w1(dev(x2), dev(idx), bits, gcodec.rng.Reservation(0, 3, i, None, K, 1))
+    assert np.isnan(n2.item())
+    assert bits_eq(u32(w2), O.qsgd_encode(x2[idx], np.float32(np.nan), bits, 1, O.philox_rng(3, 29)))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("K", [7, 10_000, 262_144])
+def test_randk_gather_then_dense_encode(world, K):
+    """W > 1 path: gc_randk_gather_absmax (subset + local norm, one launch),
+    then the dense encode of the subset == the gather encode through idx ==
+    the oracle; and the one-element-per-thread decode-scatter."""
+    n = 1_000_003
+    x = O.gen_input(n, seed=K + world, kind=1)
+    idx = np.random.default_rng(K + 1).permutation(n)[:K].astype(np.int64)
+    xd, idd = dev(x), dev(idx)
+    xk, nk = codec.randk_gather_absmax(xd, idd)
+    assert bits_eq(u32(xk), x[idx].view(np.uint32))
+    assert nk.item() == float(O.absmax(x[idx]))
+    r = gcodec.rng.Reservation(0, 4, 11, None, K, 1)
+    wd = codec.qsgd_encode(xk, nk, 4, r, world)
+    assert torch.equal(wd, codec.qsgd_encode(xd, nk, 4, r, world, idx=idd))
+    ref = O.qsgd_encode(x[idx], O.absmax(x[idx]), 4, world, O.philox_rng(4, 11))
+    assert bits_eq(u32(wd), ref)
+    wsum = (wd.to(torch.int64) * world).to(torch.int32)
+    out = dev(x)
+    codec.qsgd_decode(wsum, K, nk, 4, world, 1.0 / world, idx=idd, out=out)
+    exp = x.copy()
+    refsum = (ref.astype(np.uint64) * world).astype(np.uint32)
+    exp[idx] = O.qsgd_decode(refsum, K, O.absmax(x[idx]), 4, world, np.float32(1.0 / world))
+    assert bits_eq(u32(out), exp.view(np.uint32))
+
+
+def test_randk_step_matches_codec_calls():
+    """codec.RandKStep (pre-resolved pointers, one ctypes call per launch) ==
+    the plain codec calls, step after step (draw offsets advance by K)."""
+    n, K, bits = 14_728_266, 10_000, 4
+    g = torch.Generator(device=DEV).manual_seed(12)
+    x = torch.randn(n, device=DEV, generator=g).mul_(0.01)
+    idx = torch.randperm(n, generator=torch.Generator().manual_seed(42))[:K].to(DEV)
+    ga, gb = gcodec.Generator(5, "philox"), gcodec.Generator(5, "philox")
+    step = codec.RandKStep(x, K, bits, ga)
+    out_a, out_b = x.clone(), x.clone()
+    for _ in range(3):
+        wa, na = step.encode(idx)
+        wb, nb = codec.randk_encode_w1(x, idx, bits, gb.reserve(K))
+        assert torch.equal(wa, wb) and torch.equal(na, nb)
+        step.decode(wa, idx, out_a, 1.0)
+        codec.qsgd_decode(wb, K, nb, bits, 1, 1.0, idx=idx, out=out_b)
+        assert torch.equal(out_a, out_b)
+    assert ga.offset == gb.offset == 3 * K
+    xk, nk = step.gather(idx)
+    w2 = step.encode_gathered()
+    assert torch.equal(w2, codec.qsgd_encode(x, nk, bits, gcodec.rng.Reservation(0, 5, 3 * K, None, K, 1), 1,
+                                             idx=idx))
