@@ -153,11 +153,13 @@ __global__ __launch_bounds__(kBlock) void k_decode_scatter1(const uint32_t *__re
 // ---------------------------------------------------------------------------
 // unpacked quantize / dequantize (the literal compress()/decompress() drop-in)
 // ---------------------------------------------------------------------------
-template <int KIND, int MODE, typename QT>
+// SPLIT (the QSGDBP call site, compressors.py:344-353): q = xi (>= 0) and
+// sgn = 1 iff x < 0 as two int32 arrays, the greedy packer's two inputs
+template <int KIND, int MODE, typename QT, bool SPLIT = false>
 __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float *__restrict__ x, uint64_t n,
                                                           const float *__restrict__ normp, float s, uint32_t level,
                                                           RngArgs rng, QT *__restrict__ q, int8_t *__restrict__ le,
-                                                          int32_t le_max)
+                                                          int32_t le_max, int32_t *__restrict__ sgn = nullptr)
 {
     const float norm = *normp;
     const uint64_t groups = (n + 3) >> 2;
@@ -169,6 +171,11 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float *__restric
         for (int e = 0; e < 4; ++e) {
             if (i0 + e < n) {
                 const QElem qe = q_elem(pickf(v, e), norm, s, pick(r, e));
+                if constexpr (SPLIT) {
+                    q[i0 + e] = (QT)qe.xi;
+                    sgn[i0 + e] = pickf(v, e) < 0.0f ? 1 : 0;
+                    continue;
+                }
                 q[i0 + e] = (QT)(qe.sg * qe.xi);
                 if (le)
                     le[i0 + e] = (int8_t)(qe.xi <= le_max ? 1 : 0);
@@ -456,6 +463,32 @@ int gc_qsgd_quantize_le(const float *x, uint64_t n, const float *norm, uint32_t 
     }
 #undef GC_Q
     return launch_status("gc_qsgd_quantize");
+}
+
+int gc_qsgd_quantize_split(const float *x, uint64_t n, const float *norm, uint32_t bits, const gc_rng *rng,
+                           int32_t *xi, int32_t *sign, gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_bits(bits, "gc_qsgd_quantize_split")) || (rc = check_rng(rng, "gc_qsgd_quantize_split")))
+        return rc;
+    GC_REQUIRE(n == 0 || (x && xi && sign && norm), "gc_qsgd_quantize_split: null pointer");
+    if (n == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const RngArgs ra = rng_args(rng, n);
+    const float sf = (float)((1u << bits) - 1u);
+    const unsigned grid = grid_for((n + 3) >> 2);
+    const bool vec = aligned16(x);
+#define GC_QS(KIND_, MODE_)                                                                                         \
+    hipLaunchKernelGGL((k_qsgd_quantize<KIND_, MODE_, int32_t, true>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, \
+                       sf, 0u, ra, xi, nullptr, 0, sign)
+    if (rng->kind == GC_RNG_PHILOX) {
+        if (vec) GC_QS(0, 0); else GC_QS(0, 1);
+    } else {
+        if (vec) GC_QS(1, 0); else GC_QS(1, 1);
+    }
+#undef GC_QS
+    return launch_status("gc_qsgd_quantize_split");
 }
 
 int gc_qsgd_dequantize(const void *q, uint32_t q_dtype, uint64_t n, const float *norm, uint32_t bits, float alpha,

@@ -9,6 +9,7 @@ from ._lib import GCodecError  # noqa: F401
 from .compressors import (  # noqa: F401
     GlobalRandKMaxNormCompressor,
     GlobalRandKMaxNormTwoScaleCompressor,
+    QSGDBPCompressor,
     QSGDMaxNormCompressor,
     QSGDMaxNormMultiScaleCompressor,
     QSGDMaxNormTwoScaleCompressor,

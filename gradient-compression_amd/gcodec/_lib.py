@@ -99,6 +99,7 @@ SIGNATURES = {
     "gc_qsgd_quantize": (C.c_int, [P, u64, P, u32, RNGP, u32, P, u32, P]),
     "gc_qsgd_quantize_le": (C.c_int, [P, u64, P, u32, RNGP, u32, P, u32, P, u32, P]),
     "gc_qsgd_dequantize": (C.c_int, [P, u32, u64, P, u32, f32, P, P]),
+    "gc_qsgd_quantize_split": (C.c_int, [P, u64, P, u32, RNGP, P, P, P]),
     "gc_lane_pack": (C.c_int, [P, u32, LANESP, P, P]),
     "gc_lane_unpack": (C.c_int, [P, LANESP, P, P]),
     "gc_segments_chunks": (u64, [u64, u32]),

@@ -422,6 +422,20 @@ def qsgd_quantize(x, norm, bits, rng, level=0, dtype=torch.int8, le_bits=None):
     return (q, le) if le_bits else q
 
 
+def qsgd_quantize_split(x, norm, bits, rng):
+    """(xi, sign): int32 magnitudes and 1-iff-negative sign bits (the QSGDBP
+    call site, compressors.py:344-353)."""
+    dev = _dev(x)
+    x = _f32(x, "qsgd_quantize_split")
+    nt = norm_tensor(norm, dev)
+    xi = torch.empty(x.numel(), dtype=torch.int32, device=dev)
+    sg = torch.empty(x.numel(), dtype=torch.int32, device=dev)
+    r = rng.struct()
+    check(_lib.load().gc_qsgd_quantize_split(_p(x), x.numel(), _p(nt), bits, C.byref(r), _p(xi), _p(sg),
+                                             _stream(dev)), "gc_qsgd_quantize_split")
+    return xi, sg
+
+
 def qsgd_dequantize(q, norm, bits, alpha=1.0, out=None):
     dev = _dev(q)
     q = q.contiguous().view(-1)

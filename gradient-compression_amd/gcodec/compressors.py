@@ -8,6 +8,7 @@ kernels of libgcodec.
     QSGDMaxNormTwoScaleCompressor    612-680         QSGDMaxNormTwoScaleCompressor
     GlobalRandKMaxNormTwoScaleCompressor 683-751     GlobalRandKMaxNormTwoScaleCompressor
     QSGDMaxNormMultiScaleCompressor  754-826         QSGDMaxNormMultiScaleCompressor
+    QSGDBPCompressor (commented)     324-378         QSGDBPCompressor (greedy 4-mode packing on the GPU)
 
 compress()/decompress() return exactly what the reference returns (int8 for
 b < 8 else int32; float32), on the same device.  With the generator in
@@ -23,6 +24,7 @@ sorts the caller's level list instead of sorting it in place (768).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import codec as _codec
@@ -81,6 +83,45 @@ class GlobalRandKMaxNormCompressor(QSGDMaxNormCompressor):
         (words, norm); the same words as encode(max|tensor[idx]|, tensor, idx=idx)."""
         rng = self._reserve(idx.numel(), 1, tensor.device)
         return self.backend.randk_encode_w1(tensor, idx, self._quantization_level, rng, out=out)
+
+
+class QSGDBPCompressor(_Base):
+    """compressors.py:324-378 (kept commented out in the reference because it
+    needs the custom extension): QSGD with the bucket's own max-norm, the sign
+    bits and the magnitudes packed separately in the greedy 4-mode format of
+    extensions/Extension CPU/bitpacking.cpp.  Code: (norm / s, sign_packed,
+    xi_packed, xi_size).  Here the quantize (gc_qsgd_quantize_split) and both
+    packers (gc_greedy4_pack_device / _unpack_device) run on the GPU — the
+    reference moves each array to the host, packs it there and copies it back
+    (compressors.py:357-358, 370-372).  Defined for b <= 8 (the format's
+    domain is [0, 255])."""
+
+    def __init__(self, device, quantization_level=8, generator=None):
+        super().__init__(device, generator)
+        if not 1 <= quantization_level <= 8:
+            raise ValueError("QSGDBPCompressor: the greedy 4-mode format holds values in [0, 255] (b <= 8)")
+        self._quantization_level = quantization_level
+
+    def compress(self, tensor):
+        s = (1 << self._quantization_level) - 1
+        norm = self.backend.absmax(tensor)  # compressors.py:341 (the bucket's own max)
+        rng = self._reserve(tensor.numel(), 1, tensor.device)
+        xi, sign = self.backend.qsgd_quantize_split(tensor, norm, self._quantization_level, rng)
+        sign_packed = self.backend.greedy4_pack(sign)
+        xi_packed = self.backend.greedy4_pack(xi)
+        xi_size = torch.tensor(xi_packed.size(), device=tensor.device)
+        # norm / s, correctly rounded (numpy float32 division; the packers above already synchronised)
+        c = torch.tensor(np.float32(norm.item()) / np.float32(s), dtype=torch.float32, device=tensor.device)
+        return c, sign_packed, xi_packed, xi_size
+
+    def decompress(self, norm, sign_packed, xi_packed, tensor_size):
+        n = int(tensor_size)
+        sign = self.backend.greedy4_unpack(sign_packed)[:n]
+        xi = self.backend.greedy4_unpack(xi_packed)[:n]
+        # norm * sign * xi in the reference's order, fp32: (c * (+-1)) is exact, then one
+        # rounding; a negative x that rounded to 0 decodes to -0.0 as in the reference
+        sgn = torch.where(sign == 1, -1.0, 1.0).to(torch.float32)
+        return (norm * sgn) * xi.to(torch.float32)
 
 
 class _MultiScalePacked(_Base):

@@ -22,6 +22,7 @@
  *                              (+ compressors.py:435-451 compress, fused at W = 1)
  *   gc_qsgd_quantize ......... compressors.py:299-316, unpacked int8/int32 output (literal drop-in)
  *   gc_qsgd_dequantize ....... compressors.py:318-321, unpacked input
+ *   gc_qsgd_quantize_split ... compressors.py:338-353 QSGDBPCompressor.compress (sign bits + xi)
  *   gc_lane_pack/_unpack ..... extensions/Extension GPU/gpu_bitpacking.cpp:5-125 intent
  *                              (device packing of quantized ints), sum-compatible format
  *   gc_ms_mask_encode ........ compressors.py:778-807 compress_cache + compress_mask
@@ -153,6 +154,11 @@ int gc_qsgd_quantize(const float *x, uint64_t n, const float *norm, uint32_t bit
 int gc_qsgd_quantize_le(const float *x, uint64_t n, const float *norm, uint32_t bits, const gc_rng *rng,
                         uint32_t level, void *q, uint32_t q_dtype, int8_t *le_mask, uint32_t le_bits,
                         gc_stream_t stream);
+/* the QSGDBP call site (compressors.py:338-353): xi[i] = stochastic_round(|x[i]| / *norm * s)
+ * and sign[i] = 1 iff x[i] < 0 (0 for +-0), two int32 arrays — the inputs the
+ * reference hands to its greedy packer (bitpacking.packing, compressors.py:357-358) */
+int gc_qsgd_quantize_split(const float *x, uint64_t n, const float *norm, uint32_t bits, const gc_rng *rng,
+                           int32_t *xi, int32_t *sign, gc_stream_t stream);
 /* out[i] = RN(RN(RN(*norm/s) * q[i]) * alpha) */
 int gc_qsgd_dequantize(const void *q, uint32_t q_dtype, uint64_t n, const float *norm, uint32_t bits,
                        float alpha, float *out, gc_stream_t stream);

@@ -877,3 +877,28 @@ def test_randk_step_matches_codec_calls():
     w2 = step.encode_gathered()
     assert torch.equal(w2, codec.qsgd_encode(x, nk, bits, gcodec.rng.Reservation(0, 5, 3 * K, None, K, 1), 1,
                                              idx=idx))
+
+
+# --------------------------------------------------------------------------- QSGDBP call site (a14)
+def test_qsgdbp_compressor_matches_reference_vectors():
+    """gcodec.QSGDBPCompressor (compressors.py:324-378): device quantize into
+    sign bits + magnitudes, device greedy 4-mode packing, unpack + truncate +
+    sign map — against vectors made with the reference's quantizer and its own
+    compiled bitpacking extension (tests/golden/make_golden_bp.py), torch mode."""
+    z = gz("qsgdbp.npz")
+    cases = sorted({k.split("/")[0] for k in z.files})
+    gcodec.set_rng_mode("torch")
+    try:
+        for c in cases:
+            x, bits = z[f"{c}/x"], int(z[f"{c}/bits"])
+            torch.manual_seed(int(z[f"{c}/seed"]))
+            comp = gcodec.QSGDBPCompressor(DEV, bits)
+            norm_s, sp, xp, size = comp.compress(dev(x))
+            assert norm_s.item() == float(z[f"{c}/norm_over_s"]), c
+            assert bits_eq(sp.cpu().numpy(), z[f"{c}/sign_packed"]), c
+            assert bits_eq(xp.cpu().numpy(), z[f"{c}/xi_packed"]), c
+            assert int(size.item()) == int(z[f"{c}/xi_size"])
+            d = comp.decompress(norm_s, sp, xp, x.size)
+            assert bits_eq(u32(d), z[f"{c}/dec"].view(np.uint32)), c
+    finally:
+        gcodec.set_rng_mode("philox")

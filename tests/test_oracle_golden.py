@@ -211,3 +211,30 @@ def test_lane_pack_roundtrip_and_sum_compat():
         assert tot.max() < 2 ** 32
         got = O.lane_unpack(tot.astype(np.uint32), n, s, W, w, L, M)
         assert np.array_equal(got, np.sum(qs, axis=0))
+
+
+def _bp_cases():
+    z = _load("qsgdbp.npz")
+    return z, sorted({k.split("/")[0] for k in z.files})
+
+
+def test_qsgdbp_golden_vs_oracle():
+    """The QSGDBP call site fixture (tests/golden/make_golden_bp.py: the
+    reference's quantizer + its compiled greedy packer) restated by the
+    oracle: MT19937 draws -> quantize -> sign bits / magnitudes -> greedy4."""
+    z, cases = _bp_cases()
+    assert cases
+    for c in cases:
+        x, bits = z[f"{c}/x"], int(z[f"{c}/bits"])
+        norm = O.absmax(x)
+        q = O.qsgd_quantize(x, norm, bits, O.stream_rng(O.MT19937(int(z[f"{c}/seed"])).draws(x.size)))
+        sign = (x < 0).astype(np.int32)
+        assert np.array_equal(O.greedy4_pack(sign), z[f"{c}/sign_packed"]), c
+        assert np.array_equal(O.greedy4_pack(np.abs(q)), z[f"{c}/xi_packed"]), c
+        assert int(z[f"{c}/xi_size"]) == z[f"{c}/xi_packed"].size
+        s = (1 << bits) - 1
+        assert np.float32(norm) / np.float32(s) == z[f"{c}/norm_over_s"]
+        # (norm / s) * sign * xi with sign in {-1, +1}: a negative x that rounds to 0 gives -0.0
+        sgn = np.where(sign == 1, np.float32(-1), np.float32(1))
+        dec = (np.float32(norm) / np.float32(s) * sgn).astype(np.float32) * np.abs(q).astype(np.float32)
+        assert dec.astype(np.float32).tobytes() == z[f"{c}/dec"].tobytes(), c
