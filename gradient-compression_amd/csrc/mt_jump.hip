@@ -13,10 +13,11 @@
 //   k_mt_seq    one workgroup: the first 20561 raw words x_0.. of the stream
 //               (32 twists of the state) into the workspace; window 0 = the
 //               state itself, plus the read index
-//   k_mt_jump   one workgroup per generator g >= 1: x_0..x_20560 in LDS (82 KB),
-//               624 threads, thread j accumulates the XOR over the 19937
-//               coefficient bits (uniform per block: scalar loads of the jump
-//               table; per bit a uniform 0 / ~0 mask and one xor-and)
+//   k_mt_jump   one workgroup per generator g >= 1: the stream x_0..x_20560 in
+//               LDS (four shifted copies, in four quarters), 320 threads, each
+//               accumulating two window words over the 19937 coefficient bits
+//               (uniform per block: scalar loads of the jump table; per bit a
+//               uniform 0 / ~0 mask and one xor-and per word)
 //   k_mt_gen    one wave per generator: its window in LDS, wave-synchronous
 //               3-phase twists, tempered draws stored coalesced; the last
 //               generator writes the advanced state back
@@ -31,9 +32,8 @@ constexpr uint32_t kMtN = 624;
 constexpr uint32_t kMtM = 397;
 constexpr uint32_t kMtJ = GC_MT_JUMP_DRAWS;
 constexpr uint32_t kMtSeq = 19937 + kMtN;              // x_0 .. x_20560 (k + j <= 19936 + 624)
-constexpr uint32_t kMtSeqLds = 623 * 32 + 32 + kMtN;  // every (cw, b, j) read in bounds (pad = 0)
 constexpr uint32_t kMtSeqWs = 33 * kMtN;              // 33 twist blocks cover kMtSeq
-constexpr uint32_t kMtJumpThreads = 640;              // 10 waves; threads 0..623 own a window word
+constexpr uint32_t kMtJumpThreads = 320;              // 5 waves; thread t owns window words t and t + 320
 constexpr uint32_t kMtGenWaves = 4;                   // generators per block of k_mt_gen
 
 static_assert(kMtJ % kMtN == 0, "generator windows stay aligned to the twist blocks");
@@ -155,31 +155,73 @@ __global__ __launch_bounds__(256) void k_mt_seq(const uint32_t *__restrict__ sta
     }
 }
 
-// window of generator g = blockIdx.x + 1: thread j-1 (j = 1..624) writes
-// x_{gJ-1+j} = XOR over the set coefficient bits k of table[g-1] of x_{k+j}
+// window of generator g = blockIdx.x + 1: output word j (j = 1..624) is
+// x_{gJ-1+j} = XOR over the set coefficient bits k of table[g-1] of x_{k+j}.
+// LDS-bandwidth shaped (MI355X_MICROARCH.md §LDS: ds_read_b128 streams 256 B/clk,
+// ds_read_b32 and ds_read2_b64 half that): bits are taken four at a time and
+// lane j reads x_{k+j} .. x_{k+j+3} as ONE aligned 16-byte load from the copy
+// of the sequence shifted by j & 3 (copy c holds x_{i+c}); four copies of the
+// whole k range do not fit the LDS, so the range runs in four quarters.  A lane
+// owns outputs j and j + 320 (5 waves): the uniform per-bit masks (one s_bfe
+// each) serve two accumulators.
+constexpr uint32_t kMtJumpPart = 4992;                  // bits per quarter (4 x 4992 = 19968 >= 19937)
+// words of one copy per quarter: >= kMtJumpPart + kMtN + 4, a multiple of 4, and = 16 mod 64 so the
+// four copies sit 16 banks apart and a ds_read_b128 lane group (lanes 4a .. 4a+3 read the same
+// index of copies 0..3) touches 64 distinct banks
+constexpr uint32_t kMtJumpSpan = 5648;
+static_assert(kMtJumpSpan >= kMtJumpPart + kMtN + 4 && kMtJumpSpan % 64 == 16, "copy stride");
+
 __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws)
 {
-    __shared__ uint32_t seq[kMtSeqLds];
+    __shared__ __attribute__((aligned(16))) uint32_t cp[4][kMtJumpSpan];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < kMtSeqLds; i += kMtJumpThreads)
-        seq[i] = i < kMtSeq ? ws[kWsSeq + i] : 0u;
-    __syncthreads();
     const uint64_t g = (uint64_t)blockIdx.x + 1;
     const uint32_t *__restrict__ coef = table + (uint64_t)blockIdx.x * kMtN;
-    const uint32_t j = tid + 1;
-    uint32_t acc = 0;
-    if (tid < kMtN) {
-        for (uint32_t cw = 0; cw < kMtN; ++cw) {
-            const uint32_t c = __builtin_amdgcn_readfirstlane(coef[cw]);
-            const uint32_t *p = seq + cw * 32u + j;
+    const uint32_t ja = tid + 1, jb = tid + 1 + kMtJumpThreads;  // outputs of this lane (1-based)
+    const bool hasb = jb <= kMtN;
+    // aligned 16-byte source of lane j: copy (j & 3), element base + j - (j & 3); lanes
+    // without a second output re-read their first (no branch in the loop)
+    const uint32_t ca = ja & 3u, cb = hasb ? (jb & 3u) : ca;
+    const uint32_t oa = ja - ca, ob = hasb ? jb - cb : oa;
+    uint32_t acca = 0, accb = 0;
+    for (uint32_t h = 0; h < 4; ++h) {
+        const uint32_t k0 = h * kMtJumpPart;
+        __syncthreads();
+        for (uint32_t i = tid; i < kMtJumpSpan; i += kMtJumpThreads) {
 #pragma unroll
-            for (int b = 0; b < 32; ++b) {
-                const uint32_t m = 0u - ((c >> b) & 1u);             // uniform 0 / ~0: one s_bfe_i32
-                acc = __builtin_amdgcn_bitop3_b32(acc, p[b], m, 0x78);  // acc ^ (p & m)
+            for (uint32_t c = 0; c < 4; ++c) {
+                const uint32_t e = k0 + i + c;
+                cp[c][i] = e < kMtSeq ? ws[kWsSeq + e] : 0u;
             }
         }
-        ws[kWsWin + g * kMtN + tid] = acc;
+        __syncthreads();
+        const uint4 *pa = reinterpret_cast<const uint4 *>(&cp[ca][oa]);
+        const uint4 *pb = reinterpret_cast<const uint4 *>(&cp[cb][ob]);
+        for (uint32_t cw = 0; cw < kMtJumpPart / 32; ++cw) {
+            const uint32_t kw = (k0 >> 5) + cw;
+            const uint32_t c = kw < kMtN ? __builtin_amdgcn_readfirstlane(coef[kw]) : 0u;
+#pragma unroll
+            for (int b = 0; b < 32; b += 4) {
+                uint32_t m[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    m[e] = 0u - ((c >> (b + e)) & 1u);
+                const uint4 va = pa[cw * 8 + b / 4];
+                const uint4 vb = pb[cw * 8 + b / 4];
+                acca = __builtin_amdgcn_bitop3_b32(acca, va.x, m[0], 0x78);  // acc ^ (x & m)
+                acca = __builtin_amdgcn_bitop3_b32(acca, va.y, m[1], 0x78);
+                acca = __builtin_amdgcn_bitop3_b32(acca, va.z, m[2], 0x78);
+                acca = __builtin_amdgcn_bitop3_b32(acca, va.w, m[3], 0x78);
+                accb = __builtin_amdgcn_bitop3_b32(accb, vb.x, m[0], 0x78);
+                accb = __builtin_amdgcn_bitop3_b32(accb, vb.y, m[1], 0x78);
+                accb = __builtin_amdgcn_bitop3_b32(accb, vb.z, m[2], 0x78);
+                accb = __builtin_amdgcn_bitop3_b32(accb, vb.w, m[3], 0x78);
+            }
+        }
     }
+    ws[kWsWin + g * kMtN + (ja - 1)] = acca;
+    if (hasb)
+        ws[kWsWin + g * kMtN + (jb - 1)] = accb;
 }
 
 // one wave per generator: draws [gJ, min((g+1)J, count)) into out
