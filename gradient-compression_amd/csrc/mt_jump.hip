@@ -66,7 +66,11 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 // twist(s[k], s[k+1]) in k order): phase A k < 227 reads only old words,
 // B k < 454 reads s[k-227] from A, C k < 624 from B (and s[0] from A for
 // k = 623).  Every lane loads all its inputs of a phase before any store.
-__device__ __forceinline__ void twist_wave(uint32_t *s, uint32_t lane)
+// EMIT: the new block is consumed whole, so each new word is also tempered and
+// stored to out[k] straight from the register that computed it (no LDS read
+// back; the stores drain while the next phase's loads are in flight).
+template <bool EMIT>
+__device__ __forceinline__ void twist_wave(uint32_t *s, uint32_t lane, uint32_t *__restrict__ out = nullptr)
 {
     constexpr uint32_t H = kMtN - kMtM;  // 227
     uint32_t v[4];
@@ -79,8 +83,11 @@ __device__ __forceinline__ void twist_wave(uint32_t *s, uint32_t lane)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const uint32_t k = lane + 64u * r;
-        if (k < H)
+        if (k < H) {
             s[k] = v[r];
+            if constexpr (EMIT)
+                out[k] = mtj_temper(v[r]);
+        }
     }
     lds_order();
 #pragma unroll
@@ -92,8 +99,11 @@ __device__ __forceinline__ void twist_wave(uint32_t *s, uint32_t lane)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const uint32_t k = H + lane + 64u * r;
-        if (k < 2 * H)
+        if (k < 2 * H) {
             s[k] = v[r];
+            if constexpr (EMIT)
+                out[k] = mtj_temper(v[r]);
+        }
     }
     lds_order();
 #pragma unroll
@@ -105,8 +115,11 @@ __device__ __forceinline__ void twist_wave(uint32_t *s, uint32_t lane)
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const uint32_t k = 2 * H + lane + 64u * r;
-        if (k < kMtN)
+        if (k < kMtN) {
             s[k] = v[r];
+            if constexpr (EMIT)
+                out[k] = mtj_temper(v[r]);
+        }
     }
     lds_order();
 }
@@ -240,17 +253,29 @@ __global__ __launch_bounds__(64 * kMtGenWaves) void k_mt_gen(uint32_t *__restric
     lds_order();
     uint64_t pos = g * kMtJ;
     const uint64_t end = min(pos + kMtJ, count);
-    while (pos < end) {
-        if (ptr >= kMtN) {
-            twist_wave(s, lane);
-            ptr = 0;
-        }
+    // head: the rest of the current block
+    if (ptr < kMtN) {
         const uint32_t take = (uint32_t)min((uint64_t)(kMtN - ptr), end - pos);
         for (uint32_t i = lane; i < take; i += 64)
             out[pos + i] = mtj_temper(s[ptr + i]);
         lds_order();
         pos += take;
         ptr += take;
+    }
+    // body: whole blocks, emitted by the twist itself
+    while (end - pos >= kMtN) {
+        twist_wave<true>(s, lane, out + pos);
+        pos += kMtN;
+        ptr = kMtN;
+    }
+    // tail: a partial block
+    if (pos < end) {
+        twist_wave<false>(s, lane);
+        const uint32_t take = (uint32_t)(end - pos);
+        for (uint32_t i = lane; i < take; i += 64)
+            out[pos + i] = mtj_temper(s[i]);
+        lds_order();
+        ptr = take;
     }
     if (g == gens - 1) {  // the advanced state: this window (aligned to the twist blocks) + read index
         for (uint32_t i = lane; i < kMtN; i += 64)
