@@ -143,16 +143,22 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
         nrm = torch.empty(1, device=dev)
         holder = {}
 
+        one_pass = world == 1 and not ms.q_cache  # W = 1: mask + select in one pass (gc_ms_encode_w1)
+
         def ms_step():
             codec.absmax(x3, out=nrm)
             if world > 1:
                 dist.all_reduce(nrm, op=dist.ReduceOp.MAX)
-            m = ms.encode_mask(nrm, x3, world)
-            if world > 1:
-                dist.all_reduce(m)
-            w = ms.encode(nrm, x3, m, world)
-            if world > 1:
-                dist.all_reduce(w)
+            both = ms.encode_w1(nrm, x3) if one_pass else None
+            if both is not None:
+                m, w = both
+            else:
+                m = ms.encode_mask(nrm, x3, world)
+                if world > 1:
+                    dist.all_reduce(m)
+                w = ms.encode(nrm, x3, m, world)
+                if world > 1:
+                    dist.all_reduce(w)
             holder["d"] = ms.decode(nrm, w, m, n3, world, 1.0 / world)
 
         t = sync_ms(ms_step)
@@ -169,6 +175,8 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
         d_ = torch.empty(n3, device=dev)
         kt = {
             "absmax": (_events(torch, lambda: codec.absmax(x3, out=nrm), reps), 4 * n3),
+            **({"mask_select_one_pass": (_events(torch, lambda: ms.encode_w1(nrm, x3), reps),
+                                         4 * n3 + 4 * mwords + 4 * ql.plane_words)} if one_pass else {}),
             "mask_encode": (_events(torch, lambda: ms.encode_mask(nrm, x3, world), reps), 4 * n3 + 4 * mwords + cell),
             "select_encode": (_events(torch, lambda: ms.encode(nrm, x3, m_, world), reps),
                               (cell if cached else 4 * n3) + 4 * mwords + 4 * ql.plane_words),
@@ -177,7 +185,9 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
         }
         res[f"config3_{tag}"] = {
             "n": n3, "ms_per_step": t, "grad_floats_per_s": world * n3 / (t * 1e-3), "q_cache": cached,
-            "step": "absmax, MAX, mask encode, SUM(mask lanes), select encode, SUM(words), decode",
+            "step": ("absmax, mask+select encode in one pass (W = 1), decode" if one_pass else
+                     "absmax, MAX, mask encode, SUM(mask lanes), select encode, SUM(words), decode"),
+            "two_pass_kernels": "mask_encode / select_encode are the W > 1 passes, timed for reference",
             "kernels": {k: {"us": ms_ * 1e3, "gbs": b / (ms_ * 1e-3) / 1e9,
                             "frac_hbm_peak": b / (ms_ * 1e-3) / 1e9 / HBM_PEAK_GBS} for k, (ms_, b) in kt.items()}}
         del m_, w_, d_

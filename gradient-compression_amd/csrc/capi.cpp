@@ -73,7 +73,11 @@ int check_lanes(const gc_lanes *l, uint64_t n, const char *what)
     int rc = gc_lane_layout(l->n, l->range, l->world, l->offset, &ref);
     if (rc != GC_OK)
         return rc;
-    if (ref.bits != l->bits || ref.per_word != l->per_word || ref.plane_words != l->plane_words)
+    // plane_words may exceed the minimal layout's (the multi-scale layouts couple
+    // the mask and q plane sizes, gc_ms_layout) but keeps its alignment
+    const uint64_t align = l->plane_words >= 65536 ? 64 : 4;
+    if (ref.bits != l->bits || ref.per_word != l->per_word || l->plane_words < ref.plane_words ||
+        l->plane_words % align)
         return fail(GC_EINVAL, "%s: lane layout inconsistent with (n, range, world)", what);
     if (l->n != n)
         return fail(GC_EINVAL, "%s: lane layout is for n=%llu, call has n=%llu", what,
@@ -138,15 +142,36 @@ int gc_qsgd_layout(uint64_t n, uint32_t bits, uint32_t world, gc_lanes *out)
     return gc_lane_layout(n, 2ull * s, world, s, out);
 }
 
+// W = 1 multi-scale layouts are coupled: with r = floor(32 / Lq) (Lq = q lanes
+// per word), the q plane size Mq is a multiple of 64 r and the mask plane size
+// is Mm = Mq / r, so mask plane P = h + r k holds exactly the elements of q lane
+// k of q words h Mm .. (h+1) Mm - 1.  A kernel that owns mask-word quad t then
+// owns q-word quads t, t + Mm/4, ..., t + (r-1) Mm/4 whole: the one-pass W = 1
+// encode (gc_ms_encode_w1) writes both streams without exchanging lanes between
+// blocks.  Mask planes P >= r Lq stay empty (r Lq of the 32 used: 30 for the
+// 2-bit lower level, a mask stream 6.7% above the minimum).
+static int ms_q_lanes(uint64_t n, const gc_levels *levels, uint32_t world, gc_lanes *out, uint32_t *r)
+{
+    // |q| <= s_0 for two levels; <= s_0 + 1 for three or more (a rank whose own
+    // mask is above the common one may round level m up by one).
+    uint32_t qmax = (1u << levels->bits[0]) - 1u + (levels->count >= 3 ? 1u : 0u);
+    int rc = gc_lane_layout(n, 2ull * qmax, world, qmax, out);
+    if (rc || world != 1 || levels->count < 2)
+        return rc;
+    const uint32_t rr = 32u / out->per_word;
+    const uint64_t q = 64ull * rr;
+    out->plane_words = (((n + out->per_word - 1) / out->per_word) + q - 1) / q * q;
+    *r = rr;
+    return GC_OK;
+}
+
 int gc_ms_layout(uint64_t n, const gc_levels *levels, uint32_t world, gc_lanes *out)
 {
     int rc = gc::check_levels(levels, "gc_ms_layout");
     if (rc)
         return rc;
-    // |q| <= s_0 for two levels; <= s_0 + 1 for three or more (a rank whose own
-    // mask is above the common one may round level m up by one).
-    uint32_t qmax = (1u << levels->bits[0]) - 1u + (levels->count >= 3 ? 1u : 0u);
-    return gc_lane_layout(n, 2ull * qmax, world, qmax, out);
+    uint32_t r = 0;
+    return ms_q_lanes(n, levels, world, out, &r);
 }
 
 int gc_ms_mask_layout(uint64_t n, const gc_levels *levels, uint32_t world, gc_lanes *out)
@@ -155,7 +180,16 @@ int gc_ms_mask_layout(uint64_t n, const gc_levels *levels, uint32_t world, gc_la
     if (rc)
         return rc;
     GC_REQUIRE(levels->count >= 2, "gc_ms_mask_layout: needs >= 2 levels");
-    return gc_lane_layout(n, 1, world, 0, out);
+    if ((rc = gc_lane_layout(n, 1, world, 0, out)))
+        return rc;
+    if (world == 1) {  // coupled to the q layout (above)
+        gc_lanes ql;
+        uint32_t r = 0;
+        if ((rc = ms_q_lanes(n, levels, world, &ql, &r)))
+            return rc;
+        out->plane_words = ql.plane_words / r;
+    }
+    return GC_OK;
 }
 
 }  // extern "C"

@@ -644,6 +644,155 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
 }
 
 // ---------------------------------------------------------------------------
+// W = 1: mask + select in ONE pass (compressors.py:778-817 with the MIN
+// all-reduce of reducer.py:1680 over a single rank, the identity: the common
+// level is the rank's own).  Per 4 elements: the levels 1..NL-1 decide the
+// mask (mask_plane), the chosen level's rounding is kept, and level 0's draw
+// block is computed only when an element stays at level 0 — the same draws,
+// arithmetic and decisions as mask_plane + select_plane, so both streams are
+// bit-identical to the two-pass encode.  The coupled W = 1 layouts
+// (gc_ms_mask_layout) make mask plane P = h + r k the q lane k of q words
+// h Mm + pos: the block that owns mask quad t owns q quads t + h Mm/4 whole.
+// ---------------------------------------------------------------------------
+template <int KIND, int NL, int VAR = 0>
+__device__ __forceinline__ void fused_plane(const float *__restrict__ x, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                            uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                            const RngArgs &rng, int32_t qmax, uint4 &m, uint4 &ln)
+{
+    const float4 v = load4_nt_tail<0>(x, i0, n);
+    RangeI rg;
+    rg.add4(v);
+    m = make_uint4(0u, 0u, 0u, 0u);
+    if ((VAR & MSV_WIDE) == 0 && dv.fast && !rg.slow(lo2, hi2)) {
+        const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+        int32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;  // T at the element's level
+#pragma unroll
+        for (int l = 1; l < NL; ++l) {
+            const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
+            const gc_f2 S = {fa.S24[l], fa.S24[l]};
+            const gc_f2 a = q01 * S, b = q23 * S;
+            const int32_t u0 = ms_t(a.x, r.x), u1 = ms_t(a.y, r.y), u2 = ms_t(b.x, r.z), u3 = ms_t(b.y, r.w);
+            if (u0 >= fa.thr) { m.x = l; t0 = u0; }
+            if (u1 >= fa.thr) { m.y = l; t1 = u1; }
+            if (u2 >= fa.thr) { m.z = l; t2 = u2; }
+            if (u3 >= fa.thr) { m.w = l; t3 = u3; }
+        }
+        if (m.x == 0u || m.y == 0u || m.z == 0u || m.w == 0u) {  // level 0's draws only when needed
+            const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
+            const gc_f2 S = {fa.S24[0], fa.S24[0]};
+            const gc_f2 a = q01 * S, b = q23 * S;
+            t0 = m.x == 0u ? ms_t(a.x, r.x) : t0;
+            t1 = m.y == 0u ? ms_t(a.y, r.y) : t1;
+            t2 = m.z == 0u ? ms_t(b.x, r.z) : t2;
+            t3 = m.w == 0u ? ms_t(b.y, r.w) : t3;
+        }
+        ln = make_uint4(lane_of_t(v.x, t0, qmax), lane_of_t(v.y, t1, qmax), lane_of_t(v.z, t2, qmax),
+                        lane_of_t(v.w, t3, qmax));
+    } else {
+        const float4 ql = quot4_exact(v, dv);
+        int32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+#pragma unroll
+        for (int l = 1; l < NL; ++l) {
+            const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
+            const float s = lv.s[l];
+            const int32_t x0 = xi_from_q(ql.x, s, r.x), x1 = xi_from_q(ql.y, s, r.y);
+            const int32_t x2 = xi_from_q(ql.z, s, r.z), x3 = xi_from_q(ql.w, s, r.w);
+            if (x0 <= lv.maxv) { m.x = l; q0 = sgn_of(v.x) * x0; }
+            if (x1 <= lv.maxv) { m.y = l; q1 = sgn_of(v.y) * x1; }
+            if (x2 <= lv.maxv) { m.z = l; q2 = sgn_of(v.z) * x2; }
+            if (x3 <= lv.maxv) { m.w = l; q3 = sgn_of(v.w) * x3; }
+        }
+        if (m.x == 0u || m.y == 0u || m.z == 0u || m.w == 0u) {
+            const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
+            const float s = lv.s[0];
+            q0 = m.x == 0u ? sgn_of(v.x) * xi_from_q(ql.x, s, r.x) : q0;
+            q1 = m.y == 0u ? sgn_of(v.y) * xi_from_q(ql.y, s, r.y) : q1;
+            q2 = m.z == 0u ? sgn_of(v.z) * xi_from_q(ql.z, s, r.z) : q2;
+            q3 = m.w == 0u ? sgn_of(v.w) * xi_from_q(ql.w, s, r.w) : q3;
+        }
+        ln = make_uint4(lane_of_q(q0, qmax), lane_of_q(q1, qmax), lane_of_q(q2, qmax), lane_of_q(q3, qmax));
+    }
+    if (i0 + 4 > n) {  // elements past n: level 0, lane 0
+        m.y = i0 + 1 < n ? m.y : 0u;
+        m.z = i0 + 2 < n ? m.z : 0u;
+        m.w = i0 + 3 < n ? m.w : 0u;
+        ln.y = i0 + 1 < n ? ln.y : 0u;
+        ln.z = i0 + 2 < n ? ln.z : 0u;
+        ln.w = i0 + 3 < n ? ln.w : 0u;
+    }
+}
+
+constexpr uint32_t kMsFusedMaxR = 8;  // q words per mask word at W = 1: 32 / (q lanes per word) <= 8
+
+// planes: r * Lq mask planes in use; kdiv = ceil(2^16 / r) (P / r = (P * kdiv) >> 16 for P < 32)
+template <int KIND, int NL, int VAR = 0>
+__global__ __launch_bounds__(kBlock) void k_ms_fused_w1(const float *__restrict__ x, uint32_t n,
+                                                        const float *__restrict__ normp, LevelsArg lv, MsFastArg fa,
+                                                        RngArgs rng, uint32_t Mm, uint32_t r, uint32_t kdiv,
+                                                        uint32_t planes, uint32_t wq, int32_t qmax,
+                                                        uint32_t *__restrict__ mask_words, uint32_t *__restrict__ words)
+{
+    const float norm = *normp;
+    const DivNorm dv = make_div(norm);
+    const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
+    const uint32_t quads = Mm >> 2;
+    __shared__ uint4 part[3][kMsQuadsPerBlock];
+    // the tile's q words, [h][element e of the quad][quad]: every wave ORs its
+    // planes' lanes in (disjoint bit fields); bank = quad, conflict-free
+    __shared__ uint32_t qs[kMsFusedMaxR][4][kMsQuadsPerBlock];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    uint32_t *qflat = &qs[0][0][0];
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
+        for (uint32_t i = threadIdx.x; i < r * 4u * kMsQuadsPerBlock; i += kBlock)
+            qflat[i] = 0u;
+        __syncthreads();
+        const uint32_t t = tb + lane;
+        uint4 acc[NL - 1] = {};
+        if (t < quads) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t P = wave + 4u * j;
+                if (P >= planes)
+                    break;
+                const uint32_t i0 = P * Mm + 4u * t;
+                if (i0 >= n)
+                    break;
+                uint4 m, ln;
+                fused_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng, qmax, m, ln);
+                mask_bits<NL>(acc, m, P);
+                const uint32_t k = (P * kdiv) >> 16, h = P - k * r;
+                const uint32_t sh = k * wq;
+                atomicOr(&qs[h][0][lane], ln.x << sh);
+                atomicOr(&qs[h][1][lane], ln.y << sh);
+                atomicOr(&qs[h][2][lane], ln.z << sh);
+                atomicOr(&qs[h][3][lane], ln.w << sh);
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < NL - 1; ++f) {
+            if (wave)
+                part[wave - 1][lane] = acc[f];
+            __syncthreads();
+            if (wave == 0 && t < quads) {
+                const uint4 a = part[0][lane], b = part[1][lane], c = part[2][lane];
+                st_nt4u(mask_words + (uint64_t)f * Mm + 4u * t,
+                        make_uint4(acc[f].x | a.x | b.x | c.x, acc[f].y | a.y | b.y | c.y,
+                                   acc[f].z | a.z | b.z | c.z, acc[f].w | a.w | b.w | c.w));
+            }
+            __syncthreads();
+        }
+        // q words: quad tq of the tile in q stream h sits at q position h Mm + 4 (tb + tq)
+        for (uint32_t i = threadIdx.x; i < r * kMsQuadsPerBlock; i += kBlock) {
+            const uint32_t h = i / kMsQuadsPerBlock, tq = i % kMsQuadsPerBlock;
+            if (tb + tq < quads)
+                st_nt4u(words + (uint64_t)h * Mm + 4u * (tb + tq),
+                        make_uint4(qs[h][0][tq], qs[h][1][tq], qs[h][2][tq], qs[h][3][tq]));
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // decode (compressors.py:819-826 order 0; 668-680 order 1) + alpha
 // ---------------------------------------------------------------------------
 template <int LQ, int ORDER, int NL, int VAR = 0>

@@ -14,8 +14,8 @@
 //               (32 twists of the state) into the workspace; window 0 = the
 //               state itself, plus the read index
 //   k_mt_jump   one workgroup per generator g >= 1: the stream x_0..x_20560 in
-//               LDS (four shifted copies, in four quarters), 320 threads, each
-//               accumulating two window words over the 19937 coefficient bits
+//               LDS (four shifted copies, in four quarters), 640 threads, each
+//               accumulating one window word over the 19937 coefficient bits
 //               (uniform per block: scalar loads of the jump table; per bit a
 //               uniform 0 / ~0 mask and one xor-and per word)
 //   k_mt_gen    one wave per generator: its window in LDS, wave-synchronous
@@ -33,7 +33,7 @@ constexpr uint32_t kMtM = 397;
 constexpr uint32_t kMtJ = GC_MT_JUMP_DRAWS;
 constexpr uint32_t kMtSeq = 19937 + kMtN;              // x_0 .. x_20560 (k + j <= 19936 + 624)
 constexpr uint32_t kMtSeqWs = 33 * kMtN;              // 33 twist blocks cover kMtSeq
-constexpr uint32_t kMtJumpThreads = 320;              // 5 waves; thread t owns window words t and t + 320
+constexpr uint32_t kMtJumpThreads = 640;              // 10 waves; thread t owns window word t
 constexpr uint32_t kMtGenWaves = 4;                   // generators per block of k_mt_gen
 
 static_assert(kMtJ % kMtN == 0, "generator windows stay aligned to the twist blocks");
@@ -174,29 +174,26 @@ __global__ __launch_bounds__(256) void k_mt_seq(const uint32_t *__restrict__ sta
 // ds_read_b32 and ds_read2_b64 half that): bits are taken four at a time and
 // lane j reads x_{k+j} .. x_{k+j+3} as ONE aligned 16-byte load from the copy
 // of the sequence shifted by j & 3 (copy c holds x_{i+c}); four copies of the
-// whole k range do not fit the LDS, so the range runs in four quarters.  A lane
-// owns outputs j and j + 320 (5 waves): the uniform per-bit masks (one s_bfe
-// each) serve two accumulators.
-constexpr uint32_t kMtJumpPart = 4992;                  // bits per quarter (4 x 4992 = 19968 >= 19937)
-// words of one copy per quarter: >= kMtJumpPart + kMtN + 4, a multiple of 4, and = 16 mod 64 so the
-// four copies sit 16 banks apart and a ds_read_b128 lane group (lanes 4a .. 4a+3 read the same
-// index of copies 0..3) touches 64 distinct banks
+// whole k range do not fit the LDS, so the range runs in four quarters.  Ten
+// waves (one output word per lane), four independent xor chains per lane (bit
+// k mod 4) and the coefficient words fetched four at a time (one scalar load)
+// keep the LDS reads and the dependent xors overlapped.
+constexpr uint32_t kMtJumpPart = 4992;  // bits per quarter (4 x 4992 = 19968 >= 19937; 156 words, 39 x 4)
+// words of one copy per quarter: >= kMtJumpPart + kMtN + 20 (idle lanes up to j = 640 read in bounds),
+// a multiple of 4, and = 16 mod 64 so the four copies sit 16 banks apart and a ds_read_b128 lane
+// group (lanes 4a .. 4a+3 read the same index of copies 0..3) touches 64 distinct banks
 constexpr uint32_t kMtJumpSpan = 5648;
-static_assert(kMtJumpSpan >= kMtJumpPart + kMtN + 4 && kMtJumpSpan % 64 == 16, "copy stride");
+static_assert(kMtJumpSpan >= kMtJumpPart + kMtJumpThreads + 4 && kMtJumpSpan % 64 == 16, "copy stride");
 
 __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws)
 {
     __shared__ __attribute__((aligned(16))) uint32_t cp[4][kMtJumpSpan];
     const uint32_t tid = threadIdx.x;
     const uint64_t g = (uint64_t)blockIdx.x + 1;
-    const uint32_t *__restrict__ coef = table + (uint64_t)blockIdx.x * kMtN;
-    const uint32_t ja = tid + 1, jb = tid + 1 + kMtJumpThreads;  // outputs of this lane (1-based)
-    const bool hasb = jb <= kMtN;
-    // aligned 16-byte source of lane j: copy (j & 3), element base + j - (j & 3); lanes
-    // without a second output re-read their first (no branch in the loop)
-    const uint32_t ca = ja & 3u, cb = hasb ? (jb & 3u) : ca;
-    const uint32_t oa = ja - ca, ob = hasb ? jb - cb : oa;
-    uint32_t acca = 0, accb = 0;
+    const uint4 *__restrict__ coef4 = reinterpret_cast<const uint4 *>(table + (uint64_t)blockIdx.x * kMtN);
+    const uint32_t j = tid + 1;  // output word of this lane (1-based; lanes past 624 idle)
+    const uint32_t cj = j & 3u, oj = j - cj;  // aligned 16-byte source: copy (j & 3), element base + j - (j & 3)
+    uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
     for (uint32_t h = 0; h < 4; ++h) {
         const uint32_t k0 = h * kMtJumpPart;
         __syncthreads();
@@ -208,33 +205,26 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
             }
         }
         __syncthreads();
-        const uint4 *pa = reinterpret_cast<const uint4 *>(&cp[ca][oa]);
-        const uint4 *pb = reinterpret_cast<const uint4 *>(&cp[cb][ob]);
-        for (uint32_t cw = 0; cw < kMtJumpPart / 32; ++cw) {
-            const uint32_t kw = (k0 >> 5) + cw;
-            const uint32_t c = kw < kMtN ? __builtin_amdgcn_readfirstlane(coef[kw]) : 0u;
+        const uint4 *p = reinterpret_cast<const uint4 *>(&cp[cj][oj]);
+        for (uint32_t bi = 0; bi < kMtJumpPart / 128; ++bi) {
+            const uint4 c4 = coef4[(k0 >> 7) + bi];  // uniform: one scalar load of 4 coefficient words
+            const uint32_t cs[4] = {c4.x, c4.y, c4.z, c4.w};
 #pragma unroll
-            for (int b = 0; b < 32; b += 4) {
-                uint32_t m[4];
+            for (int cc = 0; cc < 4; ++cc) {
+                const uint32_t c = cs[cc];
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    m[e] = 0u - ((c >> (b + e)) & 1u);
-                const uint4 va = pa[cw * 8 + b / 4];
-                const uint4 vb = pb[cw * 8 + b / 4];
-                acca = __builtin_amdgcn_bitop3_b32(acca, va.x, m[0], 0x78);  // acc ^ (x & m)
-                acca = __builtin_amdgcn_bitop3_b32(acca, va.y, m[1], 0x78);
-                acca = __builtin_amdgcn_bitop3_b32(acca, va.z, m[2], 0x78);
-                acca = __builtin_amdgcn_bitop3_b32(acca, va.w, m[3], 0x78);
-                accb = __builtin_amdgcn_bitop3_b32(accb, vb.x, m[0], 0x78);
-                accb = __builtin_amdgcn_bitop3_b32(accb, vb.y, m[1], 0x78);
-                accb = __builtin_amdgcn_bitop3_b32(accb, vb.z, m[2], 0x78);
-                accb = __builtin_amdgcn_bitop3_b32(accb, vb.w, m[3], 0x78);
+                for (int b = 0; b < 32; b += 4) {
+                    const uint4 v = p[(bi * 4 + cc) * 8 + b / 4];
+                    acc0 = __builtin_amdgcn_bitop3_b32(acc0, v.x, 0u - ((c >> b) & 1u), 0x78);  // acc ^ (x & m)
+                    acc1 = __builtin_amdgcn_bitop3_b32(acc1, v.y, 0u - ((c >> (b + 1)) & 1u), 0x78);
+                    acc2 = __builtin_amdgcn_bitop3_b32(acc2, v.z, 0u - ((c >> (b + 2)) & 1u), 0x78);
+                    acc3 = __builtin_amdgcn_bitop3_b32(acc3, v.w, 0u - ((c >> (b + 3)) & 1u), 0x78);
+                }
             }
         }
     }
-    ws[kWsWin + g * kMtN + (ja - 1)] = acca;
-    if (hasb)
-        ws[kWsWin + g * kMtN + (jb - 1)] = accb;
+    if (j <= kMtN)
+        ws[kWsWin + g * kMtN + (j - 1)] = acc0 ^ acc1 ^ acc2 ^ acc3;
 }
 
 // one wave per generator: draws [gJ, min((g+1)J, count)) into out

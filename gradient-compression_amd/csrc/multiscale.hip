@@ -373,6 +373,50 @@ using namespace gc;
 
 extern "C" {
 
+int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_levels *levels, const gc_rng *rng,
+                    const gc_lanes *mask_lanes, const gc_lanes *q_lanes, uint32_t *mask_words, uint32_t *words,
+                    gc_stream_t stream)
+{
+    int rc;
+    if ((rc = check_levels(levels, "gc_ms_encode_w1")) || (rc = check_rng_ms(rng, "gc_ms_encode_w1")) ||
+        (rc = check_mask_lanes(mask_lanes, levels, n, "gc_ms_encode_w1")) ||
+        (rc = check_q_lanes(q_lanes, levels, n, "gc_ms_encode_w1")))
+        return rc;
+    GC_REQUIRE(mask_lanes->world == 1 && q_lanes->world == 1, "gc_ms_encode_w1: lanes for W = 1 only");
+    GC_REQUIRE(norm && mask_words && words && (n == 0 || x), "gc_ms_encode_w1: null pointer");
+    GC_REQUIRE(aligned16(mask_words) && aligned16(words), "gc_ms_encode_w1: streams must be 16-byte aligned");
+    const uint32_t r = 32u / q_lanes->per_word;
+    GC_REQUIRE(mask_lanes->per_word == 32 && r <= kMsFusedMaxR && q_lanes->plane_words == (uint64_t)r * mask_lanes->plane_words,
+               "gc_ms_encode_w1: layouts not coupled (gc_ms_layout / gc_ms_mask_layout at W = 1)");
+    const int mode = aligned16(x) ? 0 : 1;
+    GC_REQUIRE(ms_fast_wide_ok(mode, n, levels),
+               "gc_ms_encode_w1: needs a dense 16-byte aligned x, n < 2^32 and 2 or 3 levels of <= 24 bits");
+    if (mask_lanes->plane_words == 0)
+        return GC_OK;
+    hipStream_t st = as_stream(stream);
+    const LevelsArg la = levels_arg(levels);
+    const RngArgs ra = rng_args_ms(rng, n);
+    const MsFastArg fa = ms_fast_arg(levels);
+    const uint32_t Mm = (uint32_t)mask_lanes->plane_words;
+    const uint32_t planes = std::min(32u, r * q_lanes->per_word);
+    const uint32_t kdiv = (65536u + r - 1) / r;
+    const unsigned g = ms_grid(Mm >> 2);
+    const bool wide = !ms_fast_ok(mode, n, levels);
+    const int32_t qmax = (int32_t)q_lanes->offset;
+#define GC_FW(KIND_, NL_, VAR_)                                                                                   \
+    hipLaunchKernelGGL((k_ms_fused_w1<KIND_, NL_, VAR_>), dim3(g), dim3(kBlock), 0, st, x, (uint32_t)n, norm, la, \
+                       fa, ra, Mm, r, kdiv, planes, q_lanes->bits, qmax, mask_words, words)
+    if (levels->count == 2) {
+        if (rng->kind == GC_RNG_PHILOX) { if (wide) GC_FW(0, 2, MSV_WIDE); else GC_FW(0, 2, 0); }
+        else { if (wide) GC_FW(1, 2, MSV_WIDE); else GC_FW(1, 2, 0); }
+    } else {
+        if (rng->kind == GC_RNG_PHILOX) { if (wide) GC_FW(0, 3, MSV_WIDE); else GC_FW(0, 3, 0); }
+        else { if (wide) GC_FW(1, 3, MSV_WIDE); else GC_FW(1, 3, 0); }
+    }
+#undef GC_FW
+    return launch_status("gc_ms_encode_w1");
+}
+
 int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, const gc_levels *levels,
                       const gc_rng *rng, const gc_lanes *mask_lanes, uint32_t *mask_words, gc_stream_t stream)
 {

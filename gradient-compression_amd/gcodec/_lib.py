@@ -109,6 +109,7 @@ SIGNATURES = {
     "gc_qsgd_decode_segments": (C.c_int, [P, u64, P, u32, LANESP, f32, SEGSP, P]),
     "gc_ms_mask_encode": (C.c_int, [P, P, u64, P, LEVP, RNGP, LANESP, P, P]),
     "gc_ms_select_encode": (C.c_int, [P, P, u64, P, LEVP, RNGP, P, LANESP, LANESP, P, P]),
+    "gc_ms_encode_w1": (C.c_int, [P, u64, P, LEVP, RNGP, LANESP, LANESP, P, P, P]),
     "gc_ms_cache_bytes": (C.c_int, [u64, LEVP, P]),
     "gc_ms_mask_encode_cached": (C.c_int, [P, u64, P, LEVP, RNGP, LANESP, P, P, P]),
     "gc_ms_select_cached": (C.c_int, [P, u64, LEVP, P, LANESP, LANESP, P, P]),

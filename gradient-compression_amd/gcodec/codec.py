@@ -504,6 +504,34 @@ def ms_mask_encode(x, norm, levels, rng, world=1, idx=None, out=None, cache=None
     return out
 
 
+def ms_w1_ok(x, levels) -> bool:
+    """Whether gc_ms_encode_w1 (the one-pass W = 1 multi-scale encode) takes
+    this bucket: dense 16-byte aligned fp32 x, n < 2^32, 2 or 3 levels of <= 24 bits."""
+    lv = sorted(int(b) for b in levels)
+    return (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.data_ptr() % 16 == 0
+            and x.numel() < 2 ** 32 and len(lv) in (2, 3) and lv[-1] <= 24)
+
+
+def ms_encode_w1(x, norm, levels, rng, mask_out=None, out=None):
+    """(mask_words, words) of the W = 1 multi-scale encode in ONE pass over x:
+    the same streams as ms_mask_encode + ms_select_encode (the MIN over one rank
+    is the identity).  See ms_w1_ok for the buckets it takes."""
+    dev = _dev(x)
+    x = _f32(x, "ms_encode_w1")
+    n = x.numel()
+    ql, ml = ms_layouts(n, levels, 1)
+    lv = levels_struct(levels)
+    nt = norm_tensor(norm, dev)
+    if mask_out is None:
+        mask_out = torch.empty(mask_words_total(ml, levels), dtype=torch.int32, device=dev)
+    if out is None:
+        out = torch.empty(ql.plane_words, dtype=torch.int32, device=dev)
+    r = rng.struct()
+    check(_lib.load().gc_ms_encode_w1(_p(x), n, _p(nt), C.byref(lv), C.byref(r), C.byref(ml), C.byref(ql),
+                                      _p(mask_out), _p(out), _stream(dev)), "gc_ms_encode_w1")
+    return mask_out, out
+
+
 def ms_select_encode(x, norm, levels, rng, mask_words, world=1, idx=None, out=None, cache=None):
     """Packed q at the common levels of the W-summed mask; with `cache` (written
     by ms_mask_encode for this x, norm and rng) from the cache cells."""

@@ -173,6 +173,19 @@ class _MultiScalePacked(_Base):
         self._cache_key = (tensor.data_ptr(), n)
         return self.backend.ms_mask_encode(tensor, norm, levels, self._rng, world, cache=cache)
 
+    def encode_w1(self, norm, tensor):
+        """W = 1: (mask_words, words) in one pass over x (the MIN all-reduce of
+        the mask over one rank is the identity), the same streams as
+        encode_mask + encode; None when the backend has no one-pass form for
+        this bucket (the caller then runs the two passes)."""
+        levels = self._packed_levels()
+        ok = getattr(self.backend, "ms_w1_ok", None)
+        if ok is None or not ok(tensor, levels):
+            return None
+        self._rng = self._reserve(tensor.numel(), len(levels), tensor.device)
+        self._cache_key = None
+        return self.backend.ms_encode_w1(tensor, norm, levels, self._rng)
+
     def encode(self, norm, tensor, mask_words, world=1, idx=None):
         levels = self._packed_levels()
         n = idx.numel() if idx is not None else tensor.numel()

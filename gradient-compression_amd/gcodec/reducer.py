@@ -300,9 +300,13 @@ class QSGDMaxNormTwoScaleReducer(Reducer):
         else:
             norm = self._max_norm(flat, local, idx)
         with self._timer("reduce.compress", verbosity=2):
-            mask = comp.encode_mask(norm, x, world=W, idx=idx)
-            self._all_reduce(mask)
-            words = comp.encode(norm, x, mask, world=W, idx=idx)
+            both = comp.encode_w1(norm, x) if W == 1 and idx is None else None
+            if both is not None:  # one pass: the mask MIN over one rank is the identity
+                mask, words = both
+            else:
+                mask = comp.encode_mask(norm, x, world=W, idx=idx)
+                self._all_reduce(mask)
+                words = comp.encode(norm, x, mask, world=W, idx=idx)
         with self._timer("reduce.reduce.vector", verbosity=2):
             self._all_reduce(words)
         bits = self.n_bits(norm) + self.n_bits(mask) + self.n_bits(words)

@@ -28,6 +28,7 @@
  *   gc_ms_mask_encode ........ compressors.py:778-807 compress_cache + compress_mask
  *                              (= TwoScale compress_lower/compress_higher 630-666 for 2 levels)
  *   gc_ms_select_encode ...... compressors.py:809-817 compress(mask) (+ reducer.py:1503-1505 blend)
+ *   gc_ms_encode_w1 .......... both at W = 1 (reducer.py:1680 MIN over one rank = identity), one pass
  *   gc_ms_*_cached ........... the same pair with compressors.py:778-797's cache kept (packed cells)
  *   gc_ms_decode ............. compressors.py:819-826 (order 0) / 668-680 (order 1)
  *   gc_mt19937_seed/_generate  seed.py:6-11 torch.manual_seed + torch CPU generator stream
@@ -119,7 +120,12 @@ int gc_qsgd_layout(uint64_t n, uint32_t bits, uint32_t world, gc_lanes *out);
 /* multi-scale q lanes: qmax = s_0 (2 levels) or s_0+1 (>=3 levels) */
 int gc_ms_layout(uint64_t n, const gc_levels *levels, uint32_t world, gc_lanes *out);
 /* multi-scale mask lanes: (count-1) thermometer fields of range 1, each its own
- * stream of plane_words; total words = (count-1)*plane_words */
+ * stream of plane_words; total words = (count-1)*plane_words.
+ * At world = 1 the two layouts are coupled: r = floor(32 / q per_word), the q
+ * plane_words is a multiple of 64 r and the mask plane_words = q plane_words / r
+ * (mask plane h + r k = q lane k of q words [h M_mask, (h+1) M_mask)), which
+ * gc_ms_encode_w1 needs.  Every entry point accepts any plane_words at or
+ * above the minimal layout's with its alignment. */
 int gc_ms_mask_layout(uint64_t n, const gc_levels *levels, uint32_t world, gc_lanes *out);
 
 /* ---- max-norm ----------------------------------------------------------- */
@@ -243,6 +249,13 @@ int gc_qsgd_decode_segments(const uint32_t *words, uint64_t n, const float *norm
 /* ---- multi-scale / two-scale --------------------------------------------- */
 int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm, const gc_levels *levels,
                       const gc_rng *rng, const gc_lanes *mask_lanes, uint32_t *mask_words, gc_stream_t stream);
+/* W = 1 (the MIN over one rank is the identity): gc_ms_mask_encode + gc_ms_select_encode in ONE
+ * pass over x, both streams bit-identical to the two-pass encode.  Needs the coupled W = 1 layouts
+ * (gc_ms_layout / gc_ms_mask_layout with world = 1), a dense 16-byte aligned x, n < 2^32 and 2 or 3
+ * levels of <= 24 bits (GC_EINVAL otherwise: run the two passes). */
+int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_levels *levels, const gc_rng *rng,
+                    const gc_lanes *mask_lanes, const gc_lanes *q_lanes, uint32_t *mask_words, uint32_t *words,
+                    gc_stream_t stream);
 /* mask_words: the (W-summed) thermometer stream; selected level m = #fields with sum == W */
 int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const float *norm,
                         const gc_levels *levels, const gc_rng *rng, const uint32_t *mask_words,

@@ -113,6 +113,15 @@ def ms_select_encode(x, norm, levels, rng, mask_words, world=1, idx=None, out=No
     return torch.from_numpy(O.lane_pack(q, qmax, w, L, M).view(np.int32).copy())
 
 
+def ms_w1_ok(x, levels):
+    return len(levels) in (2, 3) and x.dim() == 1
+
+
+def ms_encode_w1(x, norm, levels, rng, mask_out=None, out=None):
+    m = ms_mask_encode(x, norm, levels, rng, 1)
+    return m, ms_select_encode(x, norm, levels, rng, m, 1)
+
+
 def ms_decode(words, mask_words, n, norm, levels, world=1, order=0, alpha=1.0, idx=None, out=None):
     m = _mask_from_sum(mask_words, n, levels, world)
     qmax = _qmax_ms(levels)

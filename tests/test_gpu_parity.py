@@ -902,3 +902,63 @@ def test_qsgdbp_compressor_matches_reference_vectors():
             assert bits_eq(u32(d), z[f"{c}/dec"].view(np.uint32)), c
     finally:
         gcodec.set_rng_mode("philox")
+
+
+# --------------------------------------------------------------------------- one-pass W = 1 multi-scale
+@pytest.mark.parametrize("levels", [(2, 4), (1, 3), (3, 7), (2, 4, 6), (1, 2, 3), (4, 7), (4, 8), (2, 8), (6, 10),
+                                    (3, 10, 16)])
+@pytest.mark.parametrize("n", [5, 4099, 7 * 4 * 4096 + 9, 300_001])
+def test_ms_encode_w1_matches_two_pass_and_oracle(levels, n):
+    """gc_ms_encode_w1 (mask + select in one pass, coupled W = 1 layouts) ==
+    gc_ms_mask_encode + gc_ms_select_encode bit for bit, == the oracle, on
+    level-boundary values, +-norm, zeros and subnormal tiles, with norms inside
+    and outside the Markstein range (the generic per-element branch)."""
+    L = len(levels)
+    for norm0 in (np.float32(0.05), np.float32(2.0**-110)):
+        s = (1 << levels[-1]) - 1
+        x = _int_path_input(n, norm0, s, seed=n % 1000 + 7 * L)
+        if n > 3:
+            s0 = (1 << levels[0]) - 1
+            k = np.random.default_rng(L).integers(-s0, s0 + 1, n // 3).astype(np.float32)
+            x[: n // 3] = np.clip((k * np.float32(norm0)) / np.float32(s0), -norm0, norm0)
+        norm = O.absmax(x)
+        r = gcodec.rng.Reservation(0, 17 + L, 9, None, n, L)
+        xd = dev(x)
+        assert codec.ms_w1_ok(xd, levels)
+        mw, words = codec.ms_encode_w1(xd, float(norm), levels, r)
+        mw2 = codec.ms_mask_encode(xd, float(norm), levels, r, 1)
+        assert torch.equal(mw, mw2), (levels, n, float(norm))
+        assert torch.equal(words, codec.ms_select_encode(xd, float(norm), levels, r, mw2, 1))
+        m_ref = O.ms_mask(x, norm, levels, O.philox_rng(17 + L, 9))
+        assert bits_eq(codec.ms_mask_unpack(mw, n, levels, 1).cpu().numpy().astype(np.uint8), m_ref)
+        q_ref = O.ms_select(x, norm, levels, O.philox_rng(17 + L, 9), m_ref)
+        ql, ml = codec.ms_layouts(n, levels, 1)
+        assert ql.plane_words == (32 // ql.per_word) * ml.plane_words  # the coupled layouts
+        assert bits_eq(u32(words), O.lane_pack(q_ref, ql.offset, ql.bits, ql.per_word, ql.plane_words))
+
+
+@pytest.mark.parametrize("name", ["ms_2_4_1e6", "ms_4_8_1e6"])
+def test_ms_encode_w1_torch_mode_digests(name):
+    """the one-pass W = 1 encode with torch-mode draws (caller stream, KIND 1)
+    reproduces the reference's 1e6-element multi-scale digests"""
+    import hashlib
+
+    meta = json.load(open(os.path.join(GOLD, "golden.json")))["digests"][name]
+    lv = meta["levels"]
+    x = O.gen_input(meta["n"], seed=42, kind=meta["kind"])
+    xd = dev(x)
+    gcodec.set_rng_mode("torch")
+    try:
+        torch.manual_seed(42)
+        norm = codec.absmax(xd)
+        c = gcodec.QSGDMaxNormMultiScaleCompressor(DEV, list(lv))
+        mw, words = c.encode_w1(norm, xd)
+        m = codec.ms_mask_unpack(mw, x.size, lv).cpu().numpy()
+        assert hashlib.sha256(m.tobytes()).hexdigest() == meta["mask"]
+        ql, _ = codec.ms_layouts(x.size, lv, 1)
+        q = codec.lane_unpack(words, ql).cpu().numpy().astype(np.int8 if lv[0] < 8 else np.int32)
+        assert hashlib.sha256(q.tobytes()).hexdigest() == meta["q"]
+        d = c.decode(norm, words, mw, x.size)
+        assert hashlib.sha256(d.cpu().numpy().tobytes()).hexdigest() == meta["dec"]
+    finally:
+        gcodec.set_rng_mode("philox")
