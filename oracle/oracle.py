@@ -60,6 +60,8 @@ def lib():
             "or_mt_fill": (None, [P, P, u64]),
             "or_philox_draw": (u32, [u64, u64, u32, u64]),
             "or_absmax": (f32, [P, u64]),
+            "or_absmax_par": (f32, [P, u64, u32]),
+            "or_qsgd_encode_par": (None, [P, u64, f32, u32, u32, P, P, u32]),
             "or_qsgd_quantize": (None, [P, u64, f32, u32, P, u32, P]),
             "or_qsgd_dequantize": (None, [P, u64, f32, u32, f32, P]),
             "or_lane_layout": (C.c_int, [u64, u64, u32, P, P, P]),
@@ -173,6 +175,21 @@ def qsgd_encode(x, norm, bits, world, rng) -> np.ndarray:
     _, _, M = lane_layout(x.size, 2 * s, world)
     out = np.empty(max(M, 1), dtype=np.uint32)
     lib().or_qsgd_encode(_p(x), x.size, float(norm), bits, world, C.byref(rng[0]), _p(out))
+    return out[:M]
+
+
+def absmax_par(x: np.ndarray, threads: int) -> np.float32:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    return np.float32(lib().or_absmax_par(_p(x), x.size, threads))
+
+
+def qsgd_encode_par(x, norm, bits, world, rng, threads: int) -> np.ndarray:
+    """qsgd_encode split over word ranges on `threads` host threads (CPU baseline)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    s = (1 << bits) - 1
+    _, _, M = lane_layout(x.size, 2 * s, world)
+    out = np.empty(max(M, 1), dtype=np.uint32)
+    lib().or_qsgd_encode_par(_p(x), x.size, float(norm), bits, world, C.byref(rng[0]), _p(out), threads)
     return out[:M]
 
 
