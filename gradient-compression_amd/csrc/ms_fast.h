@@ -749,7 +749,9 @@ __global__ __launch_bounds__(kBlock) void k_ms_fused_w1(const float *__restrict_
         const uint32_t t = tb + lane;
         uint4 acc[NL - 1] = {};
         if (t < quads) {
-#pragma unroll
+            // not unrolled: one copy of the per-plane body (with both rounding
+            // paths inlined) keeps the kernel's code and scalar registers small
+#pragma unroll 1
             for (int j = 0; j < 8; ++j) {
                 const uint32_t P = wave + 4u * j;
                 if (P >= planes)

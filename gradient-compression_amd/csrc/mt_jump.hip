@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void k_mt_seq(const uint32_t *__restrict__ sta
 // LDS-bandwidth shaped (MI355X_MICROARCH.md §LDS: ds_read_b128 streams 256 B/clk,
 // ds_read_b32 and ds_read2_b64 half that): bits are taken four at a time and
 // lane j reads x_{k+j} .. x_{k+j+3} as ONE aligned 16-byte load from the copy
-// of the sequence shifted by j & 3 (copy c holds x_{i+c}); four copies of the
+// of the sequence shifted by (j - 1) & 3 (copy c holds x_{i+c+1}); four copies of the
 // whole k range do not fit the LDS, so the range runs in four quarters.  Ten
 // waves (one output word per lane), four independent xor chains per lane (bit
 // k mod 4) and the coefficient words fetched four at a time (one scalar load)
@@ -192,7 +192,10 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
     const uint64_t g = (uint64_t)blockIdx.x + 1;
     const uint4 *__restrict__ coef4 = reinterpret_cast<const uint4 *>(table + (uint64_t)blockIdx.x * kMtN);
     const uint32_t j = tid + 1;  // output word of this lane (1-based; lanes past 624 idle)
-    const uint32_t cj = j & 3u, oj = j - cj;  // aligned 16-byte source: copy (j & 3), element base + j - (j & 3)
+    // x_{k+j} = x_{k + tid + 1} = copy c[k + tid - c] with c = tid & 3 (copy c holds x_{i+c+1}): an
+    // aligned 16-byte source, and lanes 4a .. 4a+3 (one ds_read_b128 lane group quarter) read the same
+    // index of copies 0..3, 16 banks apart
+    const uint32_t cj = tid & 3u, oj = tid - cj;
     uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
     for (uint32_t h = 0; h < 4; ++h) {
         const uint32_t k0 = h * kMtJumpPart;
@@ -200,7 +203,7 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
         for (uint32_t i = tid; i < kMtJumpSpan; i += kMtJumpThreads) {
 #pragma unroll
             for (uint32_t c = 0; c < 4; ++c) {
-                const uint32_t e = k0 + i + c;
+                const uint32_t e = k0 + i + c + 1;
                 cp[c][i] = e < kMtSeq ? ws[kWsSeq + e] : 0u;
             }
         }

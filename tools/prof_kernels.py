@@ -1,0 +1,54 @@
+"""Workload for rocprofv3 counter passes over the round-2 kernels: the config-3
+multi-scale kernels on the ResNet50 bucket (one-pass W = 1 encode, the two W > 1
+passes, decode), the parallel MT19937 (1e8 draws), the small-K GlobalRandK step,
+and the headline absmax + encode (1e8, 4-bit).  Each runs `REPS` times."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gradient-compression_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import gcodec  # noqa: E402
+from gcodec import codec  # noqa: E402
+
+REPS = int(os.environ.get("REPS", "5"))
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(11)
+n3 = 23_520_842
+x3 = torch.randn(n3, device=dev, generator=g).mul_(0.01)
+gen = gcodec.Generator(5, "philox")
+ms = gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen)
+nrm = codec.absmax(x3)
+for _ in range(REPS):
+    m, w = ms.encode_w1(nrm, x3)
+    m2 = ms.encode_mask(nrm, x3, 1)
+    w2 = ms.encode(nrm, x3, m2, 1)
+    ms.decode(nrm, w2, m2, n3, 1, 1.0)
+torch.cuda.synchronize()
+del x3
+st = torch.from_numpy(codec.mt19937_seed_state(42).view(np.int32)).to(dev)
+d = torch.empty(100_000_000, dtype=torch.int32, device=dev)
+for _ in range(REPS):
+    codec.mt19937_generate(st, d.numel(), out=d)
+torch.cuda.synchronize()
+del d
+n4, K4 = 14_728_266, 10_000
+x4 = torch.randn(n4, device=dev, generator=g).mul_(0.01)
+idx = torch.randperm(n4, generator=torch.Generator().manual_seed(42))[:K4].to(dev)
+rk = codec.RandKStep(x4, K4, 4, gen, 1)
+for _ in range(REPS):
+    w4, nk = rk.encode(idx)
+    rk.decode(w4, idx, x4, 1.0)
+torch.cuda.synchronize()
+del x4
+n = 100_000_000
+x = torch.randn(n, device=dev, generator=g).mul_(0.01)
+words = torch.empty(codec.qsgd_layout(n, 4, 1).plane_words, dtype=torch.int32, device=dev)
+for _ in range(REPS):
+    codec.absmax(x, out=nrm)
+    codec.qsgd_encode(x, nrm, 4, gen.reserve(n), 1, out=words)
+torch.cuda.synchronize()
+print("prof workload done")
