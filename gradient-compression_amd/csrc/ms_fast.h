@@ -655,11 +655,10 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
 // h Mm + pos: the block that owns mask quad t owns q quads t + h Mm/4 whole.
 // ---------------------------------------------------------------------------
 template <int KIND, int NL, int VAR = 0>
-__device__ __forceinline__ void fused_plane(const float *__restrict__ x, uint32_t n, uint32_t i0, const DivNorm &dv,
+__device__ __forceinline__ void fused_plane(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
                                             uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
                                             const RngArgs &rng, int32_t qmax, uint4 &m, uint4 &ln)
 {
-    const float4 v = load4_nt_tail<0>(x, i0, n);
     RangeI rg;
     rg.add4(v);
     m = make_uint4(0u, 0u, 0u, 0u);
@@ -750,17 +749,23 @@ __global__ __launch_bounds__(kBlock) void k_ms_fused_w1(const float *__restrict_
         uint4 acc[NL - 1] = {};
         if (t < quads) {
             // not unrolled: one copy of the per-plane body (with both rounding
-            // paths inlined) keeps the kernel's code and scalar registers small
+            // paths inlined) keeps the kernel's code and scalar registers small;
+            // the next plane's x is loaded before this plane's math (two loads in flight)
+            uint32_t P = wave;
+            uint32_t i0 = P * Mm + 4u * t;
+            float4 vn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (P < planes && i0 < n)
+                vn = load4_nt_tail<0>(x, i0, n);
 #pragma unroll 1
             for (int j = 0; j < 8; ++j) {
-                const uint32_t P = wave + 4u * j;
-                if (P >= planes)
+                if (P >= planes || i0 >= n)
                     break;
-                const uint32_t i0 = P * Mm + 4u * t;
-                if (i0 >= n)
-                    break;
+                const float4 v = vn;
+                const uint32_t Pn = P + 4u, i0n = i0 + 4u * Mm;
+                if (Pn < planes && i0n < n)
+                    vn = load4_nt_tail<0>(x, i0n, n);
                 uint4 m, ln;
-                fused_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng, qmax, m, ln);
+                fused_plane<KIND, NL, VAR>(v, n, i0, dv, lo2, hi2, lv, fa, rng, qmax, m, ln);
                 mask_bits<NL>(acc, m, P);
                 const uint32_t k = (P * kdiv) >> 16, h = P - k * r;
                 const uint32_t sh = k * wq;
@@ -768,6 +773,8 @@ __global__ __launch_bounds__(kBlock) void k_ms_fused_w1(const float *__restrict_
                 atomicOr(&qs[h][1][lane], ln.y << sh);
                 atomicOr(&qs[h][2][lane], ln.z << sh);
                 atomicOr(&qs[h][3][lane], ln.w << sh);
+                P = Pn;
+                i0 = i0n;
             }
         }
 #pragma unroll

@@ -188,9 +188,14 @@ static_assert(kMtJumpSpan >= kMtJumpPart + kMtJumpThreads + 4 && kMtJumpSpan % 6
 __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws)
 {
     __shared__ __attribute__((aligned(16))) uint32_t cp[4][kMtJumpSpan];
+    // the block's coefficient row, read from LDS (in order with the data reads:
+    // a scalar load in the loop would make every lgkmcnt wait drain to 0)
+    __shared__ __attribute__((aligned(16))) uint32_t cf[kMtN];
     const uint32_t tid = threadIdx.x;
     const uint64_t g = (uint64_t)blockIdx.x + 1;
-    const uint4 *__restrict__ coef4 = reinterpret_cast<const uint4 *>(table + (uint64_t)blockIdx.x * kMtN);
+    for (uint32_t i = tid; i < kMtN; i += kMtJumpThreads)
+        cf[i] = table[(uint64_t)blockIdx.x * kMtN + i];
+    const uint4 *coef4 = reinterpret_cast<const uint4 *>(cf);
     const uint32_t j = tid + 1;  // output word of this lane (1-based; lanes past 624 idle)
     // x_{k+j} = x_{k + tid + 1} = copy c[k + tid - c] with c = tid & 3 (copy c holds x_{i+c+1}): an
     // aligned 16-byte source, and lanes 4a .. 4a+3 (one ds_read_b128 lane group quarter) read the same
@@ -210,8 +215,9 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
         __syncthreads();
         const uint4 *p = reinterpret_cast<const uint4 *>(&cp[cj][oj]);
         for (uint32_t bi = 0; bi < kMtJumpPart / 128; ++bi) {
-            const uint4 c4 = coef4[(k0 >> 7) + bi];  // uniform: one scalar load of 4 coefficient words
-            const uint32_t cs[4] = {c4.x, c4.y, c4.z, c4.w};
+            const uint4 c4 = coef4[(k0 >> 7) + bi];  // 4 coefficient words (uniform LDS broadcast)
+            const uint32_t cs[4] = {__builtin_amdgcn_readfirstlane(c4.x), __builtin_amdgcn_readfirstlane(c4.y),
+                                    __builtin_amdgcn_readfirstlane(c4.z), __builtin_amdgcn_readfirstlane(c4.w)};
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
                 const uint32_t c = cs[cc];
