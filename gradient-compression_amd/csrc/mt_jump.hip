@@ -216,8 +216,10 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
         const uint4 *p = reinterpret_cast<const uint4 *>(&cp[cj][oj]);
         for (uint32_t bi = 0; bi < kMtJumpPart / 128; ++bi) {
             const uint4 c4 = coef4[(k0 >> 7) + bi];  // 4 coefficient words (uniform LDS broadcast)
-            const uint32_t cs[4] = {__builtin_amdgcn_readfirstlane(c4.x), __builtin_amdgcn_readfirstlane(c4.y),
-                                    __builtin_amdgcn_readfirstlane(c4.z), __builtin_amdgcn_readfirstlane(c4.w)};
+            const uint32_t cs[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(c4.x),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane(c4.y),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane(c4.z),
+                                    (uint32_t)__builtin_amdgcn_readfirstlane(c4.w)};
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
                 const uint32_t c = cs[cc];
