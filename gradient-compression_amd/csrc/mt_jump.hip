@@ -215,22 +215,27 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
         __syncthreads();
         const uint4 *p = reinterpret_cast<const uint4 *>(&cp[cj][oj]);
         for (uint32_t bi = 0; bi < kMtJumpPart / 128; ++bi) {
-            const uint4 c4 = coef4[(k0 >> 7) + bi];  // 4 coefficient words (uniform LDS broadcast)
-            const uint32_t cs[4] = {(uint32_t)__builtin_amdgcn_readfirstlane(c4.x),
-                                    (uint32_t)__builtin_amdgcn_readfirstlane(c4.y),
-                                    (uint32_t)__builtin_amdgcn_readfirstlane(c4.z),
-                                    (uint32_t)__builtin_amdgcn_readfirstlane(c4.w)};
+            // 4 coefficient words (uniform LDS broadcast), kept in VGPRs: each bit's 0 / ~0
+            // mask is one v_bfe_i32 (VALU) instead of one s_bfe_i32 per wave on the CU's
+            // shared scalar unit
+            const uint4 c4 = coef4[(k0 >> 7) + bi];
+            uint32_t z;  // an opaque per-lane zero keeps the words in VGPRs (divergence analysis)
+            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+            const uint32_t cs[4] = {c4.x + z, c4.y + z, c4.z + z, c4.w + z};
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
                 const uint32_t c = cs[cc];
-#pragma unroll
-                for (int b = 0; b < 32; b += 4) {
-                    const uint4 v = p[(bi * 4 + cc) * 8 + b / 4];
-                    acc0 = __builtin_amdgcn_bitop3_b32(acc0, v.x, 0u - ((c >> b) & 1u), 0x78);  // acc ^ (x & m)
-                    acc1 = __builtin_amdgcn_bitop3_b32(acc1, v.y, 0u - ((c >> (b + 1)) & 1u), 0x78);
-                    acc2 = __builtin_amdgcn_bitop3_b32(acc2, v.z, 0u - ((c >> (b + 2)) & 1u), 0x78);
-                    acc3 = __builtin_amdgcn_bitop3_b32(acc3, v.w, 0u - ((c >> (b + 3)) & 1u), 0x78);
-                }
+#define GC_MT_STEP(B)                                                                             \
+    {                                                                                             \
+        const uint4 v = p[(bi * 4 + cc) * 8 + (B) / 4];                                           \
+        acc0 = __builtin_amdgcn_bitop3_b32(acc0, v.x, 0u - ((c >> (B)) & 1u), 0x78); /* acc ^ (x & m) */ \
+        acc1 = __builtin_amdgcn_bitop3_b32(acc1, v.y, 0u - ((c >> ((B) + 1)) & 1u), 0x78);         \
+        acc2 = __builtin_amdgcn_bitop3_b32(acc2, v.z, 0u - ((c >> ((B) + 2)) & 1u), 0x78);         \
+        acc3 = __builtin_amdgcn_bitop3_b32(acc3, v.w, 0u - ((c >> ((B) + 3)) & 1u), 0x78);         \
+    }
+                GC_MT_STEP(0) GC_MT_STEP(4) GC_MT_STEP(8) GC_MT_STEP(12)
+                GC_MT_STEP(16) GC_MT_STEP(20) GC_MT_STEP(24) GC_MT_STEP(28)
+#undef GC_MT_STEP
             }
         }
     }
