@@ -14,8 +14,8 @@
 //               (32 twists of the state) into the workspace; window 0 = the
 //               state itself, plus the read index
 //   k_mt_jump   one workgroup per generator g >= 1: the stream x_0..x_20560 in
-//               LDS (four shifted copies, in four quarters), 640 threads, each
-//               accumulating one window word over the 19937 coefficient bits
+//               LDS (82 KB), 640 threads, each accumulating one window word
+//               over the 19937 coefficient bits
 //               (uniform per block: scalar loads of the jump table; per bit a
 //               uniform 0 / ~0 mask and one xor-and per word)
 //   k_mt_gen    one wave per generator: its window in LDS, wave-synchronous
@@ -168,79 +168,40 @@ __global__ __launch_bounds__(256) void k_mt_seq(const uint32_t *__restrict__ sta
     }
 }
 
-// window of generator g = blockIdx.x + 1: output word j (j = 1..624) is
+// window of generator g = blockIdx.x + 1: thread j-1 (j = 1..624) writes
 // x_{gJ-1+j} = XOR over the set coefficient bits k of table[g-1] of x_{k+j}.
-// LDS-bandwidth shaped (MI355X_MICROARCH.md §LDS: ds_read_b128 streams 256 B/clk,
-// ds_read_b32 and ds_read2_b64 half that): bits are taken four at a time and
-// lane j reads x_{k+j} .. x_{k+j+3} as ONE aligned 16-byte load from the copy
-// of the sequence shifted by (j - 1) & 3 (copy c holds x_{i+c+1}); four copies of the
-// whole k range do not fit the LDS, so the range runs in four quarters.  Ten
-// waves (one output word per lane), four independent xor chains per lane (bit
-// k mod 4) and the coefficient words fetched four at a time (one scalar load)
-// keep the LDS reads and the dependent xors overlapped.
-constexpr uint32_t kMtJumpPart = 4992;  // bits per quarter (4 x 4992 = 19968 >= 19937; 156 words, 39 x 4)
-// words of one copy per quarter: >= kMtJumpPart + kMtN + 20 (idle lanes up to j = 640 read in bounds),
-// a multiple of 4, and = 16 mod 64 so the four copies sit 16 banks apart and a ds_read_b128 lane
-// group (lanes 4a .. 4a+3 read the same index of copies 0..3) touches 64 distinct banks
-constexpr uint32_t kMtJumpSpan = 5648;
-static_assert(kMtJumpSpan >= kMtJumpPart + kMtJumpThreads + 4 && kMtJumpSpan % 64 == 16, "copy stride");
+// The whole stream x_0..x_20560 sits in LDS once (82 KB, one block per CU);
+// per coefficient bit one uniform s_bfe mask and one xor-and per lane, in four
+// independent chains (bit k mod 4).  Measured against four-copy ds_read_b128
+// forms (four LDS refills per block) and VALU masks, this is the fastest
+// (profiles/r02k_kernel_stats.csv and earlier r02 traces).
+constexpr uint32_t kMtSeqLds = 623 * 32 + 32 + kMtN;  // every (cw, b, j) read in bounds (pad = 0)
 
 __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t cp[4][kMtJumpSpan];
-    // the block's coefficient row, read from LDS (in order with the data reads:
-    // a scalar load in the loop would make every lgkmcnt wait drain to 0)
-    __shared__ __attribute__((aligned(16))) uint32_t cf[kMtN];
+    __shared__ uint32_t seq[kMtSeqLds];
     const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < kMtSeqLds; i += kMtJumpThreads)
+        seq[i] = i < kMtSeq ? ws[kWsSeq + i] : 0u;
+    __syncthreads();
     const uint64_t g = (uint64_t)blockIdx.x + 1;
-    for (uint32_t i = tid; i < kMtN; i += kMtJumpThreads)
-        cf[i] = table[(uint64_t)blockIdx.x * kMtN + i];
-    const uint4 *coef4 = reinterpret_cast<const uint4 *>(cf);
-    const uint32_t j = tid + 1;  // output word of this lane (1-based; lanes past 624 idle)
-    // x_{k+j} = x_{k + tid + 1} = copy c[k + tid - c] with c = tid & 3 (copy c holds x_{i+c+1}): an
-    // aligned 16-byte source, and lanes 4a .. 4a+3 (one ds_read_b128 lane group quarter) read the same
-    // index of copies 0..3, 16 banks apart
-    const uint32_t cj = tid & 3u, oj = tid - cj;
-    uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
-    for (uint32_t h = 0; h < 4; ++h) {
-        const uint32_t k0 = h * kMtJumpPart;
-        __syncthreads();
-        for (uint32_t i = tid; i < kMtJumpSpan; i += kMtJumpThreads) {
+    const uint32_t *__restrict__ coef = table + (uint64_t)blockIdx.x * kMtN;
+    const uint32_t j = tid + 1;
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    if (tid < kMtN) {
+        for (uint32_t cw = 0; cw < kMtN; ++cw) {
+            const uint32_t c = __builtin_amdgcn_readfirstlane(coef[cw]);
+            const uint32_t *p = seq + cw * 32u + j;
 #pragma unroll
-            for (uint32_t c = 0; c < 4; ++c) {
-                const uint32_t e = k0 + i + c + 1;
-                cp[c][i] = e < kMtSeq ? ws[kWsSeq + e] : 0u;
+            for (int b = 0; b < 32; b += 4) {  // uniform 0 / ~0 masks: one s_bfe_i32 each
+                a0 = __builtin_amdgcn_bitop3_b32(a0, p[b], 0u - ((c >> b) & 1u), 0x78);  // acc ^ (x & m)
+                a1 = __builtin_amdgcn_bitop3_b32(a1, p[b + 1], 0u - ((c >> (b + 1)) & 1u), 0x78);
+                a2 = __builtin_amdgcn_bitop3_b32(a2, p[b + 2], 0u - ((c >> (b + 2)) & 1u), 0x78);
+                a3 = __builtin_amdgcn_bitop3_b32(a3, p[b + 3], 0u - ((c >> (b + 3)) & 1u), 0x78);
             }
         }
-        __syncthreads();
-        const uint4 *p = reinterpret_cast<const uint4 *>(&cp[cj][oj]);
-        for (uint32_t bi = 0; bi < kMtJumpPart / 128; ++bi) {
-            // 4 coefficient words (uniform LDS broadcast), kept in VGPRs: each bit's 0 / ~0
-            // mask is one v_bfe_i32 (VALU) instead of one s_bfe_i32 per wave on the CU's
-            // shared scalar unit
-            const uint4 c4 = coef4[(k0 >> 7) + bi];
-            uint32_t z;  // an opaque per-lane zero keeps the words in VGPRs (divergence analysis)
-            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-            const uint32_t cs[4] = {c4.x + z, c4.y + z, c4.z + z, c4.w + z};
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-                const uint32_t c = cs[cc];
-#define GC_MT_STEP(B)                                                                             \
-    {                                                                                             \
-        const uint4 v = p[(bi * 4 + cc) * 8 + (B) / 4];                                           \
-        acc0 = __builtin_amdgcn_bitop3_b32(acc0, v.x, 0u - ((c >> (B)) & 1u), 0x78); /* acc ^ (x & m) */ \
-        acc1 = __builtin_amdgcn_bitop3_b32(acc1, v.y, 0u - ((c >> ((B) + 1)) & 1u), 0x78);         \
-        acc2 = __builtin_amdgcn_bitop3_b32(acc2, v.z, 0u - ((c >> ((B) + 2)) & 1u), 0x78);         \
-        acc3 = __builtin_amdgcn_bitop3_b32(acc3, v.w, 0u - ((c >> ((B) + 3)) & 1u), 0x78);         \
+        ws[kWsWin + g * kMtN + tid] = a0 ^ a1 ^ a2 ^ a3;
     }
-                GC_MT_STEP(0) GC_MT_STEP(4) GC_MT_STEP(8) GC_MT_STEP(12)
-                GC_MT_STEP(16) GC_MT_STEP(20) GC_MT_STEP(24) GC_MT_STEP(28)
-#undef GC_MT_STEP
-            }
-        }
-    }
-    if (j <= kMtN)
-        ws[kWsWin + g * kMtN + (j - 1)] = acc0 ^ acc1 ^ acc2 ^ acc3;
 }
 
 // one wave per generator: draws [gJ, min((g+1)J, count)) into out
