@@ -724,8 +724,9 @@ __device__ __forceinline__ void fused_plane(const float4 &v, uint32_t n, uint32_
 constexpr uint32_t kMsFusedMaxR = 8;  // q words per mask word at W = 1: 32 / (q lanes per word) <= 8
 
 // planes: r * Lq mask planes in use; kdiv = ceil(2^16 / r) (P / r = (P * kdiv) >> 16 for P < 32)
-template <int KIND, int NL, int VAR = 0>
-__global__ __launch_bounds__(kBlock) void k_ms_fused_w1(const float *__restrict__ x, uint32_t n,
+// WPB waves per block take the mask planes P = wave, wave + WPB, ...
+template <int KIND, int NL, int VAR = 0, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void k_ms_fused_w1(const float *__restrict__ x, uint32_t n,
                                                         const float *__restrict__ normp, LevelsArg lv, MsFastArg fa,
                                                         RngArgs rng, uint32_t Mm, uint32_t r, uint32_t kdiv,
                                                         uint32_t planes, uint32_t wq, int32_t qmax,
@@ -735,14 +736,14 @@ __global__ __launch_bounds__(kBlock) void k_ms_fused_w1(const float *__restrict_
     const DivNorm dv = make_div(norm);
     const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
     const uint32_t quads = Mm >> 2;
-    __shared__ uint4 part[3][kMsQuadsPerBlock];
+    __shared__ uint4 part[WPB - 1][kMsQuadsPerBlock];
     // the tile's q words, [h][element e of the quad][quad]: every wave ORs its
     // planes' lanes in (disjoint bit fields); bank = quad, conflict-free
     __shared__ uint32_t qs[kMsFusedMaxR][4][kMsQuadsPerBlock];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     uint32_t *qflat = &qs[0][0][0];
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
-        for (uint32_t i = threadIdx.x; i < r * 4u * kMsQuadsPerBlock; i += kBlock)
+        for (uint32_t i = threadIdx.x; i < r * 4u * kMsQuadsPerBlock; i += 64u * WPB)
             qflat[i] = 0u;
         __syncthreads();
         const uint32_t t = tb + lane;
@@ -757,11 +758,11 @@ __global__ __launch_bounds__(kBlock) void k_ms_fused_w1(const float *__restrict_
             if (P < planes && i0 < n)
                 vn = load4_nt_tail<0>(x, i0, n);
 #pragma unroll 1
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < 32 / WPB; ++j) {
                 if (P >= planes || i0 >= n)
                     break;
                 const float4 v = vn;
-                const uint32_t Pn = P + 4u, i0n = i0 + 4u * Mm;
+                const uint32_t Pn = P + WPB, i0n = i0 + WPB * Mm;
                 if (Pn < planes && i0n < n)
                     vn = load4_nt_tail<0>(x, i0n, n);
                 uint4 m, ln;
@@ -783,15 +784,18 @@ __global__ __launch_bounds__(kBlock) void k_ms_fused_w1(const float *__restrict_
                 part[wave - 1][lane] = acc[f];
             __syncthreads();
             if (wave == 0 && t < quads) {
-                const uint4 a = part[0][lane], b = part[1][lane], c = part[2][lane];
-                st_nt4u(mask_words + (uint64_t)f * Mm + 4u * t,
-                        make_uint4(acc[f].x | a.x | b.x | c.x, acc[f].y | a.y | b.y | c.y,
-                                   acc[f].z | a.z | b.z | c.z, acc[f].w | a.w | b.w | c.w));
+                uint4 o = acc[f];
+#pragma unroll
+                for (int q = 0; q < WPB - 1; ++q) {
+                    const uint4 a = part[q][lane];
+                    o = make_uint4(o.x | a.x, o.y | a.y, o.z | a.z, o.w | a.w);
+                }
+                st_nt4u(mask_words + (uint64_t)f * Mm + 4u * t, o);
             }
             __syncthreads();
         }
         // q words: quad tq of the tile in q stream h sits at q position h Mm + 4 (tb + tq)
-        for (uint32_t i = threadIdx.x; i < r * kMsQuadsPerBlock; i += kBlock) {
+        for (uint32_t i = threadIdx.x; i < r * kMsQuadsPerBlock; i += 64u * WPB) {
             const uint32_t h = i / kMsQuadsPerBlock, tq = i % kMsQuadsPerBlock;
             if (tb + tq < quads)
                 st_nt4u(words + (uint64_t)h * Mm + 4u * (tb + tq),

@@ -13,11 +13,12 @@
 //   k_mt_seq    one workgroup: the first 20561 raw words x_0.. of the stream
 //               (32 twists of the state) into the workspace; window 0 = the
 //               state itself, plus the read index
-//   k_mt_jump   one workgroup per generator g >= 1: the stream x_0..x_20560 in
-//               LDS (82 KB), 640 threads, each accumulating one window word
-//               over the 19937 coefficient bits
-//               (uniform per block: scalar loads of the jump table; per bit a
-//               uniform 0 / ~0 mask and one xor-and per word)
+//   k_mt_jump   8 workgroups per generator g >= 1, each over 1/8 of the 19937
+//               coefficient bits with its slice of x_0..x_20560 in LDS; a
+//               thread accumulates four window words from a sliding register
+//               window (one ds_read_b128 per four bits; per bit a uniform
+//               0 / ~0 mask and one xor-and per word); k_mt_gen XORs the 8
+//               partial windows
 //   k_mt_gen    one wave per generator: its window in LDS, wave-synchronous
 //               3-phase twists, tempered draws stored coalesced; the last
 //               generator writes the advanced state back
@@ -33,13 +34,13 @@ constexpr uint32_t kMtM = 397;
 constexpr uint32_t kMtJ = GC_MT_JUMP_DRAWS;
 constexpr uint32_t kMtSeq = 19937 + kMtN;              // x_0 .. x_20560 (k + j <= 19936 + 624)
 constexpr uint32_t kMtSeqWs = 33 * kMtN;              // 33 twist blocks cover kMtSeq
-constexpr uint32_t kMtJumpThreads = 640;              // 10 waves; thread t owns window word t
 constexpr uint32_t kMtGenWaves = 4;                   // generators per block of k_mt_gen
 
 static_assert(kMtJ % kMtN == 0, "generator windows stay aligned to the twist blocks");
 static_assert(kMtSeqWs >= kMtSeq, "sequence blocks");
 
-// workspace (uint32): [0] read index, [64 ..) sequence, then windows [G][624]
+// workspace (uint32): [0] read index, [64 ..) sequence, window 0, then the
+// jump partials of generators 1 .. G-1
 constexpr uint64_t kWsSeq = 64;
 constexpr uint64_t kWsWin = kWsSeq + kMtSeqWs;
 
@@ -168,40 +169,62 @@ __global__ __launch_bounds__(256) void k_mt_seq(const uint32_t *__restrict__ sta
     }
 }
 
-// window of generator g = blockIdx.x + 1: thread j-1 (j = 1..624) writes
-// x_{gJ-1+j} = XOR over the set coefficient bits k of table[g-1] of x_{k+j}.
-// The whole stream x_0..x_20560 sits in LDS once (82 KB, one block per CU);
-// per coefficient bit one uniform s_bfe mask and one xor-and per lane, in four
-// independent chains (bit k mod 4).  Measured against four-copy ds_read_b128
-// forms (four LDS refills per block) and VALU masks, this is the fastest
-// (profiles/r02k_kernel_stats.csv and earlier r02 traces).
-constexpr uint32_t kMtSeqLds = 623 * 32 + 32 + kMtN;  // every (cw, b, j) read in bounds (pad = 0)
+// window of generator g >= 1: x_{gJ-1+j} = XOR over the set coefficient bits k
+// of table[g-1] of x_{k+j}, j = 1..624, split over kMtJumpSplit blocks by
+// coefficient range (block s: bits [s*2496, (s+1)*2496), its slice of the
+// stream staged in 13 KB of LDS) whose partial windows k_mt_gen XORs.
+// Thread q owns the four window words j = 4q+1 .. 4q+4: over four consecutive
+// bits k..k+3 they need x_{k+j} .. x_{k+j+6}, a sliding register window fed by
+// ONE aligned ds_read_b128 per four bits (lanes read consecutive 16 B: no bank
+// conflicts), i.e. a quarter of a b32 read per (bit, word) where one word per
+// thread needed a whole one; per (bit, word) one xor-and with a uniform mask.
+constexpr uint32_t kMtJumpSplit = 8;                             // blocks per generator
+constexpr uint32_t kMtJumpWords = kMtN / kMtJumpSplit;           // 78 coefficient words per block
+constexpr uint32_t kMtJumpThreads = 192;                         // 3 waves; thread q < 156 owns words 4q..4q+3
+constexpr uint32_t kMtJumpLds = 4 * (kMtJumpWords * 8 + kMtJumpThreads);  // >= 4 (623 + 191 + 1) + 4
+static_assert(kMtJumpWords * kMtJumpSplit == kMtN, "coefficient split");
 
-__global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws)
+// workspace: partial windows [split][gens - 1][624] after window 0
+constexpr uint64_t kWsPart = kWsWin + kMtN;
+
+__global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws,
+                                                           uint32_t jumps)
 {
-    __shared__ uint32_t seq[kMtSeqLds];
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < kMtSeqLds; i += kMtJumpThreads)
-        seq[i] = i < kMtSeq ? ws[kWsSeq + i] : 0u;
-    __syncthreads();
-    const uint64_t g = (uint64_t)blockIdx.x + 1;
-    const uint32_t *__restrict__ coef = table + (uint64_t)blockIdx.x * kMtN;
-    const uint32_t j = tid + 1;
-    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    if (tid < kMtN) {
-        for (uint32_t cw = 0; cw < kMtN; ++cw) {
-            const uint32_t c = __builtin_amdgcn_readfirstlane(coef[cw]);
-            const uint32_t *p = seq + cw * 32u + j;
-#pragma unroll
-            for (int b = 0; b < 32; b += 4) {  // uniform 0 / ~0 masks: one s_bfe_i32 each
-                a0 = __builtin_amdgcn_bitop3_b32(a0, p[b], 0u - ((c >> b) & 1u), 0x78);  // acc ^ (x & m)
-                a1 = __builtin_amdgcn_bitop3_b32(a1, p[b + 1], 0u - ((c >> (b + 1)) & 1u), 0x78);
-                a2 = __builtin_amdgcn_bitop3_b32(a2, p[b + 2], 0u - ((c >> (b + 2)) & 1u), 0x78);
-                a3 = __builtin_amdgcn_bitop3_b32(a3, p[b + 3], 0u - ((c >> (b + 3)) & 1u), 0x78);
-            }
-        }
-        ws[kWsWin + g * kMtN + tid] = a0 ^ a1 ^ a2 ^ a3;
+    __shared__ uint4 lds4[kMtJumpLds / 4];
+    uint32_t *lds = reinterpret_cast<uint32_t *>(lds4);
+    const uint32_t gi = blockIdx.x / kMtJumpSplit, sp = blockIdx.x % kMtJumpSplit;
+    const uint32_t k0 = sp * kMtJumpWords * 32u;
+    for (uint32_t v = threadIdx.x; v < kMtJumpLds; v += kMtJumpThreads) {  // lds[v] = x_{k0+v+1} (0 past the end)
+        const uint32_t xi = k0 + v + 1;
+        lds[v] = xi < kMtSeqWs ? ws[kWsSeq + xi] : 0u;
     }
+    __syncthreads();
+    const uint32_t q = threadIdx.x;
+    const uint32_t *__restrict__ coef = table + (uint64_t)gi * kMtN + sp * kMtJumpWords;
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    uint4 A = lds4[q];
+    uint32_t cn = coef[0];
+    for (uint32_t cw = 0; cw < kMtJumpWords; ++cw) {
+        const uint32_t c = __builtin_amdgcn_readfirstlane(cn);
+        if (cw + 1 < kMtJumpWords)
+            cn = coef[cw + 1];
+#pragma unroll
+        for (uint32_t b = 0; b < 32; b += 4) {  // bits k = k0 + 32 cw + b + d, d = 0..3
+            const uint4 B = lds4[q + cw * 8u + b / 4u + 1u];
+            const uint32_t e[7] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z};  // x_{k+j} .. x_{k+j+6}, j = 4q+1
+#pragma unroll
+            for (uint32_t d = 0; d < 4; ++d) {
+                const uint32_t m = 0u - ((c >> (b + d)) & 1u);  // uniform 0 / ~0
+                a0 = __builtin_amdgcn_bitop3_b32(a0, e[d], m, 0x78);  // acc ^ (x & m)
+                a1 = __builtin_amdgcn_bitop3_b32(a1, e[d + 1], m, 0x78);
+                a2 = __builtin_amdgcn_bitop3_b32(a2, e[d + 2], m, 0x78);
+                a3 = __builtin_amdgcn_bitop3_b32(a3, e[d + 3], m, 0x78);
+            }
+            A = B;
+        }
+    }
+    if (q < kMtN / 4)
+        *reinterpret_cast<uint4 *>(ws + kWsPart + ((uint64_t)sp * jumps + gi) * kMtN + 4u * q) = make_uint4(a0, a1, a2, a3);
 }
 
 // one wave per generator: draws [gJ, min((g+1)J, count)) into out
@@ -214,8 +237,17 @@ __global__ __launch_bounds__(64 * kMtGenWaves) void k_mt_gen(uint32_t *__restric
     if (g >= gens)
         return;  // whole waves only: nothing below synchronises across waves
     uint32_t *s = win[wave];
-    for (uint32_t i = lane; i < kMtN; i += 64)
-        s[i] = ws[kWsWin + g * kMtN + i];
+    if (g == 0)
+        for (uint32_t i = lane; i < kMtN; i += 64)
+            s[i] = ws[kWsWin + i];
+    else
+        for (uint32_t i = lane; i < kMtN; i += 64) {
+            uint32_t v = 0;
+#pragma unroll
+            for (uint32_t sp = 0; sp < kMtJumpSplit; ++sp)
+                v ^= ws[kWsPart + (sp * (gens - 1) + g - 1) * kMtN + i];
+            s[i] = v;
+        }
     uint32_t ptr = ws[0];
     lds_order();
     uint64_t pos = g * kMtJ;
@@ -261,7 +293,7 @@ extern "C" {
 size_t gc_mt19937_workspace_size(uint64_t count)
 {
     const uint64_t gens = count ? (count + kMtJ - 1) / kMtJ : 1;
-    return 4 * (kWsWin + gens * kMtN);
+    return 4 * (kWsPart + kMtJumpSplit * (gens - 1) * kMtN);
 }
 
 int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,
@@ -275,12 +307,13 @@ int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, u
     GC_REQUIRE(gens - 1 <= table_gens && (gens == 1 || table_dev),
                "gc_mt19937_generate_jumped: jump table holds %llu generators, %llu draws need %llu",
                (unsigned long long)table_gens, (unsigned long long)count, (unsigned long long)(gens - 1));
-    GC_REQUIRE(gens <= 0x7fffffffull, "gc_mt19937_generate_jumped: count too large");
+    GC_REQUIRE(gens <= 0x7fffffffull / kMtJumpSplit, "gc_mt19937_generate_jumped: count too large");
     hipStream_t st = as_stream(stream);
     uint32_t *ws = reinterpret_cast<uint32_t *>(workspace);
     hipLaunchKernelGGL(k_mt_seq, dim3(1), dim3(256), 0, st, state_dev, ws);
     if (gens > 1)
-        hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)(gens - 1)), dim3(kMtJumpThreads), 0, st, table_dev, ws);
+        hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)((gens - 1) * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st, table_dev,
+                           ws, (uint32_t)(gens - 1));
     hipLaunchKernelGGL(k_mt_gen, dim3((unsigned)((gens + kMtGenWaves - 1) / kMtGenWaves)), dim3(64 * kMtGenWaves), 0,
                        st, ws, gens, count, out, state_dev);
     return launch_status("gc_mt19937_generate_jumped");

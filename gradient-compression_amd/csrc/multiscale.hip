@@ -407,11 +407,11 @@ int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_leve
     hipLaunchKernelGGL((k_ms_fused_w1<KIND_, NL_, VAR_>), dim3(g), dim3(kBlock), 0, st, x, (uint32_t)n, norm, la, \
                        fa, ra, Mm, r, kdiv, planes, q_lanes->bits, qmax, mask_words, words)
     if (levels->count == 2) {
-        if (rng->kind == GC_RNG_PHILOX) { if (wide) GC_FW(0, 2, MSV_WIDE); else GC_FW(0, 2, 0); }
-        else { if (wide) GC_FW(1, 2, MSV_WIDE); else GC_FW(1, 2, 0); }
+        if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 2, MSV_WIDE); } else { GC_FW(0, 2, 0); } }
+        else { if (wide) { GC_FW(1, 2, MSV_WIDE); } else { GC_FW(1, 2, 0); } }
     } else {
-        if (rng->kind == GC_RNG_PHILOX) { if (wide) GC_FW(0, 3, MSV_WIDE); else GC_FW(0, 3, 0); }
-        else { if (wide) GC_FW(1, 3, MSV_WIDE); else GC_FW(1, 3, 0); }
+        if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 3, MSV_WIDE); } else { GC_FW(0, 3, 0); } }
+        else { if (wide) { GC_FW(1, 3, MSV_WIDE); } else { GC_FW(1, 3, 0); } }
     }
 #undef GC_FW
     return launch_status("gc_ms_encode_w1");
