@@ -13,12 +13,11 @@
 //   k_mt_seq    one workgroup: the first 20561 raw words x_0.. of the stream
 //               (32 twists of the state) into the workspace; window 0 = the
 //               state itself, plus the read index
-//   k_mt_jump   8 workgroups per generator g >= 1, each over 1/8 of the 19937
-//               coefficient bits with its slice of x_0..x_20560 in LDS; a
-//               thread accumulates four window words from a sliding register
-//               window (one ds_read_b128 per four bits; per bit a uniform
-//               0 / ~0 mask and one xor-and per word); k_mt_gen XORs the 8
-//               partial windows
+//   k_mt_jump   16 workgroups per generator g >= 1, each over 1/16 of the
+//               19937 coefficient bits with four shifted copies of its slice
+//               of x_0..x_20560 in LDS; per SET bit a thread reads four
+//               stream words (one aligned ds_read_b128) into its four window
+//               words; k_mt_gen XORs the 16 partial windows
 //   k_mt_gen    one wave per generator: its window in LDS, wave-synchronous
 //               3-phase twists, tempered draws stored coalesced; the last
 //               generator writes the advanced state back
@@ -171,18 +170,26 @@ __global__ __launch_bounds__(256) void k_mt_seq(const uint32_t *__restrict__ sta
 
 // window of generator g >= 1: x_{gJ-1+j} = XOR over the set coefficient bits k
 // of table[g-1] of x_{k+j}, j = 1..624, split over kMtJumpSplit blocks by
-// coefficient range (block s: bits [s*2496, (s+1)*2496), its slice of the
-// stream staged in 13 KB of LDS) whose partial windows k_mt_gen XORs.
-// Thread q owns the four window words j = 4q+1 .. 4q+4: over four consecutive
-// bits k..k+3 they need x_{k+j} .. x_{k+j+6}, a sliding register window fed by
-// ONE aligned ds_read_b128 per four bits (lanes read consecutive 16 B: no bank
-// conflicts), i.e. a quarter of a b32 read per (bit, word) where one word per
-// thread needed a whole one; per (bit, word) one xor-and with a uniform mask.
-constexpr uint32_t kMtJumpSplit = 8;                             // blocks per generator
-constexpr uint32_t kMtJumpWords = kMtN / kMtJumpSplit;           // 78 coefficient words per block
+// coefficient range (block s: bits [s*1248, (s+1)*1248)) whose partial windows
+// k_mt_gen XORs.  Only SET bits cost work (about half of them):
+//   - the block expands its 39 coefficient words into a list of set-bit
+//     positions in LDS (popcount prefix over the words);
+//   - thread q owns the four window words j = 4q+1 .. 4q+4; for set bit k it
+//     needs x_{k+j} .. x_{k+j+3}, an aligned ds_read_b128 from the copy of the
+//     stream slice shifted by k mod 4 (four copies in LDS; lanes read
+//     consecutive 16 B: no bank conflicts);
+//   - two set bits fold into each window word with one v_xor3.
+// LDS traffic is the bound: 16 B per (set bit, thread).  (The earlier forms —
+// one word per thread with a uniform mask per bit, then a sliding b128 window
+// with a mask per bit — were VALU-bound at 506 and 207 us for 1e8 draws.)
+constexpr uint32_t kMtJumpSplit = 16;                            // blocks per generator
+constexpr uint32_t kMtJumpWords = kMtN / kMtJumpSplit;           // 39 coefficient words per block
+constexpr uint32_t kMtJumpBits = kMtJumpWords * 32;              // 1248
 constexpr uint32_t kMtJumpThreads = 192;                         // 3 waves; thread q < 156 owns words 4q..4q+3
-constexpr uint32_t kMtJumpLds = 4 * (kMtJumpWords * 8 + kMtJumpThreads);  // >= 4 (623 + 191 + 1) + 4
+constexpr uint32_t kMtJumpOwners = kMtN / 4;                     // 156
+constexpr uint32_t kMtJumpQuads = (kMtJumpBits / 4 + kMtJumpThreads + 1 + 7) & ~7u;  // per copy: a + q < 504
 static_assert(kMtJumpWords * kMtJumpSplit == kMtN, "coefficient split");
+static_assert((kMtJumpBits - 1) / 4 + kMtJumpThreads - 1 < kMtJumpQuads, "copy length");
 
 // workspace: partial windows [split][gens - 1][624] after window 0
 constexpr uint64_t kWsPart = kWsWin + kMtN;
@@ -190,41 +197,76 @@ constexpr uint64_t kWsPart = kWsWin + kMtN;
 __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws,
                                                            uint32_t jumps)
 {
-    __shared__ uint4 lds4[kMtJumpLds / 4];
-    uint32_t *lds = reinterpret_cast<uint32_t *>(lds4);
+    __shared__ uint4 cp4[4 * kMtJumpQuads];  // copy r: word u = x_{k0 + u + r + 1}
+    __shared__ alignas(16) uint32_t pos[kMtJumpBits + 8];  // byte offset of set bit kk in its copy: ((kk&3)*Q + (kk>>2)) * 16
+    __shared__ uint32_t cnt[kMtJumpWords + 1];
+    uint32_t *cp = reinterpret_cast<uint32_t *>(cp4);
     const uint32_t gi = blockIdx.x / kMtJumpSplit, sp = blockIdx.x % kMtJumpSplit;
-    const uint32_t k0 = sp * kMtJumpWords * 32u;
-    for (uint32_t v = threadIdx.x; v < kMtJumpLds; v += kMtJumpThreads) {  // lds[v] = x_{k0+v+1} (0 past the end)
+    const uint32_t k0 = sp * kMtJumpBits, tid = threadIdx.x;
+    const uint32_t *__restrict__ coef = table + (uint64_t)gi * kMtN + sp * kMtJumpWords;
+    uint32_t c = 0;
+    if (tid < kMtJumpWords) {
+        c = coef[tid];
+        cnt[tid + 1] = __builtin_popcount(c);
+    }
+    for (uint32_t v = tid; v < 4 * kMtJumpQuads + 3; v += kMtJumpThreads) {
         const uint32_t xi = k0 + v + 1;
-        lds[v] = xi < kMtSeqWs ? ws[kWsSeq + xi] : 0u;
+        const uint32_t x = xi < kMtSeqWs ? ws[kWsSeq + xi] : 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r)
+            if (v >= r && v - r < 4 * kMtJumpQuads)
+                cp[r * 4 * kMtJumpQuads + v - r] = x;
     }
     __syncthreads();
-    const uint32_t q = threadIdx.x;
-    const uint32_t *__restrict__ coef = table + (uint64_t)gi * kMtN + sp * kMtJumpWords;
-    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    uint4 A = lds4[q];
-    uint32_t cn = coef[0];
-    for (uint32_t cw = 0; cw < kMtJumpWords; ++cw) {
-        const uint32_t c = __builtin_amdgcn_readfirstlane(cn);
-        if (cw + 1 < kMtJumpWords)
-            cn = coef[cw + 1];
-#pragma unroll
-        for (uint32_t b = 0; b < 32; b += 4) {  // bits k = k0 + 32 cw + b + d, d = 0..3
-            const uint4 B = lds4[q + cw * 8u + b / 4u + 1u];
-            const uint32_t e[7] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z};  // x_{k+j} .. x_{k+j+6}, j = 4q+1
-#pragma unroll
-            for (uint32_t d = 0; d < 4; ++d) {
-                const uint32_t m = 0u - ((c >> (b + d)) & 1u);  // uniform 0 / ~0
-                a0 = __builtin_amdgcn_bitop3_b32(a0, e[d], m, 0x78);  // acc ^ (x & m)
-                a1 = __builtin_amdgcn_bitop3_b32(a1, e[d + 1], m, 0x78);
-                a2 = __builtin_amdgcn_bitop3_b32(a2, e[d + 2], m, 0x78);
-                a3 = __builtin_amdgcn_bitop3_b32(a3, e[d + 3], m, 0x78);
-            }
-            A = B;
+    if (tid == 0) {
+        uint32_t t = 0;
+        cnt[0] = 0;
+        for (uint32_t w = 1; w <= kMtJumpWords; ++w)
+            cnt[w] = t += cnt[w];
+    }
+    __syncthreads();
+    if (tid < kMtJumpWords) {
+        uint32_t o = cnt[tid];
+        while (c) {
+            const uint32_t kk = tid * 32 + __builtin_ctz(c);
+            c &= c - 1;
+            pos[o++] = ((kk & 3u) * kMtJumpQuads + (kk >> 2)) * 16u;
         }
     }
-    if (q < kMtN / 4)
-        *reinterpret_cast<uint4 *>(ws + kWsPart + ((uint64_t)sp * jumps + gi) * kMtN + 4u * q) = make_uint4(a0, a1, a2, a3);
+    __syncthreads();
+    if (tid >= kMtJumpOwners)
+        return;  // no barrier below
+    const uint32_t n = cnt[kMtJumpWords];
+    const char *base = reinterpret_cast<const char *>(cp4) + 16u * tid;
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    auto ld = [&](uint32_t off) { return *reinterpret_cast<const uint4 *>(base + off); };
+    auto fold2 = [&](const uint4 &u, const uint4 &v) {  // v_xor3 (truth table 0x96)
+        a0 = __builtin_amdgcn_bitop3_b32(a0, u.x, v.x, 0x96);
+        a1 = __builtin_amdgcn_bitop3_b32(a1, u.y, v.y, 0x96);
+        a2 = __builtin_amdgcn_bitop3_b32(a2, u.z, v.z, 0x96);
+        a3 = __builtin_amdgcn_bitop3_b32(a3, u.w, v.w, 0x96);
+    };
+    uint32_t i = 0;
+    const uint4 *pos4 = reinterpret_cast<const uint4 *>(pos);
+    uint4 q0 = pos4[0], q1 = pos4[1];  // the next batch's positions, loaded one batch ahead
+    for (; i + 8 <= n; i += 8) {
+        const uint4 p0 = q0, p1 = q1;
+        q0 = pos4[i / 4 + 2];  // in bounds: pos has kMtJumpBits + 8 entries
+        q1 = pos4[i / 4 + 3];
+        const uint4 u0 = ld(p0.x), u1 = ld(p0.y), u2 = ld(p0.z), u3 = ld(p0.w);
+        const uint4 u4 = ld(p1.x), u5 = ld(p1.y), u6 = ld(p1.z), u7 = ld(p1.w);
+        fold2(u0, u1);
+        fold2(u2, u3);
+        fold2(u4, u5);
+        fold2(u6, u7);
+        // keep the prefetch where it is: the positions arrived before u0..u7 (DS returns in order)
+        asm volatile("" : "+v"(q0.x), "+v"(q0.y), "+v"(q0.z), "+v"(q0.w), "+v"(q1.x), "+v"(q1.y), "+v"(q1.z), "+v"(q1.w));
+    }
+    for (; i + 2 <= n; i += 2)
+        fold2(ld(pos[i]), ld(pos[i + 1]));
+    if (i < n)
+        fold2(ld(pos[i]), make_uint4(0u, 0u, 0u, 0u));
+    *reinterpret_cast<uint4 *>(ws + kWsPart + ((uint64_t)sp * jumps + gi) * kMtN + 4u * tid) = make_uint4(a0, a1, a2, a3);
 }
 
 // one wave per generator: draws [gJ, min((g+1)J, count)) into out
