@@ -18,9 +18,10 @@
 //               of x_0..x_20560 in LDS; per SET bit a thread reads four
 //               stream words (one aligned ds_read_b128) into its four window
 //               words; k_mt_gen XORs the 16 partial windows
-//   k_mt_gen    one wave per generator: its window in LDS, wave-synchronous
-//               3-phase twists, tempered draws stored coalesced; the last
-//               generator writes the advanced state back
+//   k_mt_gen    one 3-wave workgroup per generator: its window in LDS; one
+//               wave twists (column-owned, in registers; double-buffered
+//               blocks) while two temper the previous block and store the
+//               draws coalesced; the last generator writes the state back
 // Bit-exact with the serial stream (tests/test_gpu_parity.py vs the oracle's
 // MT19937 and the reference's torch-mode goldens).
 #include "gc_device.h"
@@ -33,7 +34,6 @@ constexpr uint32_t kMtM = 397;
 constexpr uint32_t kMtJ = GC_MT_JUMP_DRAWS;
 constexpr uint32_t kMtSeq = 19937 + kMtN;              // x_0 .. x_20560 (k + j <= 19936 + 624)
 constexpr uint32_t kMtSeqWs = 33 * kMtN;              // 33 twist blocks cover kMtSeq
-constexpr uint32_t kMtGenWaves = 4;                   // generators per block of k_mt_gen
 
 static_assert(kMtJ % kMtN == 0, "generator windows stay aligned to the twist blocks");
 static_assert(kMtSeqWs >= kMtSeq, "sequence blocks");
@@ -58,70 +58,45 @@ __device__ __forceinline__ uint32_t mtj_mix(uint32_t a, uint32_t b, uint32_t c)
     return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
 
-// compiler-level ordering of LDS accesses between the phases of a
-// wave-synchronous twist (the hardware executes one wave's DS ops in order)
-__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
-
-// one in-place twist of a 624-word window by one wave (s[k] = s[k+397] ^
-// twist(s[k], s[k+1]) in k order): phase A k < 227 reads only old words,
-// B k < 454 reads s[k-227] from A, C k < 624 from B (and s[0] from A for
-// k = 623).  Every lane loads all its inputs of a phase before any store.
-// EMIT: the new block is consumed whole, so each new word is also tempered and
-// stored to out[k] straight from the register that computed it (no LDS read
-// back; the stores drain while the next phase's loads are in flight).
-template <bool EMIT>
-__device__ __forceinline__ void twist_wave(uint32_t *s, uint32_t lane, uint32_t *__restrict__ out = nullptr)
+// the twist block after `o` into `nw` (another buffer) by one wave.  With
+// H = 227: nw[k] = mix(o[k], o[k+1], o[k+397]) for k < H, mix(o[k], o[k+1],
+// nw[k-H]) for k < 623, and nw[623] = mix(o[623], nw[0], nw[396]).  Lane
+// column m (< H) owns nw[m], nw[m+H], nw[m+2H]: each word's in-block
+// dependency is the word before it in the SAME lane, so the three phases run
+// in registers (only nw[0] crosses lanes: a readlane) after one batch of
+// old-block loads.
+__device__ __forceinline__ void twist_into(const uint32_t *o, uint32_t *nw, uint32_t lane)
 {
     constexpr uint32_t H = kMtN - kMtM;  // 227
-    uint32_t v[4];
+    uint32_t oa[4], ob[4], oc[4], pb[4], qb[4], pc[4], qc[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const uint32_t k = lane + 64u * r;
-        v[r] = k < H ? mtj_mix(s[k], s[k + 1], s[k + kMtM]) : 0u;
+        const uint32_t m = min(lane + 64u * r, H - 1);
+        oa[r] = o[m];
+        ob[r] = o[m + 1];
+        oc[r] = o[m + kMtM];
+        pb[r] = o[m + H];
+        qb[r] = o[m + H + 1];
+        pc[r] = o[min(m + 2 * H, kMtN - 1)];
+        qc[r] = o[min(m + 2 * H + 1, kMtN - 1)];
     }
-    lds_order();
+    uint32_t A[4], B[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const uint32_t k = lane + 64u * r;
-        if (k < H) {
-            s[k] = v[r];
-            if constexpr (EMIT)
-                out[k] = mtj_temper(v[r]);
+        A[r] = mtj_mix(oa[r], ob[r], oc[r]);
+        B[r] = mtj_mix(pb[r], qb[r], A[r]);
+    }
+    const uint32_t nw0 = __builtin_amdgcn_readlane(A[0], 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t m = lane + 64u * r;
+        if (m < H) {
+            nw[m] = A[r];
+            nw[m + H] = B[r];
+            if (m + 2 * H < kMtN)
+                nw[m + 2 * H] = mtj_mix(pc[r], m + 2 * H == kMtN - 1 ? nw0 : qc[r], B[r]);
         }
     }
-    lds_order();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint32_t k = H + lane + 64u * r;
-        v[r] = k < 2 * H ? mtj_mix(s[k], s[k + 1], s[k - H]) : 0u;
-    }
-    lds_order();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint32_t k = H + lane + 64u * r;
-        if (k < 2 * H) {
-            s[k] = v[r];
-            if constexpr (EMIT)
-                out[k] = mtj_temper(v[r]);
-        }
-    }
-    lds_order();
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const uint32_t k = 2 * H + lane + 64u * r;
-        v[r] = k < kMtN - 1 ? mtj_mix(s[k], s[k + 1], s[k - H]) : (k == kMtN - 1 ? mtj_mix(s[k], s[0], s[k - H]) : 0u);
-    }
-    lds_order();
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const uint32_t k = 2 * H + lane + 64u * r;
-        if (k < kMtN) {
-            s[k] = v[r];
-            if constexpr (EMIT)
-                out[k] = mtj_temper(v[r]);
-        }
-    }
-    lds_order();
 }
 
 // x_0 .. x_{kMtSeqWs-1} of the caller's state frame; window 0 and the read index
@@ -269,60 +244,67 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
     *reinterpret_cast<uint4 *>(ws + kWsPart + ((uint64_t)sp * jumps + gi) * kMtN + 4u * tid) = make_uint4(a0, a1, a2, a3);
 }
 
-// one wave per generator: draws [gJ, min((g+1)J, count)) into out
-__global__ __launch_bounds__(64 * kMtGenWaves) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t count,
-                                                             uint32_t *__restrict__ out, uint32_t *__restrict__ state)
+// one workgroup of three waves per generator: draws [gJ, min((g+1)J, count))
+// into out.  Wave 0 twists block t+1 into the other buffer while waves 1-2
+// temper block t and store it (one barrier per block): the serial chain is the
+// twist alone, the tempering and the HBM stores ride beside it.
+constexpr uint32_t kMtGenThreads = 192;
+
+__global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t count,
+                                                         uint32_t *__restrict__ out, uint32_t *__restrict__ state)
 {
-    __shared__ uint32_t win[kMtGenWaves][kMtN];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint64_t g = (uint64_t)blockIdx.x * kMtGenWaves + wave;
-    if (g >= gens)
-        return;  // whole waves only: nothing below synchronises across waves
-    uint32_t *s = win[wave];
+    __shared__ uint32_t buf[2][kMtN];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const uint64_t g = blockIdx.x;
     if (g == 0)
-        for (uint32_t i = lane; i < kMtN; i += 64)
-            s[i] = ws[kWsWin + i];
+        for (uint32_t i = tid; i < kMtN; i += kMtGenThreads)
+            buf[0][i] = ws[kWsWin + i];
     else
-        for (uint32_t i = lane; i < kMtN; i += 64) {
+        for (uint32_t i = tid; i < kMtN; i += kMtGenThreads) {
             uint32_t v = 0;
 #pragma unroll
             for (uint32_t sp = 0; sp < kMtJumpSplit; ++sp)
                 v ^= ws[kWsPart + (sp * (gens - 1) + g - 1) * kMtN + i];
-            s[i] = v;
+            buf[0][i] = v;
         }
-    uint32_t ptr = ws[0];
-    lds_order();
-    uint64_t pos = g * kMtJ;
-    const uint64_t end = min(pos + kMtJ, count);
-    // head: the rest of the current block
-    if (ptr < kMtN) {
-        const uint32_t take = (uint32_t)min((uint64_t)(kMtN - ptr), end - pos);
-        for (uint32_t i = lane; i < take; i += 64)
-            out[pos + i] = mtj_temper(s[ptr + i]);
-        lds_order();
-        pos += take;
-        ptr += take;
+    const uint32_t ptr0 = ws[0];
+    __syncthreads();
+    const uint64_t pos0 = g * kMtJ, end = min(pos0 + kMtJ, count);
+    const uint32_t head = ptr0 < kMtN ? (uint32_t)min((uint64_t)(kMtN - ptr0), end - pos0) : 0u;  // rest of block 0
+    const uint64_t rest = end - pos0 - head;
+    const uint32_t twists = (uint32_t)((rest + kMtN - 1) / kMtN);
+    const uint32_t ct = tid - 64u;  // consumer thread 0..127
+    for (uint32_t t = 0; t <= twists; ++t) {
+        const uint32_t *cur = buf[t & 1u];
+        if (wave == 0) {
+            if (t < twists)
+                twist_into(cur, buf[(t + 1) & 1u], lane);
+        } else if (t == 0) {
+            for (uint32_t i = ct; i < head; i += 128)
+                out[pos0 + i] = mtj_temper(cur[ptr0 + i]);
+        } else {
+            const uint64_t at = pos0 + head + (uint64_t)(t - 1) * kMtN;
+            uint32_t *o = out + at;
+            const uint32_t take = (uint32_t)min((uint64_t)kMtN, end - at);
+            if (take == kMtN) {
+#pragma unroll
+                for (uint32_t r = 0; r < 5; ++r) {
+                    const uint32_t i = ct + 128u * r;
+                    if (r < 4 || i < kMtN)
+                        o[i] = mtj_temper(cur[i]);
+                }
+            } else {
+                for (uint32_t i = ct; i < take; i += 128)
+                    o[i] = mtj_temper(cur[i]);
+            }
+        }
+        __syncthreads();
     }
-    // body: whole blocks, emitted by the twist itself
-    while (end - pos >= kMtN) {
-        twist_wave<true>(s, lane, out + pos);
-        pos += kMtN;
-        ptr = kMtN;
-    }
-    // tail: a partial block
-    if (pos < end) {
-        twist_wave<false>(s, lane);
-        const uint32_t take = (uint32_t)(end - pos);
-        for (uint32_t i = lane; i < take; i += 64)
-            out[pos + i] = mtj_temper(s[i]);
-        lds_order();
-        ptr = take;
-    }
-    if (g == gens - 1) {  // the advanced state: this window (aligned to the twist blocks) + read index
-        for (uint32_t i = lane; i < kMtN; i += 64)
-            state[i] = s[i];
-        if (lane == 0)
-            state[kMtN] = ptr;
+    if (g == gens - 1) {  // the advanced state: the last block (aligned to the twist blocks) + read index
+        for (uint32_t i = tid; i < kMtN; i += kMtGenThreads)
+            state[i] = buf[twists & 1u][i];
+        if (tid == 0)
+            state[kMtN] = twists ? (uint32_t)(rest - (uint64_t)(twists - 1) * kMtN) : ptr0 + head;
     }
 }
 
@@ -356,8 +338,7 @@ int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, u
     if (gens > 1)
         hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)((gens - 1) * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st, table_dev,
                            ws, (uint32_t)(gens - 1));
-    hipLaunchKernelGGL(k_mt_gen, dim3((unsigned)((gens + kMtGenWaves - 1) / kMtGenWaves)), dim3(64 * kMtGenWaves), 0,
-                       st, ws, gens, count, out, state_dev);
+    hipLaunchKernelGGL(k_mt_gen, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out, state_dev);
     return launch_status("gc_mt19937_generate_jumped");
 }
 
