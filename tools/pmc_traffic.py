@@ -21,8 +21,12 @@ def _rows(pattern):
             yield from csv.DictReader(f)
 
 
+KERNELS = ("k_qsgd_encode", "k_absmax", "k_qsgd_decode", "k_ms_fused_w1", "k_ms_mask_fast", "k_ms_select_fast",
+           "k_ms_decode_fast", "k_mt_seq", "k_mt_jump", "k_mt_gen", "k_randk_gather", "k_decode_scatter1")
+
+
 def _short(name):
-    for k in ("k_qsgd_encode", "k_absmax", "k_qsgd_decode"):
+    for k in KERNELS:
         if k in name:
             return k
     return name[:60]
@@ -52,6 +56,17 @@ def main(tag, n=100_000_000, bits=4):
         f, w = fetch.get(k), write.get(k)
         out["kernels"][k] = {"fetch_size_kib_raw": f, "write_size_kib": w,
                              "hbm_bytes_per_launch": None if f is None or w is None else (2 * f + w) * 1024}
+    # the per-kernel workload of tools/prof_kernels.py (tools/profile_r02.sh -> prof_<tag>_k)
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out", f"prof_{tag}_k")):
+        kf, kw = counter(f"{tag}_k", "fetch", "FETCH_SIZE"), counter(f"{tag}_k", "write", "WRITE_SIZE")
+        kstats = glob.glob(os.path.join(ROOT, "gpurun_out", f"prof_{tag}_k", "trace", "**", "*kernel_stats.csv"),
+                           recursive=True)
+        if kstats:
+            shutil.copy(kstats[0], os.path.join(ROOT, "profiles", f"{tag}_k_kernel_stats.csv"))
+        out["prof_kernels"] = {"workload": "tools/prof_kernels.py (see its docstring)", "kernels": {
+            k: {"fetch_size_kib_raw": kf.get(k), "write_size_kib": kw.get(k),
+                "hbm_bytes_per_launch": None if kf.get(k) is None or kw.get(k) is None else (2 * kf[k] + kw[k]) * 1024}
+            for k in sorted(set(kf) | set(kw))}}
     for name in (f"{tag}_pmc.json", "pmc_traffic.json"):
         with open(os.path.join(ROOT, "profiles", name), "w") as fh:
             json.dump(out, fh, indent=1)

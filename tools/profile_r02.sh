@@ -5,7 +5,7 @@
 set -u
 TAG=${1:-r02}
 ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
-OUT="$ROOT/gpurun_out/prof_$TAG"
+OUT="$ROOT/gpurun_out/prof_${TAG}_k"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 W="$ROOT/tools/prof_kernels.py"
