@@ -565,13 +565,19 @@ def main():
         torch.manual_seed(42)
         nm = codec.absmax(x)
         pgen.reserve(n)  # warm: builds the jump table once per process
+        codec.qsgd_encode_torch(x, nm, bits, 1, out=words, lanes=lanes)
         torch.cuda.synchronize()
         reps_mt = 5
         t0 = time.perf_counter()
-        for _ in range(reps_mt):
+        for _ in range(reps_mt):  # draw buffer: 4n bytes of draws, then the full-chip encode reads them
             codec.qsgd_encode(x, nm, bits, pgen.reserve(n), 1, out=words, lanes=lanes)
         torch.cuda.synchronize()
         t_mt = (time.perf_counter() - t0) / reps_mt
+        t0 = time.perf_counter()
+        for _ in range(reps_mt):  # fused: the generator kernel quantizes with its own draws, then the lane pack
+            codec.qsgd_encode_torch(x, nm, bits, 1, out=words, lanes=lanes)
+        torch.cuda.synchronize()
+        t_mt_fused = (time.perf_counter() - t0) / reps_mt
         st = codec.mt19937_seed_state(42)
         sd = torch.from_numpy(st.view(np.int32)).to(dev)
         draws = torch.empty(n, dtype=torch.int32, device=dev)
@@ -579,11 +585,13 @@ def main():
         ms_ser = _events(torch, lambda: codec.mt19937_generate(sd, 10_000_000, out=draws, parallel=False), 1)
         out["torch_parity_mode"] = {
             "n": n, "grad_floats_per_s": n / t_mt, "ms_per_call": t_mt * 1e3,
+            "fused_generator_quantize_ms_per_call": t_mt_fused * 1e3,
             "mt19937_parallel_ms": ms_gen, "mt19937_parallel_draws_per_s": n / (ms_gen * 1e-3),
             "mt19937_serial_draws_per_s": 10_000_000 / (ms_ser * 1e-3),
             "note": "torch-CPU-generator (MT19937) draws, bit-exact with compressors.py: jump-ahead parallel "
                     "generators (gc_mt19937_generate_jumped) -> encode from the draws; includes the torch "
-                    "state hand-off (H2D + D2H sync) per call"}
+                    "state hand-off (H2D + D2H sync) per call.  fused_*: the generator kernel quantizes "
+                    "with its own draws (gc_qsgd_quantize_mt19937, no draw buffer) + lane pack"}
         del draws
 
     if not args.no_extras:

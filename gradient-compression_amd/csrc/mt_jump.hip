@@ -24,8 +24,11 @@
 //               draws coalesced; the last generator writes the state back
 // Bit-exact with the serial stream (tests/test_gpu_parity.py vs the oracle's
 // MT19937 and the reference's torch-mode goldens).
+#include <type_traits>
+
 #include "gc_device.h"
 #include "gc_host.h"
+#include "qsgd_encode.h"
 
 namespace gc {
 
@@ -58,45 +61,29 @@ __device__ __forceinline__ uint32_t mtj_mix(uint32_t a, uint32_t b, uint32_t c)
     return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
 
-// the twist block after `o` into `nw` (another buffer) by one wave.  With
-// H = 227: nw[k] = mix(o[k], o[k+1], o[k+397]) for k < H, mix(o[k], o[k+1],
-// nw[k-H]) for k < 623, and nw[623] = mix(o[623], nw[0], nw[396]).  Lane
-// column m (< H) owns nw[m], nw[m+H], nw[m+2H]: each word's in-block
-// dependency is the word before it in the SAME lane, so the three phases run
-// in registers (only nw[0] crosses lanes: a readlane) after one batch of
-// old-block loads.
-__device__ __forceinline__ void twist_into(const uint32_t *o, uint32_t *nw, uint32_t lane)
+// column m (< H = 227) of the twist block after `o`, written into `nw`
+// (another buffer): nw[m] = mix(o[m], o[m+1], o[m+397]), nw[m+H] =
+// mix(o[m+H], o[m+H+1], nw[m]) and, for m < 170, nw[m+2H] = mix(o[m+2H],
+// o[m+2H+1], nw[m+H]) with nw[0] in place of o[624] for word 623 (recomputed
+// from o there).  Each word's in-block dependency is the column's previous
+// word, so a column is three register steps after one batch of loads, and the
+// 227 columns are independent: one per lane of the twisting waves.
+__device__ __forceinline__ void twist_column(const uint32_t *o, uint32_t *nw, uint32_t m)
 {
     constexpr uint32_t H = kMtN - kMtM;  // 227
-    uint32_t oa[4], ob[4], oc[4], pb[4], qb[4], pc[4], qc[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint32_t m = min(lane + 64u * r, H - 1);
-        oa[r] = o[m];
-        ob[r] = o[m + 1];
-        oc[r] = o[m + kMtM];
-        pb[r] = o[m + H];
-        qb[r] = o[m + H + 1];
-        pc[r] = o[min(m + 2 * H, kMtN - 1)];
-        qc[r] = o[min(m + 2 * H + 1, kMtN - 1)];
-    }
-    uint32_t A[4], B[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        A[r] = mtj_mix(oa[r], ob[r], oc[r]);
-        B[r] = mtj_mix(pb[r], qb[r], A[r]);
-    }
-    const uint32_t nw0 = __builtin_amdgcn_readlane(A[0], 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint32_t m = lane + 64u * r;
-        if (m < H) {
-            nw[m] = A[r];
-            nw[m + H] = B[r];
-            if (m + 2 * H < kMtN)
-                nw[m + 2 * H] = mtj_mix(pc[r], m + 2 * H == kMtN - 1 ? nw0 : qc[r], B[r]);
-        }
-    }
+    if (m >= H)
+        return;
+    const uint32_t a0 = o[m], a1 = o[m + 1], a2 = o[m + kMtM], b0 = o[m + H], b1 = o[m + H + 1];
+    const uint32_t k = m + 2 * H;
+    const uint32_t c0 = o[min(k, kMtN - 1)], c1 = o[min(k + 1, kMtN - 1)];
+    const uint32_t A = mtj_mix(a0, a1, a2);
+    const uint32_t B = mtj_mix(b0, b1, A);
+    nw[m] = A;
+    nw[m + H] = B;
+    if (k < kMtN - 1)
+        nw[k] = mtj_mix(c0, c1, B);
+    else if (k == kMtN - 1)
+        nw[k] = mtj_mix(c0, mtj_mix(o[0], o[1], o[kMtM]), B);
 }
 
 // x_0 .. x_{kMtSeqWs-1} of the caller's state frame; window 0 and the read index
@@ -166,8 +153,10 @@ constexpr uint32_t kMtJumpQuads = (kMtJumpBits / 4 + kMtJumpThreads + 1 + 7) & ~
 static_assert(kMtJumpWords * kMtJumpSplit == kMtN, "coefficient split");
 static_assert((kMtJumpBits - 1) / 4 + kMtJumpThreads - 1 < kMtJumpQuads, "copy length");
 
-// workspace: partial windows [split][gens - 1][624] after window 0
+// workspace: partial windows [split][gens - 1][624] after window 0; word 1 is
+// the quantize modes' sink for out-of-range stores
 constexpr uint64_t kWsPart = kWsWin + kMtN;
+constexpr uint64_t kWsSpare = 1;
 
 __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws,
                                                            uint32_t jumps)
@@ -244,17 +233,88 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
     *reinterpret_cast<uint4 *>(ws + kWsPart + ((uint64_t)sp * jumps + gi) * kMtN + 4u * tid) = make_uint4(a0, a1, a2, a3);
 }
 
-// one workgroup of three waves per generator: draws [gJ, min((g+1)J, count))
-// into out.  Wave 0 twists block t+1 into the other buffer while waves 1-2
-// temper block t and store it (one barrier per block): the serial chain is the
-// twist alone, the tempering and the HBM stores ride beside it.
-constexpr uint32_t kMtGenThreads = 192;
+// one workgroup of kMtTwistWaves + kMtTemperWaves waves per generator: draws
+// [gJ, min((g+1)J, count)) into out.  The twisting waves (one column per lane)
+// build block t+1 in the other buffer while the tempering waves temper block t
+// and store it (one barrier per block): the serial chain is one column's three
+// register steps per block; the tempering and the HBM stores ride beside it.
+// MODE 0: out = the draws (uint32).  MODE 1 / 2: draw i is consumed at once by
+// element i of x, as torch.bernoulli consumes it (compressors.py:299-316), and
+// out = q = sign(x)*xi as int8 / int32: the draws never reach HBM.
+constexpr uint32_t kMtTwistWaves = 4;  // 256 lanes >= the 227 columns
+constexpr uint32_t kMtTemperWaves = 4;
+constexpr uint32_t kMtTemperThreads = 64 * kMtTemperWaves;
+constexpr uint32_t kMtGenThreads = 64 * kMtTwistWaves + kMtTemperThreads;
+constexpr uint32_t kMtRounds = (kMtN + kMtTemperThreads - 1) / kMtTemperThreads;  // elements per tempering thread
 
+constexpr uint32_t kMtPre = 4;  // blocks of x in flight per tempering thread (quantize modes)
+
+// the per-block hand-off between the twisting and the tempering waves: only the
+// LDS traffic has to be complete (__syncthreads would also drain every global
+// load and store in flight: the draws' stores and the x prefetch)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// RN(|x| / norm) as the reference computes it: Markstein's one-correction
+// quotient where it is exact (the encode's per-tile check made
+// per element), else the IEEE division
+__device__ __forceinline__ float mt_quot(float v, const DivNorm &dv)
+{
+    const float a = fabsf(v);
+    const uint32_t b = __float_as_uint(a);
+    return (dv.fast && b - 1u >= dv.lo1 && b <= dv.hi) ? div_fast(a, dv) : a / dv.norm;
+}
+
+template <int MODE>
+__device__ __forceinline__ void mt_store_q(void *out, uint64_t e, float v, uint32_t r, const DivNorm &dv, float s)
+{
+    const uint32_t q = enc_lane<0>(v, mt_quot(v, dv), s, 0, r);
+    if constexpr (MODE == 1)
+        reinterpret_cast<int8_t *>(out)[e] = (int8_t)q;
+    else
+        reinterpret_cast<int32_t *>(out)[e] = (int32_t)q;
+}
+
+template <int MODE>
+__device__ __forceinline__ void mt_emit(void *out, uint64_t e, uint32_t r, const float *__restrict__ x,
+                                        const DivNorm &dv, float s)
+{
+    if constexpr (MODE == 0)
+        reinterpret_cast<uint32_t *>(out)[e] = r;
+    else
+        mt_store_q<MODE>(out, e, x[e], r, dv, s);
+}
+
+// x of the block starting at element `at` into ring row `row` (768 floats:
+// element i of the block at row[i]) as tempering thread ct consumes it, with
+// global_load_lds_dword: the data goes straight to LDS (lane l of a wave to
+// M0 + 4 l), no registers wait for it.  Indices are clamped into [0, end), so
+// every thread issues exactly kMtRounds loads per call and the waves' memory
+// counter counts nothing else (they issue no other global memory operation in
+// the loop): s_waitcnt vmcnt((kMtPre - 1) * kMtRounds) before reading a row
+// is exact.  The row's previous contents must have been read (lgkmcnt(0)).
+__device__ __forceinline__ void mt_load_row(float *row, const float *__restrict__ x, uint64_t at, uint64_t end,
+                                            uint32_t ct)
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (uint32_t r = 0; r < kMtRounds; ++r) {
+        const float *p = x + min(at + min(ct + kMtTemperThreads * r, kMtN - 1), end - 1);
+        const uint32_t lds = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(row + kMtTemperThreads * r + (ct & ~63u)));
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(lds), "v"(p) : "memory");
+    }
+}
+static_assert(kMtPre == 4 && kMtRounds == 3, "mt_wait_row's count");
+__device__ __forceinline__ void mt_wait_row() { asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); }
+
+template <int MODE>
 __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t count,
-                                                         uint32_t *__restrict__ out, uint32_t *__restrict__ state)
+                                                         void *__restrict__ out, uint32_t *__restrict__ state,
+                                                         const float *__restrict__ x, const float *__restrict__ normp,
+                                                         float s, void *__restrict__ spare)
 {
     __shared__ uint32_t buf[2][kMtN];
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
     const uint64_t g = blockIdx.x;
     if (g == 0)
         for (uint32_t i = tid; i < kMtN; i += kMtGenThreads)
@@ -273,33 +333,96 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
     const uint32_t head = ptr0 < kMtN ? (uint32_t)min((uint64_t)(kMtN - ptr0), end - pos0) : 0u;  // rest of block 0
     const uint64_t rest = end - pos0 - head;
     const uint32_t twists = (uint32_t)((rest + kMtN - 1) / kMtN);
-    const uint32_t ct = tid - 64u;  // consumer thread 0..127
-    for (uint32_t t = 0; t <= twists; ++t) {
-        const uint32_t *cur = buf[t & 1u];
-        if (wave == 0) {
-            if (t < twists)
-                twist_into(cur, buf[(t + 1) & 1u], lane);
-        } else if (t == 0) {
-            for (uint32_t i = ct; i < head; i += 128)
-                out[pos0 + i] = mtj_temper(cur[ptr0 + i]);
-        } else {
+    const uint32_t ct = tid - 64u * kMtTwistWaves;  // tempering thread 0 .. kMtTemperThreads-1
+    // The twisting wave and the tempering waves run separate loops with the
+    // same number of barriers (twists + 1): each loop is straight-line code
+    // for the compiler's memory-counter tracking, so the tempering waves'
+    // prefetched x loads stay in flight across blocks.
+    typedef typename std::conditional<MODE == 2, int32_t, int8_t>::type QT;
+    __shared__ QT qbuf[2][kMtN];  // quantize modes: q of block t in qbuf[t & 1], stored by the twisting waves
+    __shared__ float xring[MODE ? kMtPre : 1][MODE ? kMtTemperThreads * kMtRounds : 1];  // x, kMtPre blocks ahead
+    if (wave < kMtTwistWaves) {
+        // block t's q (t >= 1) lands in qbuf[t & 1] during iteration t and is
+        // stored to HBM by these waves during iteration t + 1: the global stores
+        // never sit in the same wave as the tempering waves' x prefetch
+        auto store_q = [&](uint32_t t) {
+            const uint64_t at = t ? pos0 + head + (uint64_t)(t - 1) * kMtN : pos0;
+            const uint32_t take = t ? (uint32_t)min((uint64_t)kMtN, end - at) : head;
+            QT *o = reinterpret_cast<QT *>(out) + at;
+            for (uint32_t i = tid; i < take; i += 64u * kMtTwistWaves)
+                o[i] = qbuf[t & 1u][i];
+        };
+        for (uint32_t t = 0; t < twists; ++t) {
+            twist_column(buf[t & 1u], buf[(t + 1) & 1u], tid);
+            if (MODE != 0 && t > 0)
+                store_q(t - 1);
+            lds_barrier();
+        }
+        if (MODE != 0 && twists > 0)
+            store_q(twists - 1);
+        lds_barrier();
+        if (MODE != 0)
+            store_q(twists);
+    } else if constexpr (MODE == 0) {
+        for (uint32_t i = ct; i < head; i += kMtTemperThreads)
+            mt_emit<0>(out, pos0 + i, mtj_temper(buf[0][ptr0 + i]), x, DivNorm{}, s);
+        lds_barrier();
+        for (uint32_t t = 1; t <= twists; ++t) {
+            const uint32_t *cur = buf[t & 1u];
             const uint64_t at = pos0 + head + (uint64_t)(t - 1) * kMtN;
-            uint32_t *o = out + at;
             const uint32_t take = (uint32_t)min((uint64_t)kMtN, end - at);
             if (take == kMtN) {
 #pragma unroll
-                for (uint32_t r = 0; r < 5; ++r) {
-                    const uint32_t i = ct + 128u * r;
-                    if (r < 4 || i < kMtN)
-                        o[i] = mtj_temper(cur[i]);
+                for (uint32_t r = 0; r < kMtRounds; ++r) {
+                    const uint32_t i = ct + kMtTemperThreads * r;
+                    if (i < kMtN)
+                        mt_emit<0>(out, at + i, mtj_temper(cur[i]), x, DivNorm{}, s);
                 }
             } else {
-                for (uint32_t i = ct; i < take; i += 128)
-                    o[i] = mtj_temper(cur[i]);
+                for (uint32_t i = ct; i < take; i += kMtTemperThreads)
+                    mt_emit<0>(out, at + i, mtj_temper(cur[i]), x, DivNorm{}, s);
+            }
+            lds_barrier();
+        }
+    } else {
+        // quantize modes: x of block t is fetched kMtPre blocks ahead into an
+        // LDS ring by global_load_lds (mt_load_row), and these waves issue no
+        // other global memory operation in the loop (their q goes to qbuf, the
+        // twisting waves store it), so each wait is an exact count
+        const DivNorm dv = make_div(*normp);
+        const uint64_t body = pos0 + head;  // element of block 1's first draw
+        for (uint32_t i = ct; i < head; i += kMtTemperThreads) {
+            const float v = x[pos0 + i];
+            qbuf[0][i] = (QT)enc_lane<0>(v, mt_quot(v, dv), s, 0, mtj_temper(buf[0][ptr0 + i]));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the head's loads: the ring's counts start from zero
+#pragma unroll
+        for (uint32_t d = 0; d < kMtPre; ++d)
+            mt_load_row(xring[d], x, body + (uint64_t)d * kMtN, end, ct);
+        lds_barrier();
+        for (uint32_t t0 = 1; t0 <= twists; t0 += kMtPre) {
+#pragma unroll
+            for (uint32_t d = 0; d < kMtPre; ++d) {
+                const uint32_t t = t0 + d;
+                if (t > twists)
+                    break;  // uniform over the tempering waves
+                const uint32_t *cur = buf[t & 1u];
+                const uint64_t at = body + (uint64_t)(t - 1) * kMtN;
+                mt_wait_row();
+#pragma unroll
+                for (uint32_t r = 0; r < kMtRounds; ++r) {
+                    const uint32_t i = ct + kMtTemperThreads * r;
+                    const uint32_t ic = min(i, kMtN - 1);  // past 623: recomputes word 623 (same x, same draw)
+                    const float v = xring[d][i];
+                    qbuf[t & 1u][ic] = (QT)enc_lane<0>(v, mt_quot(v, dv), s, 0, mtj_temper(cur[ic]));
+                }
+                mt_load_row(xring[d], x, at + (uint64_t)kMtPre * kMtN, end, ct);
+                lds_barrier();
             }
         }
-        __syncthreads();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-bound load outlives the workgroup
     }
+    __syncthreads();
     if (g == gens - 1) {  // the advanced state: the last block (aligned to the twist blocks) + read index
         for (uint32_t i = tid; i < kMtN; i += kMtGenThreads)
             state[i] = buf[twists & 1u][i];
@@ -320,26 +443,55 @@ size_t gc_mt19937_workspace_size(uint64_t count)
     return 4 * (kWsPart + kMtJumpSplit * (gens - 1) * kMtN);
 }
 
-int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,
-                               uint64_t count, void *workspace, gc_stream_t stream)
+// seq -> jump -> gen<MODE> for `count` draws of state_dev
+static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens,
+                  void *out, uint64_t count, void *workspace, gc_stream_t stream, const float *x, const float *norm,
+                  float s)
 {
-    GC_REQUIRE(state_dev && workspace, "gc_mt19937_generate_jumped: null state/workspace");
-    GC_REQUIRE(count == 0 || out, "gc_mt19937_generate_jumped: null out");
+    GC_REQUIRE(state_dev && workspace, "%s: null state/workspace", what);
+    GC_REQUIRE(count == 0 || out, "%s: null out", what);
     if (count == 0)
         return GC_OK;
     const uint64_t gens = (count + kMtJ - 1) / kMtJ;
     GC_REQUIRE(gens - 1 <= table_gens && (gens == 1 || table_dev),
-               "gc_mt19937_generate_jumped: jump table holds %llu generators, %llu draws need %llu",
-               (unsigned long long)table_gens, (unsigned long long)count, (unsigned long long)(gens - 1));
-    GC_REQUIRE(gens <= 0x7fffffffull / kMtJumpSplit, "gc_mt19937_generate_jumped: count too large");
+               "%s: jump table holds %llu generators, %llu draws need %llu", what, (unsigned long long)table_gens,
+               (unsigned long long)count, (unsigned long long)(gens - 1));
+    GC_REQUIRE(gens <= 0x7fffffffull / kMtJumpSplit, "%s: count too large", what);
     hipStream_t st = as_stream(stream);
     uint32_t *ws = reinterpret_cast<uint32_t *>(workspace);
     hipLaunchKernelGGL(k_mt_seq, dim3(1), dim3(256), 0, st, state_dev, ws);
     if (gens > 1)
         hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)((gens - 1) * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st, table_dev,
                            ws, (uint32_t)(gens - 1));
-    hipLaunchKernelGGL(k_mt_gen, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out, state_dev);
-    return launch_status("gc_mt19937_generate_jumped");
+    if (mode == 0)
+        hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out,
+                           state_dev, x, norm, s, ws + kWsSpare);
+    else if (mode == 1)
+        hipLaunchKernelGGL(k_mt_gen<1>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out,
+                           state_dev, x, norm, s, ws + kWsSpare);
+    else
+        hipLaunchKernelGGL(k_mt_gen<2>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out,
+                           state_dev, x, norm, s, ws + kWsSpare);
+    return launch_status(what);
+}
+
+int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,
+                               uint64_t count, void *workspace, gc_stream_t stream)
+{
+    return mt_run("gc_mt19937_generate_jumped", 0, state_dev, table_dev, table_gens, out, count, workspace, stream,
+                  nullptr, nullptr, 0.0f);
+}
+
+int gc_qsgd_quantize_mt19937(const float *x, uint64_t n, const float *norm, uint32_t bits, uint32_t *state_dev,
+                             const uint32_t *table_dev, uint64_t table_gens, void *q, uint32_t q_dtype,
+                             void *workspace, gc_stream_t stream)
+{
+    GC_REQUIRE(bits >= 1 && bits <= 8, "gc_qsgd_quantize_mt19937: bits must be 1..8");
+    GC_REQUIRE(q_dtype == GC_I32 || (q_dtype == GC_I8 && bits <= 7),
+               "gc_qsgd_quantize_mt19937: q_dtype must be GC_I8 (bits <= 7) or GC_I32");
+    GC_REQUIRE(n == 0 || (x && norm), "gc_qsgd_quantize_mt19937: null x/norm");
+    return mt_run("gc_qsgd_quantize_mt19937", q_dtype == GC_I8 ? 1 : 2, state_dev, table_dev, table_gens, q, n,
+                  workspace, stream, x, norm, (float)((1u << bits) - 1u));
 }
 
 }  // extern "C"

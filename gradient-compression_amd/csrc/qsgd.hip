@@ -5,7 +5,7 @@
 //   k_qsgd_decode   unpack W-summed lanes + dequantize + 1/W
 //                   (compressors.py:318-321, reducer.py:544-549)
 //   k_qsgd_quantize / k_qsgd_dequantize   unpacked int8/int32 drop-ins
-//   k_lane_pack / k_lane_unpack           packing of already-quantized ints
+//   k_lane_pack4 / k_lane_unpack          packing of already-quantized ints
 //
 // Memory-bound streaming kernels.  Planar lane layout: word j of the packed
 // stream holds elements j + k*M (k < L), so a thread that owns words
@@ -199,19 +199,95 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_dequantize(const QT *__restrict
 // ---------------------------------------------------------------------------
 // lane pack / unpack of integer arrays
 // ---------------------------------------------------------------------------
-template <int L, typename QT>
-__global__ __launch_bounds__(kBlock) void k_lane_pack(const QT *__restrict__ q, uint64_t n, int32_t off, uint32_t w,
-                                                      uint64_t M, uint32_t *__restrict__ words)
+// four consecutive words per thread: one 4-byte (int8) / 16-byte (int32) load
+// per plane (plane starts are 4-word aligned, check_lanes)
+template <typename QT>
+__device__ __forceinline__ int4 load_q4(const QT *__restrict__ q, uint64_t i, uint64_t n)
 {
-    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < M; j += (uint64_t)gridDim.x * kBlock) {
-        uint32_t acc = 0;
+    if (i + 3 < n) {
+        if constexpr (sizeof(QT) == 1) {
+            const uint32_t u = *reinterpret_cast<const uint32_t *>(q + i);
+            return make_int4((int8_t)u, (int8_t)(u >> 8), (int8_t)(u >> 16), (int8_t)(u >> 24));
+        } else {
+            return *reinterpret_cast<const int4 *>(q + i);
+        }
+    }
+    return make_int4(i < n ? (int32_t)q[i] : 0, i + 1 < n ? (int32_t)q[i + 1] : 0, i + 2 < n ? (int32_t)q[i + 2] : 0,
+                     i + 3 < n ? (int32_t)q[i + 3] : 0);
+}
+
+template <int L, typename QT>
+__global__ __launch_bounds__(kBlock) void k_lane_pack4(const QT *__restrict__ q, uint64_t n, int32_t off, uint32_t w,
+                                                       uint64_t M, uint32_t *__restrict__ words)
+{
+    const uint64_t quads = M >> 2;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < quads; t += (uint64_t)gridDim.x * kBlock) {
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (int k = 0; k < L; ++k) {
-            const uint64_t i = (uint64_t)k * M + j;
-            if (i < n)
-                acc |= (uint32_t)((int32_t)q[i] + off) << ((uint32_t)k * w);
+            const uint64_t i = (uint64_t)k * M + 4 * t;
+            if (i >= n)
+                break;
+            const int4 v = load_q4(q, i, n);
+            const uint32_t sh = (uint32_t)k * w;
+            acc.x |= (uint32_t)(v.x + off) << sh;
+            acc.y |= i + 1 < n ? (uint32_t)(v.y + off) << sh : 0u;
+            acc.z |= i + 2 < n ? (uint32_t)(v.z + off) << sh : 0u;
+            acc.w |= i + 3 < n ? (uint32_t)(v.w + off) << sh : 0u;
         }
-        words[j] = acc;
+        *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
+    }
+}
+
+// int8 q with 16-word-aligned planes (M % 16 == 0, every big bucket): a block
+// owns 4096 consecutive words, thread t words 16t .. 16t+15 of them: one
+// 16-byte nontemporal load per plane, then the words go through LDS so that
+// every store instruction writes 1 KB of consecutive words per wave
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_lane_pack16(const int8_t *__restrict__ q, uint64_t n, int32_t off,
+                                                        uint32_t w, uint64_t M, uint32_t *__restrict__ words)
+{
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    __shared__ u4v stage[kBlock * 4];
+    const uint64_t groups = M >> 4;
+    for (uint64_t g0 = (uint64_t)blockIdx.x * kBlock; g0 < groups; g0 += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t t = g0 + threadIdx.x;
+        if (t < groups) {
+            uint32_t acc[16] = {};
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                const uint64_t i = (uint64_t)k * M + 16 * t;
+                if (i >= n)
+                    break;
+                const uint32_t sh = (uint32_t)k * w;
+                if (i + 15 < n) {
+                    const u4v u = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(q + i));
+                    const uint32_t v4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                    for (int j = 0; j < 16; ++j)
+                        acc[j] |= (uint32_t)((int32_t)(int8_t)(v4[j >> 2] >> (8 * (j & 3))) + off) << sh;
+                } else {
+                    for (int j = 0; j < 16; ++j)
+                        if (i + j < n)
+                            acc[j] |= (uint32_t)((int32_t)q[i + j] + off) << sh;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {  // quad j of thread t at slot 4t + j, rotated by t against bank conflicts
+                const u4v r = {acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
+                stage[4 * threadIdx.x + ((j + threadIdx.x) & 3)] = r;
+            }
+        }
+        __syncthreads();
+        const uint64_t quads = min((uint64_t)kBlock, groups - g0) * 4;  // word quads of this block chunk
+        u4v *o = reinterpret_cast<u4v *>(words + 16 * g0);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t s = j * kBlock + threadIdx.x;  // quad s = 4 * owner + its j'
+            if (s < quads)
+                __builtin_nontemporal_store(stage[4 * (s >> 2) + (((s & 3) + (s >> 2)) & 3)], o + s);
+        }
+        __syncthreads();
     }
 }
 
@@ -523,16 +599,22 @@ int gc_lane_pack(const void *q, uint32_t q_dtype, const gc_lanes *lanes, uint32_
     if (lanes->plane_words == 0)
         return GC_OK;
     hipStream_t st = as_stream(stream);
-    const unsigned grid = grid_for(lanes->plane_words);
+    const unsigned grid = grid_for(lanes->plane_words / 4);
     const int32_t off = (int32_t)lanes->offset;
-    if (q_dtype == GC_I8) {
+    if (q_dtype == GC_I8 && lanes->plane_words % 16 == 0 && (reinterpret_cast<uintptr_t>(q) & 15u) == 0 &&
+        (reinterpret_cast<uintptr_t>(words) & 15u) == 0) {
         GC_DISPATCH_L(lanes->per_word,
-                      hipLaunchKernelGGL((k_lane_pack<LL, int8_t>), dim3(grid), dim3(kBlock), 0, st,
+                      hipLaunchKernelGGL((k_lane_pack16<LL>), dim3(grid_for(lanes->plane_words / 16)), dim3(kBlock), 0,
+                                         st, reinterpret_cast<const int8_t *>(q), lanes->n, off, lanes->bits,
+                                         lanes->plane_words, words));
+    } else if (q_dtype == GC_I8) {
+        GC_DISPATCH_L(lanes->per_word,
+                      hipLaunchKernelGGL((k_lane_pack4<LL, int8_t>), dim3(grid), dim3(kBlock), 0, st,
                                          reinterpret_cast<const int8_t *>(q), lanes->n, off, lanes->bits,
                                          lanes->plane_words, words));
     } else {
         GC_DISPATCH_L(lanes->per_word,
-                      hipLaunchKernelGGL((k_lane_pack<LL, int32_t>), dim3(grid), dim3(kBlock), 0, st,
+                      hipLaunchKernelGGL((k_lane_pack4<LL, int32_t>), dim3(grid), dim3(kBlock), 0, st,
                                          reinterpret_cast<const int32_t *>(q), lanes->n, off, lanes->bits,
                                          lanes->plane_words, words));
     }

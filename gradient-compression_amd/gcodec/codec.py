@@ -666,13 +666,78 @@ def mt19937_generate(state_dev: torch.Tensor, count: int, out=None, parallel: bo
         return out
     gens = -(-count // _lib.GC_MT_JUMP_DRAWS)
     table, tgens = _mt_jump_table(dev, gens - 1) if gens > 1 else (None, 0)
-    need = int(lib.gc_mt19937_workspace_size(count))
+    ws = _mt_ws(dev, st, count)
+    check(lib.gc_mt19937_generate_jumped(_p(state_dev), _p(table), tgens, _p(out), count, _p(ws), st),
+          "gc_mt19937_generate_jumped")
+    return out
+
+
+def _mt_ws(dev, st, count: int) -> torch.Tensor:
+    need = int(_lib.load().gc_mt19937_workspace_size(count))
     key = (dev.index, st.value)
     ws = _MT_WS.get(key)
     if ws is None or ws.numel() < need:
         ws = _MT_WS[key] = torch.empty(need, dtype=torch.uint8, device=dev)
-    check(lib.gc_mt19937_generate_jumped(_p(state_dev), _p(table), tgens, _p(out), count, _p(ws), st),
-          "gc_mt19937_generate_jumped")
+    return ws
+
+
+def _torch_state_to(device) -> torch.Tensor:
+    from .rng import torch_mt_state
+
+    words, idx = torch_mt_state()
+    st = np.empty(625, dtype=np.uint32)
+    st[:624] = words
+    st[624] = idx
+    return torch.from_numpy(st.view(np.int32)).to(device)
+
+
+def _torch_state_back(state_dev: torch.Tensor):
+    from .rng import set_torch_mt_state
+
+    new = state_dev.cpu().numpy().view(np.uint32)  # synchronises
+    set_torch_mt_state(new[:624], int(new[624]))
+
+
+def _quantize_mt(x, norm_t, bits, q, state_dev):
+    dev = _dev(x)
+    n = x.numel()
+    st = _stream(dev)
+    gens = -(-n // _lib.GC_MT_JUMP_DRAWS) if n else 1
+    table, tgens = _mt_jump_table(dev, gens - 1) if gens > 1 else (None, 0)
+    check(_lib.load().gc_qsgd_quantize_mt19937(_p(x), n, _p(norm_t), bits, _p(state_dev), _p(table), tgens, _p(q),
+                                               DTYPE_CODE[q.dtype], _p(_mt_ws(dev, st, n)), st),
+          "gc_qsgd_quantize_mt19937")
+
+
+def qsgd_quantize_torch(x, norm, bits, dtype=None, out=None) -> torch.Tensor:
+    """compressors.py:299-316 under torch's CPU generator (torch mode): the
+    MT19937 draws are generated on the GPU and consumed in the same kernel (no
+    4n draw buffer); torch's generator state advances by x.numel() draws."""
+    dev = _dev(x)
+    x = _f32(x, "qsgd_quantize_torch")
+    dtype = dtype or (torch.int8 if bits < 8 else torch.int32)
+    q = out if out is not None else torch.empty(x.numel(), dtype=dtype, device=dev)
+    state_dev = _torch_state_to(dev)
+    _quantize_mt(x, norm_tensor(norm, dev), bits, q, state_dev)
+    _torch_state_back(state_dev)
+    return q
+
+
+def qsgd_encode_torch(x, norm, bits, world=1, out=None, lanes=None) -> torch.Tensor:
+    """Packed words of the torch-mode encode (the same words as qsgd_encode with
+    a torch-mode reservation): the fused MT19937 quantize into int8 / int32 q,
+    then the planar lane pack."""
+    dev = _dev(x)
+    x = _f32(x, "qsgd_encode_torch")
+    n = x.numel()
+    lanes = lanes or qsgd_layout(n, bits, world)
+    q = torch.empty(n, dtype=torch.int8 if bits < 8 else torch.int32, device=dev)
+    if out is None:
+        out = torch.empty(lanes.plane_words, dtype=torch.int32, device=dev)
+    state_dev = _torch_state_to(dev)
+    _quantize_mt(x, norm_tensor(norm, dev), bits, q, state_dev)
+    lane_pack(q, lanes, out)
+    _torch_state_back(state_dev)
     return out
 
 

@@ -56,6 +56,10 @@ class QSGDMaxNormCompressor(_Base):
         self._dtype = _qdtype(quantization_level)
 
     def compress(self, norm, tensor):
+        # torch mode: the draws are generated on the GPU into a buffer, then
+        # quantized by the full-chip kernel.  (codec.qsgd_quantize_torch, the
+        # generator kernel consuming its own draws, gives the same q but runs
+        # slower on MI355X: DESIGN §7.)
         rng = self._reserve(tensor.numel(), 1, tensor.device)
         return self.backend.qsgd_quantize(tensor, norm, self._quantization_level, rng, 0, self._dtype)
 

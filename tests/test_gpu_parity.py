@@ -301,6 +301,46 @@ def test_mt19937_jumped_matches_serial(count, pre):
         assert bits_eq(u32(a), mt.draws(count))
 
 
+@pytest.mark.parametrize("bits", [2, 4, 8])
+@pytest.mark.parametrize("n", [1, 1000, MTJ - 3, MTJ + 1, 2 * MTJ + 7])
+@pytest.mark.parametrize("pre", [0, 5])
+def test_torch_mode_fused_quantize_matches_draw_path(bits, n, pre):
+    """Torch mode with the MT19937 draws consumed inside the generator kernel
+    (gc_qsgd_quantize_mt19937, no draw buffer) == the oracle fed with torch's
+    stream, == the draw-buffer path (torch-mode reservation + gc_qsgd_quantize),
+    and torch's CPU generator ends in the same state; the packed form
+    (qsgd_encode_torch) == qsgd_encode from the draws, at W = 1 and 8."""
+    x = torch.from_numpy(O.gen_input(n, seed=n + bits)).to(DEV)
+    x[::97] = 0.0
+    x[1::211] = -0.0
+    x[3::1009] = 1e-39   # subnormal / tiny |x|: the exact-division branch
+    x[5::2003] = -3e-42
+    norm = codec.absmax(x)
+    dtype = torch.int8 if bits < 8 else torch.int32
+
+    def fresh():
+        torch.manual_seed(7)
+        torch.bernoulli(torch.zeros(pre))  # consumes `pre` draws: the read index moves off the block start
+
+    fresh()
+    q1 = codec.qsgd_quantize_torch(x, norm, bits)
+    s1 = torch.get_rng_state()
+    fresh()
+    q2 = codec.qsgd_quantize(x, norm, bits, gcodec.Generator(0, "torch").reserve(n, 1, DEV), 0, dtype)
+    assert torch.equal(q1, q2)
+    assert torch.equal(s1, torch.get_rng_state())
+    mt = O.MT19937(7)
+    mt.draws(pre)
+    exp = O.qsgd_quantize(x.cpu().numpy(), np.float32(norm.item()), bits, O.stream_rng(mt.draws(n)))
+    assert np.array_equal(q1.cpu().numpy().astype(np.int32), exp.astype(np.int32))
+    for world in (1, 8):
+        fresh()
+        w1 = codec.qsgd_encode_torch(x, norm, bits, world)
+        fresh()
+        w2 = codec.qsgd_encode(x, norm, bits, gcodec.Generator(0, "torch").reserve(n, 1, DEV), world)
+        assert torch.equal(w1, w2)
+
+
 def test_mt19937_jumped_1e8_vs_oracle():
     """1e8 draws (382 generators) of the parallel stream == the oracle's
     serial MT19937, and the final state == the serial GPU kernel's."""
@@ -523,10 +563,13 @@ def test_grandk_torch_mode_matches_reference(case):
 
 
 # --------------------------------------------------------------------------- packers
-def test_lane_pack_unpack_kernels():
+@pytest.mark.parametrize("n", [70_001, 96, 95, 400_003])
+def test_lane_pack_unpack_kernels(n):
+    """int8 / int32 q -> planar words (k_lane_pack4; k_lane_pack16 when the
+    planes are 16-word aligned: n = 96 and 400,003 at W = 1) and back."""
     rng = np.random.default_rng(3)
     for world in (1, 2, 8):
-        n, s = 70_001, 15
+        s = 15
         q = rng.integers(-s, s + 1, n).astype(np.int32)
         ln = codec.qsgd_layout(n, 4, world)
         for dt in (torch.int8, torch.int32):

@@ -161,3 +161,32 @@ def test_reducer_fused_equals_unfused(name, kw, inplace):
     assert b0 == b1
     for a, b in zip(o0, o1):
         assert a.tobytes() == b.tobytes()
+
+
+def test_reducer_fresh_grad_out_every_step_pins_nothing():
+    """The reference trainer hands fresh p.grad tensors to the reducer every
+    step (zero_grad sets them to None).  The fused reducer must give the same
+    bits as with stable tensors, keep at most SEG_CACHE tables, and hold no
+    reference to any step's gradients (the table cache must not pin
+    old gradient generations in device memory)."""
+    import gc
+    import weakref
+
+    sizes = [27, 64, 1000, 3, 4099, 70_001]
+    ts, _ = carve(sizes, seed=91)
+    stable = [torch.empty_like(t) for t in ts]
+    ref = gcodec.QSGDMaxNormReducer(DEV, generator=gcodec.Generator(3, "philox"), quantization_level=4)
+    r = gcodec.QSGDMaxNormReducer(DEV, generator=gcodec.Generator(3, "philox"), quantization_level=4)
+    dead = []
+    for step in range(12):
+        ref.reduce(ts, stable)
+        fresh = [torch.full_like(t, float(step)) for t in ts]  # new allocations every step
+        r.reduce(ts, fresh)
+        for a, b in zip(stable, fresh):
+            assert u32(a).tobytes() == u32(b).tobytes()
+        dead += [weakref.ref(t) for t in fresh]
+        del fresh, a, b
+        assert len(r._seg_cache) <= r.SEG_CACHE
+    gc.collect()
+    alive = [i for i, w in enumerate(dead) if w() is not None]
+    assert not alive, f"{len(alive)} of {len(dead)} gradient tensors still referenced: {alive[:12]}"

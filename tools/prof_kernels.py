@@ -1,7 +1,8 @@
 """Workload for rocprofv3 counter passes over the round-2 kernels: the config-3
 multi-scale kernels on the ResNet50 bucket (one-pass W = 1 encode, the two W > 1
 passes, decode), the parallel MT19937 (1e8 draws), the small-K GlobalRandK step,
-and the headline absmax + encode (1e8, 4-bit).  Each runs `REPS` times."""
+the headline absmax + encode (1e8, 4-bit) and its torch-parity form
+(MT19937 draws consumed by the generator kernel, then the lane pack).  Each runs `REPS` times."""
 import os
 import sys
 
@@ -50,5 +51,12 @@ words = torch.empty(codec.qsgd_layout(n, 4, 1).plane_words, dtype=torch.int32, d
 for _ in range(REPS):
     codec.absmax(x, out=nrm)
     codec.qsgd_encode(x, nrm, 4, gen.reserve(n), 1, out=words)
+torch.cuda.synchronize()
+torch.manual_seed(42)  # torch-parity mode: draws -> encode from the draws; and the fused form
+tgen = gcodec.Generator(0, "torch")
+for _ in range(REPS):
+    codec.qsgd_encode(x, nrm, 4, tgen.reserve(n), 1, out=words)
+for _ in range(REPS):
+    codec.qsgd_encode_torch(x, nrm, 4, 1, out=words)
 torch.cuda.synchronize()
 print("prof workload done")
