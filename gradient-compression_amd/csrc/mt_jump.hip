@@ -153,10 +153,8 @@ constexpr uint32_t kMtJumpQuads = (kMtJumpBits / 4 + kMtJumpThreads + 1 + 7) & ~
 static_assert(kMtJumpWords * kMtJumpSplit == kMtN, "coefficient split");
 static_assert((kMtJumpBits - 1) / 4 + kMtJumpThreads - 1 < kMtJumpQuads, "copy length");
 
-// workspace: partial windows [split][gens - 1][624] after window 0; word 1 is
-// the quantize modes' sink for out-of-range stores
+// workspace: partial windows [split][gens - 1][624] after window 0
 constexpr uint64_t kWsPart = kWsWin + kMtN;
-constexpr uint64_t kWsSpare = 1;
 
 __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws,
                                                            uint32_t jumps)
@@ -311,7 +309,7 @@ template <int MODE>
 __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t count,
                                                          void *__restrict__ out, uint32_t *__restrict__ state,
                                                          const float *__restrict__ x, const float *__restrict__ normp,
-                                                         float s, void *__restrict__ spare)
+                                                         float s)
 {
     __shared__ uint32_t buf[2][kMtN];
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
@@ -465,13 +463,13 @@ static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_
                            ws, (uint32_t)(gens - 1));
     if (mode == 0)
         hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out,
-                           state_dev, x, norm, s, ws + kWsSpare);
+                           state_dev, x, norm, s);
     else if (mode == 1)
         hipLaunchKernelGGL(k_mt_gen<1>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out,
-                           state_dev, x, norm, s, ws + kWsSpare);
+                           state_dev, x, norm, s);
     else
         hipLaunchKernelGGL(k_mt_gen<2>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out,
-                           state_dev, x, norm, s, ws + kWsSpare);
+                           state_dev, x, norm, s);
     return launch_status(what);
 }
 

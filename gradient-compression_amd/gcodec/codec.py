@@ -681,21 +681,40 @@ def _mt_ws(dev, st, count: int) -> torch.Tensor:
     return ws
 
 
+_MT_PIN = {}  # device index -> (pinned host state in, pinned host state out, device state): 625 int32 each
+
+
 def _torch_state_to(device) -> torch.Tensor:
+    """torch's CPU-generator state (624 words + read index) on `device`, copied
+    asynchronously from a pinned buffer: the host does not wait for the work
+    already queued on the stream (a pageable copy would)."""
     from .rng import torch_mt_state
 
     words, idx = torch_mt_state()
-    st = np.empty(625, dtype=np.uint32)
-    st[:624] = words
-    st[624] = idx
-    return torch.from_numpy(st.view(np.int32)).to(device)
+    bufs = _MT_PIN.get(device.index)
+    if bufs is None:
+        bufs = _MT_PIN[device.index] = (torch.empty(625, dtype=torch.int32).pin_memory(),
+                                        torch.empty(625, dtype=torch.int32).pin_memory(),
+                                        torch.empty(625, dtype=torch.int32, device=device))
+    hin, _, dst = bufs
+    h = hin.numpy().view(np.uint32)  # free: the previous call synchronised after its copy
+    h[:624] = words
+    h[624] = idx
+    dst.copy_(hin, non_blocking=True)
+    return dst
 
 
 def _torch_state_back(state_dev: torch.Tensor):
+    """Advance torch's CPU generator to the device state (synchronises: the
+    draws' consumers may be queued behind the copy but the state must reach
+    the host before torch's generator is used again)."""
     from .rng import set_torch_mt_state
 
-    new = state_dev.cpu().numpy().view(np.uint32)  # synchronises
-    set_torch_mt_state(new[:624], int(new[624]))
+    hout = _MT_PIN[state_dev.device.index][1]
+    hout.copy_(state_dev, non_blocking=True)
+    torch.cuda.current_stream(state_dev.device).synchronize()
+    new = hout.numpy().view(np.uint32)
+    set_torch_mt_state(new[:624].copy(), int(new[624]))
 
 
 def _quantize_mt(x, norm_t, bits, q, state_dev):
@@ -744,17 +763,12 @@ def qsgd_encode_torch(x, norm, bits, world=1, out=None, lanes=None) -> torch.Ten
 def mt19937_draws(count: int, device) -> torch.Tensor:
     """`count` draws of torch's CPU generator, produced on `device`; torch's
     generator state advances exactly as torch.bernoulli would advance it."""
-    from .rng import set_torch_mt_state, torch_mt_state
-
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-    words, idx = torch_mt_state()
-    st = np.empty(625, dtype=np.uint32)
-    st[:624] = words
-    st[624] = idx
-    st_dev = torch.from_numpy(st.view(np.int32)).to(device)
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    st_dev = _torch_state_to(device)
     out = mt19937_generate(st_dev, count)
-    new = st_dev.cpu().numpy().view(np.uint32)  # synchronises
-    set_torch_mt_state(new[:624], int(new[624]))
+    _torch_state_back(st_dev)
     return out
 
 

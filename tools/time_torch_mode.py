@@ -1,0 +1,33 @@
+"""Per-call time of the torch-parity (MT19937) encode at 1e8, 4-bit, W = 1:
+the draw-buffer path (compressor / reducer default) and the fused generator
+quantize, each over REPS back-to-back calls (includes the torch state hand-off)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gradient-compression_amd"))
+import torch  # noqa: E402
+
+import gcodec  # noqa: E402
+from gcodec import codec  # noqa: E402
+
+REPS = 10
+dev = torch.device("cuda", 0)
+n = 100_000_000
+x = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(1)).mul_(0.01)
+nm = codec.absmax(x)
+lanes = codec.qsgd_layout(n, 4, 1)
+words = torch.empty(lanes.plane_words, dtype=torch.int32, device=dev)
+gen = gcodec.Generator(0, "torch")
+torch.manual_seed(42)
+for f in ("buffer", "fused", "buffer", "fused"):
+    call = ((lambda: codec.qsgd_encode(x, nm, 4, gen.reserve(n), 1, out=words, lanes=lanes)) if f == "buffer"
+            else (lambda: codec.qsgd_encode_torch(x, nm, 4, 1, out=words, lanes=lanes)))
+    call()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(REPS):
+        call()
+    torch.cuda.synchronize()
+    print(f"{f}: {(time.perf_counter() - t0) / REPS * 1e3:.3f} ms per call")
