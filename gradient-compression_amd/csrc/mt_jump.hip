@@ -9,6 +9,8 @@
 // the last generator's final window IS torch's state array), with the caller's
 // read index.  Its window comes from the jump-ahead of mt_poly.cpp:
 //     x_{gJ-1+j} = XOR_{k : a_k = 1} x_{k+j},   a = x^(gJ-1) mod P,  j = 1..624
+// J is GC_MT_JUMP_DRAWS, or any multiple of 624 through the _j entry points
+// (the package picks one per count so that the generators spread over the CUs).
 // Three launches, all on the caller's stream, no host synchronisation:
 //   k_mt_seq    one workgroup: the first 20561 raw words x_0.. of the stream
 //               (32 twists of the state) into the workspace; window 0 = the
@@ -34,11 +36,9 @@ namespace gc {
 
 constexpr uint32_t kMtN = 624;
 constexpr uint32_t kMtM = 397;
-constexpr uint32_t kMtJ = GC_MT_JUMP_DRAWS;
 constexpr uint32_t kMtSeq = 19937 + kMtN;              // x_0 .. x_20560 (k + j <= 19936 + 624)
 constexpr uint32_t kMtSeqWs = 33 * kMtN;              // 33 twist blocks cover kMtSeq
 
-static_assert(kMtJ % kMtN == 0, "generator windows stay aligned to the twist blocks");
 static_assert(kMtSeqWs >= kMtSeq, "sequence blocks");
 
 // workspace (uint32): [0] read index, [64 ..) sequence, window 0, then the
@@ -306,7 +306,8 @@ static_assert(kMtPre == 4 && kMtRounds == 3, "mt_wait_row's count");
 __device__ __forceinline__ void mt_wait_row() { asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); }
 
 template <int MODE>
-__global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t count,
+__global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t J,
+                                                         uint64_t count,
                                                          void *__restrict__ out, uint32_t *__restrict__ state,
                                                          const float *__restrict__ x, const float *__restrict__ normp,
                                                          float s)
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
         }
     const uint32_t ptr0 = ws[0];
     __syncthreads();
-    const uint64_t pos0 = g * kMtJ, end = min(pos0 + kMtJ, count);
+    const uint64_t pos0 = g * J, end = min(pos0 + J, count);  // J % 624 == 0: windows stay block-aligned
     const uint32_t head = ptr0 < kMtN ? (uint32_t)min((uint64_t)(kMtN - ptr0), end - pos0) : 0u;  // rest of block 0
     const uint64_t rest = end - pos0 - head;
     const uint32_t twists = (uint32_t)((rest + kMtN - 1) / kMtN);
@@ -435,22 +436,25 @@ using namespace gc;
 
 extern "C" {
 
-size_t gc_mt19937_workspace_size(uint64_t count)
+size_t gc_mt19937_workspace_size_j(uint64_t count, uint64_t J)
 {
-    const uint64_t gens = count ? (count + kMtJ - 1) / kMtJ : 1;
+    const uint64_t gens = count && J ? (count + J - 1) / J : 1;
     return 4 * (kWsPart + kMtJumpSplit * (gens - 1) * kMtN);
 }
 
-// seq -> jump -> gen<MODE> for `count` draws of state_dev
+size_t gc_mt19937_workspace_size(uint64_t count) { return gc_mt19937_workspace_size_j(count, GC_MT_JUMP_DRAWS); }
+
+// seq -> jump -> gen<MODE> for `count` draws of state_dev, generators of J draws
 static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens,
-                  void *out, uint64_t count, void *workspace, gc_stream_t stream, const float *x, const float *norm,
-                  float s)
+                  uint64_t J, void *out, uint64_t count, void *workspace, gc_stream_t stream, const float *x,
+                  const float *norm, float s)
 {
     GC_REQUIRE(state_dev && workspace, "%s: null state/workspace", what);
     GC_REQUIRE(count == 0 || out, "%s: null out", what);
+    GC_REQUIRE(J > 0 && J % kMtN == 0, "%s: J = %llu is not a positive multiple of 624", what, (unsigned long long)J);
     if (count == 0)
         return GC_OK;
-    const uint64_t gens = (count + kMtJ - 1) / kMtJ;
+    const uint64_t gens = (count + J - 1) / J;
     GC_REQUIRE(gens - 1 <= table_gens && (gens == 1 || table_dev),
                "%s: jump table holds %llu generators, %llu draws need %llu", what, (unsigned long long)table_gens,
                (unsigned long long)count, (unsigned long long)(gens - 1));
@@ -462,33 +466,40 @@ static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_
         hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)((gens - 1) * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st, table_dev,
                            ws, (uint32_t)(gens - 1));
     if (mode == 0)
-        hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out,
+        hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, J, count, out,
                            state_dev, x, norm, s);
     else if (mode == 1)
-        hipLaunchKernelGGL(k_mt_gen<1>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out,
+        hipLaunchKernelGGL(k_mt_gen<1>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, J, count, out,
                            state_dev, x, norm, s);
     else
-        hipLaunchKernelGGL(k_mt_gen<2>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, count, out,
+        hipLaunchKernelGGL(k_mt_gen<2>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, J, count, out,
                            state_dev, x, norm, s);
     return launch_status(what);
+}
+
+int gc_mt19937_generate_jumped_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                 uint32_t *out, uint64_t count, void *workspace, gc_stream_t stream)
+{
+    return mt_run("gc_mt19937_generate_jumped", 0, state_dev, table_dev, table_gens, J, out, count, workspace, stream,
+                  nullptr, nullptr, 0.0f);
 }
 
 int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,
                                uint64_t count, void *workspace, gc_stream_t stream)
 {
-    return mt_run("gc_mt19937_generate_jumped", 0, state_dev, table_dev, table_gens, out, count, workspace, stream,
-                  nullptr, nullptr, 0.0f);
+    return gc_mt19937_generate_jumped_j(state_dev, table_dev, table_gens, GC_MT_JUMP_DRAWS, out, count, workspace,
+                                        stream);
 }
 
 int gc_qsgd_quantize_mt19937(const float *x, uint64_t n, const float *norm, uint32_t bits, uint32_t *state_dev,
-                             const uint32_t *table_dev, uint64_t table_gens, void *q, uint32_t q_dtype,
+                             const uint32_t *table_dev, uint64_t table_gens, uint64_t J, void *q, uint32_t q_dtype,
                              void *workspace, gc_stream_t stream)
 {
     GC_REQUIRE(bits >= 1 && bits <= 8, "gc_qsgd_quantize_mt19937: bits must be 1..8");
     GC_REQUIRE(q_dtype == GC_I32 || (q_dtype == GC_I8 && bits <= 7),
                "gc_qsgd_quantize_mt19937: q_dtype must be GC_I8 (bits <= 7) or GC_I32");
     GC_REQUIRE(n == 0 || (x && norm), "gc_qsgd_quantize_mt19937: null x/norm");
-    return mt_run("gc_qsgd_quantize_mt19937", q_dtype == GC_I8 ? 1 : 2, state_dev, table_dev, table_gens, q, n,
+    return mt_run("gc_qsgd_quantize_mt19937", q_dtype == GC_I8 ? 1 : 2, state_dev, table_dev, table_gens, J, q, n,
                   workspace, stream, x, norm, (float)((1u << bits) - 1u));
 }
 

@@ -298,10 +298,13 @@ int fail(int code, const char *fmt, ...);
 
 extern "C" {
 
-int gc_mt19937_jump_table(uint64_t first, uint64_t count, uint32_t *table)
+int gc_mt19937_jump_table_j(uint64_t J, uint64_t first, uint64_t count, uint32_t *table)
 {
     if (count && !table)
         return gc::fail(GC_EINVAL, "gc_mt19937_jump_table: null table");
+    if (J == 0 || J % 624 != 0)
+        return gc::fail(GC_EINVAL, "gc_mt19937_jump_table: J = %llu is not a positive multiple of 624",
+                        (unsigned long long)J);
     if (first < 1)
         return gc::fail(GC_EINVAL, "gc_mt19937_jump_table: generators start at 1 (generator 0 is the state itself)");
     if (!count)
@@ -309,7 +312,6 @@ int gc_mt19937_jump_table(uint64_t first, uint64_t count, uint32_t *table)
     const Field &F = field();
     if (F.P.empty())
         return gc::fail(GC_EINVAL, "gc_mt19937_jump_table: characteristic polynomial not found");
-    const uint64_t J = GC_MT_JUMP_DRAWS;
     uint64_t cur[NW], RJ[NW], nxt[NW];
     xpow(F, first * J - 1, cur);
     if (count > 1)
@@ -322,6 +324,11 @@ int gc_mt19937_jump_table(uint64_t first, uint64_t count, uint32_t *table)
         }
     }
     return GC_OK;
+}
+
+int gc_mt19937_jump_table(uint64_t first, uint64_t count, uint32_t *table)
+{
+    return gc_mt19937_jump_table_j(GC_MT_JUMP_DRAWS, first, count, table);
 }
 
 }  // extern "C"

@@ -629,31 +629,46 @@ def mt19937_seed_state(seed: int) -> np.ndarray:
     return st
 
 
-_MT_TABLE = {}  # device index -> (int32 tensor [gens * 624], gens): jump coefficients of generators 1..gens
+_MT_TABLE = {}  # (device index, J) -> (int32 tensor [gens * 624], gens): jump coefficients of generators 1..gens
 _MT_WS = {}     # (device index, stream) -> workspace tensor
+MT_MAX_GENERATORS = 1024
 
 
-def _mt_jump_table(dev, gens: int):
-    """Device jump table covering generators 1..gens (host-computed once per
-    process and grown geometrically; it depends only on the generator index)."""
-    cur = _MT_TABLE.get(dev.index)
+def mt_generator_draws(count: int) -> int:
+    """Draws per parallel generator J for `count` draws.  The jump costs about
+    0.37 us of chip time per generator and a generator about 0.34 us per
+    624-draw block (latency-bound: measured with 382 and 256 generators), so
+    G = sqrt(count * 0.34 / (624 * 0.37)) generators balance the two kernels
+    (DESIGN §7); J is a multiple of 624.  1e8 draws: G = 383, J = 261,456."""
+    g = int(min(MT_MAX_GENERATORS, max(1, round((count * 1.47e-3) ** 0.5))))
+    return 624 * max(1, -(-count // (624 * g)))
+
+
+def _mt_jump_table(dev, gens: int, J: int = _lib.GC_MT_JUMP_DRAWS):
+    """Device jump table covering generators 1..gens for generators of J draws
+    (host-computed once per process and J, grown geometrically; it depends
+    only on J and the generator index, not on the seed)."""
+    key = (dev.index, J)
+    cur = _MT_TABLE.get(key)
     have = cur[1] if cur is not None else 0
     if have >= gens:
         return cur
     total = max(gens, 2 * have, 16)
     host = np.empty((total - have) * 624, dtype=np.uint32)
-    check(_lib.load().gc_mt19937_jump_table(have + 1, total - have, host.ctypes.data_as(C.c_void_p)),
+    check(_lib.load().gc_mt19937_jump_table_j(J, have + 1, total - have, host.ctypes.data_as(C.c_void_p)),
           "gc_mt19937_jump_table")
     part = torch.from_numpy(host.view(np.int32)).to(dev)
     table = part if cur is None else torch.cat([cur[0], part])
-    _MT_TABLE[dev.index] = (table, total)
-    return _MT_TABLE[dev.index]
+    _MT_TABLE[key] = (table, total)
+    return _MT_TABLE[key]
 
 
-def mt19937_generate(state_dev: torch.Tensor, count: int, out=None, parallel: bool = True) -> torch.Tensor:
+def mt19937_generate(state_dev: torch.Tensor, count: int, out=None, parallel: bool = True,
+                     J: int | None = None) -> torch.Tensor:
     """The next `count` draws of the MT19937 state on the device (625 words:
     state + read index), which advances.  parallel: the jumped multi-generator
-    kernels (gc_mt19937_generate_jumped); else one workgroup walks the stream."""
+    kernels (gc_mt19937_generate_jumped_j) with generators of J draws (default:
+    mt_generator_draws(count)); else one workgroup walks the stream."""
     dev = _dev(state_dev)
     if out is None:
         out = torch.empty(count, dtype=torch.int32, device=dev)
@@ -664,16 +679,17 @@ def mt19937_generate(state_dev: torch.Tensor, count: int, out=None, parallel: bo
         return out
     if count == 0:
         return out
-    gens = -(-count // _lib.GC_MT_JUMP_DRAWS)
-    table, tgens = _mt_jump_table(dev, gens - 1) if gens > 1 else (None, 0)
-    ws = _mt_ws(dev, st, count)
-    check(lib.gc_mt19937_generate_jumped(_p(state_dev), _p(table), tgens, _p(out), count, _p(ws), st),
+    J = J or mt_generator_draws(count)
+    gens = -(-count // J)
+    table, tgens = _mt_jump_table(dev, gens - 1, J) if gens > 1 else (None, 0)
+    ws = _mt_ws(dev, st, count, J)
+    check(lib.gc_mt19937_generate_jumped_j(_p(state_dev), _p(table), tgens, J, _p(out), count, _p(ws), st),
           "gc_mt19937_generate_jumped")
     return out
 
 
-def _mt_ws(dev, st, count: int) -> torch.Tensor:
-    need = int(_lib.load().gc_mt19937_workspace_size(count))
+def _mt_ws(dev, st, count: int, J: int) -> torch.Tensor:
+    need = int(_lib.load().gc_mt19937_workspace_size_j(count, J))
     key = (dev.index, st.value)
     ws = _MT_WS.get(key)
     if ws is None or ws.numel() < need:
@@ -721,10 +737,11 @@ def _quantize_mt(x, norm_t, bits, q, state_dev):
     dev = _dev(x)
     n = x.numel()
     st = _stream(dev)
-    gens = -(-n // _lib.GC_MT_JUMP_DRAWS) if n else 1
-    table, tgens = _mt_jump_table(dev, gens - 1) if gens > 1 else (None, 0)
-    check(_lib.load().gc_qsgd_quantize_mt19937(_p(x), n, _p(norm_t), bits, _p(state_dev), _p(table), tgens, _p(q),
-                                               DTYPE_CODE[q.dtype], _p(_mt_ws(dev, st, n)), st),
+    J = mt_generator_draws(max(n, 1))
+    gens = -(-n // J) if n else 1
+    table, tgens = _mt_jump_table(dev, gens - 1, J) if gens > 1 else (None, 0)
+    check(_lib.load().gc_qsgd_quantize_mt19937(_p(x), n, _p(norm_t), bits, _p(state_dev), _p(table), tgens, J, _p(q),
+                                               DTYPE_CODE[q.dtype], _p(_mt_ws(dev, st, n, J)), st),
           "gc_qsgd_quantize_mt19937")
 
 

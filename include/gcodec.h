@@ -316,14 +316,23 @@ int gc_mt19937_jump_table(uint64_t first, uint64_t count, uint32_t *table_host);
 size_t gc_mt19937_workspace_size(uint64_t count);
 int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,
                                uint64_t count, void *workspace, gc_stream_t stream);
+/* the same with generators of J draws (J a positive multiple of 624): the
+ * table must then come from gc_mt19937_jump_table_j with the same J, and the
+ * workspace is gc_mt19937_workspace_size_j(count, J) bytes.  A J near
+ * count / (number of CUs) balances the generator kernel over the chip. */
+int gc_mt19937_jump_table_j(uint64_t J, uint64_t first, uint64_t count, uint32_t *table_host);
+size_t gc_mt19937_workspace_size_j(uint64_t count, uint64_t J);
+int gc_mt19937_generate_jumped_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                 uint32_t *out, uint64_t count, void *workspace, gc_stream_t stream);
 /* torch-mode QSGD quantize with the MT19937 draws consumed in-kernel (never
  * stored): q[i] = sign(x_i)*xi_i exactly as compressors.py:299-316 computes it
  * under torch.bernoulli (one draw per element, in order), as GC_I8 (bits <= 7)
  * or GC_I32 (the reference's _dtype, compressors.py:294-297).  state_dev
- * advances by n draws, like gc_mt19937_generate_jumped; same table and
- * workspace (gc_mt19937_workspace_size(n)).  Pack with gc_lane_pack. */
+ * advances by n draws, like gc_mt19937_generate_jumped_j with the same J,
+ * table and workspace (gc_mt19937_workspace_size_j(n, J)).  Pack with
+ * gc_lane_pack. */
 int gc_qsgd_quantize_mt19937(const float *x, uint64_t n, const float *norm, uint32_t bits, uint32_t *state_dev,
-                             const uint32_t *table_dev, uint64_t table_gens, void *q, uint32_t q_dtype,
+                             const uint32_t *table_dev, uint64_t table_gens, uint64_t J, void *q, uint32_t q_dtype,
                              void *workspace, gc_stream_t stream);
 
 /* ---- reference-compatible packers ----------------------------------------- */

@@ -280,22 +280,25 @@ def test_mt19937_kernel_matches_oracle():
 MTJ = gcodec._lib.GC_MT_JUMP_DRAWS
 
 
-@pytest.mark.parametrize("count", [1, 1000, MTJ - 1, MTJ, MTJ + 1, 3 * MTJ + 5])
+@pytest.mark.parametrize("J", [MTJ, 1872])
+@pytest.mark.parametrize("mult", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("pre", [0, 1, 300])
-def test_mt19937_jumped_matches_serial(count, pre):
+def test_mt19937_jumped_matches_serial(J, mult, pre):
     """The parallel (jump-ahead) MT19937 stream == the serial one: every draw
     and the advanced state (state array + read index) bit for bit, from read
-    indices 624 (fresh seed), 1 and 300; generator boundaries at J - 1, J, J + 1."""
+    indices 624 (fresh seed), 1 and 300; generator boundaries at J - 1, J,
+    J + 1 for the default generator length and a short one (J = 3 x 624)."""
+    count = [1, 1000, J - 1, J, J + 1, 3 * J + 5][mult]
     st = codec.mt19937_seed_state(42)
     sd = torch.from_numpy(st.view(np.int32)).to(DEV)
     if pre:
         codec.mt19937_generate(sd, pre, parallel=False)
     s2 = sd.clone()
-    a = codec.mt19937_generate(sd, count)
+    a = codec.mt19937_generate(sd, count, J=J)
     b = codec.mt19937_generate(s2, count, parallel=False)
     assert torch.equal(a, b)
     assert torch.equal(sd, s2)
-    if count <= 3 * MTJ + 5:
+    if count <= 3 * J + 5:
         mt = O.MT19937(42)
         mt.draws(pre)
         assert bits_eq(u32(a), mt.draws(count))

@@ -42,9 +42,13 @@ def temper(y):
     return y ^ (y >> np.uint32(18))
 
 
-def jump_table(first, count):
+def jump_table(first, count, j=None):
     out = np.empty(count * 624, dtype=np.uint32)
-    _lib.check(_lib.load().gc_mt19937_jump_table(first, count, out.ctypes.data_as(C.c_void_p)), "jump_table")
+    lib = _lib.load()
+    if j is None:
+        _lib.check(lib.gc_mt19937_jump_table(first, count, out.ctypes.data_as(C.c_void_p)), "jump_table")
+    else:
+        _lib.check(lib.gc_mt19937_jump_table_j(j, first, count, out.ctypes.data_as(C.c_void_p)), "jump_table")
     return out.reshape(count, 624)
 
 
@@ -77,3 +81,31 @@ def test_jump_table_offsets_agree():
     assert np.array_equal(jump_table(2, 2), a[1:])
     assert np.array_equal(jump_table(3, 1), a[2:])
     assert np.any(a[0] != a[1])
+
+
+@pytest.mark.parametrize("j", [624, 1872, 624 * 627])
+def test_jump_windows_any_generator_length(j):
+    """gc_mt19937_jump_table_j: generators of any multiple of 624 draws (the
+    package picks J per count)"""
+    st = codec.mt19937_seed_state(11)
+    tab = jump_table(1, 3, j)
+    x = raw_stream(st, 3 * j + 2 * N)
+    for g in (1, 2, 3):
+        assert np.array_equal(window_from_table(x, tab[g - 1]), x[g * j:g * j + 624]), g
+    assert np.array_equal(jump_table(1, 2, J), jump_table(1, 2))
+
+
+def test_jump_table_rejects_bad_lengths():
+    out = np.empty(624, dtype=np.uint32)
+    lib = _lib.load()
+    for j in (0, 625, 1000):
+        assert lib.gc_mt19937_jump_table_j(j, 1, 1, out.ctypes.data_as(C.c_void_p)) != 0
+
+
+def test_generator_length_choice():
+    """J: a multiple of 624, generators bounded, balanced near sqrt(count)"""
+    for n in (1, 1000, 10 ** 6, 10 ** 7, 10 ** 8, 10 ** 9):
+        j = codec.mt_generator_draws(n)
+        assert j % 624 == 0 and j > 0
+        assert -(-n // j) <= codec.MT_MAX_GENERATORS
+    assert -(-10 ** 8 // codec.mt_generator_draws(10 ** 8)) == 383

@@ -7,6 +7,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gradient-compression_amd"))
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import gcodec  # noqa: E402
@@ -31,3 +32,17 @@ for f in ("buffer", "fused", "buffer", "fused"):
         call()
     torch.cuda.synchronize()
     print(f"{f}: {(time.perf_counter() - t0) / REPS * 1e3:.3f} ms per call")
+
+# generator length: the package's per-count J against the fixed default
+st = torch.from_numpy(codec.mt19937_seed_state(7).view(np.int32)).to(dev)
+for cnt in (10_000_000, 23_520_842 * 2, 100_000_000):
+    out = torch.empty(cnt, dtype=torch.int32, device=dev)
+    for J in (gcodec._lib.GC_MT_JUMP_DRAWS, codec.mt_generator_draws(cnt)):
+        codec.mt19937_generate(st, cnt, out=out, J=J)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(REPS):
+            codec.mt19937_generate(st, cnt, out=out, J=J)
+        torch.cuda.synchronize()
+        print(f"mt19937 {cnt} draws, J = {J} ({-(-cnt // J)} generators): "
+              f"{(time.perf_counter() - t0) / REPS * 1e3:.3f} ms")
