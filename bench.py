@@ -367,12 +367,38 @@ def main():
         norm_step()
         encode_step()
 
+    norms = (norm, torch.empty_like(norm))
+
+    def run_steps(k):
+        """k whole steps.  N > 1: software-pipelined over consecutive buckets, as
+        a bucketed DDP backward issues them: bucket t's max-norm and its async
+        all_reduce(MAX) are enqueued before bucket t-1's encode, so the RCCL
+        latency of the 4-byte MAX runs beside an encode instead of between the
+        two kernels.  Every bucket still runs absmax -> MAX -> encode with its own
+        global norm (two norm buffers; the encode waits on its bucket's MAX work
+        only).  The last bucket's encode is issued before returning, so k steps
+        are complete when the caller synchronises."""
+        if world == 1 or k == 0:
+            for _ in range(k):
+                step()
+            return
+        pend = None
+        for t in range(k):
+            nb = norms[t & 1]
+            codec.absmax(x, out=nb)
+            work = dist.all_reduce(nb, op=dist.ReduceOp.MAX, async_op=True)
+            if pend is not None:
+                pend[1].wait()  # the current stream waits on bucket t-1's MAX (no host block on RCCL)
+                codec.qsgd_encode(x, pend[0], bits, gen.reserve(n), world, out=words, lanes=lanes)
+            pend = (nb, work)
+        pend[1].wait()
+        codec.qsgd_encode(x, pend[0], bits, gen.reserve(n), world, out=words, lanes=lanes)
+
     # clock settle (untimed), then the W warmup steps
     settle_steps = 0
     t_settle = time.perf_counter()
     while args.settle > 0:
-        for _ in range(20):
-            step()
+        run_steps(20)
         settle_steps += 20
         torch.cuda.synchronize()
         done = torch.tensor([float(time.perf_counter() - t_settle >= args.settle)], device=dev)
@@ -380,15 +406,13 @@ def main():
             dist.all_reduce(done, op=dist.ReduceOp.MAX)
         if done.item() > 0:
             break
-    for _ in range(Wm):
-        step()
+    run_steps(Wm)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(K):
-        step()
+    run_steps(K)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -439,7 +463,9 @@ def main():
         "config": {"workload": f"QSGD-MN {bits}-bit encode+pack, {n} fp32 per rank, W={world} carry-free "
                                f"{lanes.bits}-bit lanes x{lanes.per_word}/word",
                    "global_batch": n * world, "parallelism": f"dp{world}",
-                   "step": "absmax -> all_reduce(MAX) if N>1 -> quantize+round+pack"},
+                   "step": "absmax -> all_reduce(MAX) if N>1 -> quantize+round+pack",
+                   "pipelining": ("bucket t's absmax + async RCCL MAX enqueued before bucket t-1's encode "
+                                  "(double-buffered norm)" if world > 1 else None)},
         "clock_settle": {"seconds": args.settle, "steps": settle_steps},
         "collectives": backend if world > 1 else None,
         "pct_hbm_peak_step": 100.0 * step_bytes * K / el / 1e9 / HBM_PEAK_GBS,

@@ -139,13 +139,15 @@ class _MultiScalePacked(_Base):
     x, 2-3 levels of <= 7 bits), the cache as one 1-2 byte cell per element;
     encode then reads the cells at the common level instead of x and the
     draws.  Without a cache encode recomputes the chosen level from the same
-    reserved draws.  Either way the words are identical.  Off by default
-    (q_cache=False): on MI355X both splits cost the same, because the two
-    kernels are bound by the Philox draws, not by reading x twice (config 3:
-    mask 25 + select 38 us vs 46 + 16 us with the cache, 112 us per step
-    either way; profiles/r01s_bench_cache.log, r01s_lab_ms.log)."""
+    reserved draws.  Either way the words are identical.  q_cache=None (the
+    default) picks by world size: at W = 1 the reducers run the one-pass
+    encode (encode_w1, no cache needed); at W > 1 the cache pays, because the
+    select then runs no Philox at all (ResNet50 bucket, MI355X r02y: mask 41.2
+    + select 15.3 us with the cache against 25.7 + 38.5 us without; both
+    kernels are VALU-issue bound).  True / False force
+    it on / off."""
 
-    def __init__(self, device, generator=None, q_cache=False):
+    def __init__(self, device, generator=None, q_cache=None):
         super().__init__(device, generator)
         self.q_cache = q_cache
         self._rng = None
@@ -155,9 +157,10 @@ class _MultiScalePacked(_Base):
     def _packed_levels(self):
         raise NotImplementedError
 
-    def _cache_buffer(self, tensor, n, idx, levels):
+    def _cache_buffer(self, tensor, n, idx, levels, world):
         nbytes = getattr(self.backend, "ms_cache_bytes", None)
-        if not self.q_cache or nbytes is None or idx is not None or tensor.data_ptr() % 16:
+        use = self.q_cache if self.q_cache is not None else world > 1
+        if not use or nbytes is None or idx is not None or tensor.data_ptr() % 16:
             return None
         nb = nbytes(n, levels)
         if not nb:
@@ -171,7 +174,7 @@ class _MultiScalePacked(_Base):
         n = idx.numel() if idx is not None else tensor.numel()
         self._rng = self._reserve(n, len(levels), tensor.device)
         self._cache_key = None
-        cache = self._cache_buffer(tensor, n, idx, levels)
+        cache = self._cache_buffer(tensor, n, idx, levels, world)
         if cache is None:
             return self.backend.ms_mask_encode(tensor, norm, levels, self._rng, world, idx)
         self._cache_key = (tensor.data_ptr(), n)
@@ -204,7 +207,7 @@ class QSGDMaxNormTwoScaleCompressor(_MultiScalePacked):
     compress_higher [n, 2n) of one reservation (level 0 / level 1)."""
 
     def __init__(self, device, lower_quantization_level=6, higher_quantization_level=10, generator=None,
-                 q_cache=False):
+                 q_cache=None):
         super().__init__(device, generator, q_cache)
         self._lower_quantization_level = lower_quantization_level
         self._higher_quantization_level = higher_quantization_level
@@ -250,7 +253,7 @@ class QSGDMaxNormMultiScaleCompressor(_MultiScalePacked):
     Packed forms: optionally the cache as 1-2 byte cells where the levels
     allow it (_MultiScalePacked, q_cache=True)."""
 
-    def __init__(self, device, quantization_levels=None, generator=None, q_cache=False):
+    def __init__(self, device, quantization_levels=None, generator=None, q_cache=None):
         super().__init__(device, generator, q_cache)
         if not quantization_levels:
             quantization_levels = [6, 10]

@@ -121,15 +121,27 @@ def qsgd_hook(state: QSGDHookState, bucket) -> torch.futures.Future:
 def _multiscale(state: QSGDHookState, x, n, norm) -> torch.futures.Future:
     codec, W, levels = state.codec, state.world, state.levels
     rng = state.gen.reserve(n, len(levels), device=x.device, backend=codec)
-    mask = codec.ms_mask_encode(x, norm, levels, rng, W)
-    # the mask SUM is enqueued in line (with RCCL the stream waits on it, the
-    # host does not): the select pass needs the common levels before it runs
-    if W > 1:
-        if state.topology is not None:
-            state.topology.all_reduce(mask)
-        else:
-            dist.all_reduce(mask, group=state.group)
-    words = codec.ms_select_encode(x, norm, levels, rng, mask, W)
+    w1_ok = getattr(codec, "ms_w1_ok", None)
+    if W == 1 and w1_ok is not None and w1_ok(x, levels):
+        # one pass over x (the MIN over one rank is the identity): the same
+        # words as the mask + select passes below
+        mask, words = codec.ms_encode_w1(x, norm, levels, rng)
+    else:
+        # W > 1: the mask pass also writes the packed q cache when the backend
+        # has one for these levels, and the select reads it instead of x and
+        # the draws (no Philox in the select; _MultiScalePacked's q_cache)
+        cbytes = getattr(codec, "ms_cache_bytes", None)
+        nb = cbytes(n, levels) if cbytes is not None and x.data_ptr() % 16 == 0 else 0
+        ck = {"cache": torch.empty(n * nb, dtype=torch.uint8, device=x.device)} if nb else {}
+        mask = codec.ms_mask_encode(x, norm, levels, rng, W, **ck)
+        # the mask SUM is enqueued in line (with RCCL the stream waits on it, the
+        # host does not): the select pass needs the common levels before it runs
+        if W > 1:
+            if state.topology is not None:
+                state.topology.all_reduce(mask)
+            else:
+                dist.all_reduce(mask, group=state.group)
+        words = codec.ms_select_encode(x, norm, levels, rng, mask, W, **ck)
     state.bits_sent += 32 + 32 * mask.numel() + 32 * words.numel()
 
     def _decode(f):

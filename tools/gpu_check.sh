@@ -24,5 +24,6 @@ run() {  # name, timeout, cmd...
 run smoke_$TAG 400 python -c "import __graft_entry__ as g; g.smoke()"
 run pytest_gpu_$TAG 900 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider
 run bench_$TAG 600 python bench.py
+run gloo2_$TAG 300 env GC_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 3 --cpu-seconds 0
 run profile_$TAG 1000 bash tools/profile.sh $TAG
 echo ALL DONE

@@ -67,6 +67,14 @@ def main(tag, n=100_000_000, bits=4):
             k: {"fetch_size_kib_raw": kf.get(k), "write_size_kib": kw.get(k),
                 "hbm_bytes_per_launch": None if kf.get(k) is None or kw.get(k) is None else (2 * kf[k] + kw[k]) * 1024}
             for k in sorted(set(kf) | set(kw))}}
+    else:  # keep the last per-kernel workload passes in the latest summary (tagged)
+        try:
+            with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
+                prev = json.load(fh)
+            if "prof_kernels" in prev:
+                out["prof_kernels"] = dict(prev["prof_kernels"], tag=prev["prof_kernels"].get("tag", prev.get("tag")))
+        except (OSError, ValueError):
+            pass
     for name in (f"{tag}_pmc.json", "pmc_traffic.json"):
         with open(os.path.join(ROOT, "profiles", name), "w") as fh:
             json.dump(out, fh, indent=1)
