@@ -31,6 +31,10 @@ for _p in (ROOT, os.path.join(ROOT, "gradient-compression_amd")):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU issue ceiling: 256 CUs x 4 SIMD16 = one wave64 VALU instruction per cycle per CU
+# at the 2.4 GHz peak clock (measured 0.85-1.07 per cycle per CU for the encode's
+# instruction mix, tools/valu_rates.hip, profiles/r01m_valu_rates.log)
+VALU_PEAK_WAVE_INSTR_S = 256 * 2.4e9
 
 
 def _args():
@@ -75,6 +79,19 @@ def _traffic(kernel: str, n: int, bits: int):
     except Exception:
         pass
     return None, None
+
+
+def _valu_insts(kernel: str):
+    """VALU wave-instructions per launch of `kernel` from the committed SQ
+    counter pass (profiles/pmc_sq.json: rocprofv3 --pmc SQ_INSTS_VALU over
+    tools/prof_kernels.py, whose config-3 legs are the TS (2,4) ResNet50 bucket
+    at W = 1) -> (count, source) or (None, None)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_sq.json")) as f:
+            d = json.load(f)
+        return d["kernels"][kernel]["SQ_INSTS_VALU"], f"profiles/pmc_sq.json (rocprofv3 --pmc, tag {d.get('tag')})"
+    except Exception:
+        return None, None
 
 
 def cpu_baseline(n: int, bits: int, budget_s: float):
@@ -192,13 +209,24 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
             "decode": (_events(torch, lambda: ms.decode(nrm, w_, m_, n3, world, 1.0 / world, out=d_), reps),
                        4 * n3 + 4 * mwords + 4 * ql.plane_words),
         }
+        kernels = {k: {"us": ms_ * 1e3, "gbs": b / (ms_ * 1e-3) / 1e9,
+                       "frac_hbm_peak": b / (ms_ * 1e-3) / 1e9 / HBM_PEAK_GBS} for k, (ms_, b) in kt.items()}
+        if tag == "twoscale_2_4" and world == 1:
+            # the multi-scale kernels issue Philox + rounding work, not bytes: their
+            # roofline is VALU issue (the SQ pass ran this same workload)
+            for k, sq in (("mask_select_one_pass", "k_ms_fused_w1"), ("mask_encode", "k_ms_mask_fast"),
+                          ("select_encode", "k_ms_select_fast"), ("decode", "k_ms_decode_fast")):
+                ins, src = _valu_insts(sq)
+                if k in kernels and ins:
+                    kernels[k]["valu"] = {"kernel": sq, "wave_instr_per_launch": ins, "source": src,
+                                          "per_element": 64 * ins / n3,
+                                          "frac_valu_issue_peak": ins / (kernels[k]["us"] * 1e-6) / VALU_PEAK_WAVE_INSTR_S}
         res[f"config3_{tag}"] = {
             "n": n3, "ms_per_step": t, "grad_floats_per_s": world * n3 / (t * 1e-3), "q_cache": cached,
             "step": ("absmax, mask+select encode in one pass (W = 1), decode" if one_pass else
                      "absmax, MAX, mask encode, SUM(mask lanes), select encode, SUM(words), decode"),
             "two_pass_kernels": "mask_encode / select_encode are the W > 1 passes, timed for reference",
-            "kernels": {k: {"us": ms_ * 1e3, "gbs": b / (ms_ * 1e-3) / 1e9,
-                            "frac_hbm_peak": b / (ms_ * 1e-3) / 1e9 / HBM_PEAK_GBS} for k, (ms_, b) in kt.items()}}
+            "kernels": kernels}
         del m_, w_, d_
     del x3
 

@@ -166,6 +166,12 @@ __device__ __forceinline__ uint32_t lane_of_t(float x, int32_t T, int32_t qmax)
     const int32_t nq = __mul24(T >> 24, med3_i32(__float_as_int(x), -1, 1));  // -q
     return (uint32_t)(qmax - min(max(nq, -qmax), qmax));
 }
+// the same without the clamp, where |q| <= qmax is known: the W = 1 fused
+// fast path (|x| <= norm, and the element's own level has xi <= maxv = qmax)
+__device__ __forceinline__ uint32_t lane_of_t_nc(float x, int32_t T, int32_t qmax)
+{
+    return (uint32_t)(qmax - __mul24(T >> 24, med3_i32(__float_as_int(x), -1, 1)));
+}
 __device__ __forceinline__ uint32_t lane_of_q(int32_t q, int32_t qmax)
 {
     return (uint32_t)(min(max(q, -qmax), qmax) + qmax);
@@ -685,8 +691,8 @@ __device__ __forceinline__ void fused_plane(const float4 &v, uint32_t n, uint32_
             t2 = m.z == 0u ? ms_t(b.x, r.z) : t2;
             t3 = m.w == 0u ? ms_t(b.y, r.w) : t3;
         }
-        ln = make_uint4(lane_of_t(v.x, t0, qmax), lane_of_t(v.y, t1, qmax), lane_of_t(v.z, t2, qmax),
-                        lane_of_t(v.w, t3, qmax));
+        ln = make_uint4(lane_of_t_nc(v.x, t0, qmax), lane_of_t_nc(v.y, t1, qmax), lane_of_t_nc(v.z, t2, qmax),
+                        lane_of_t_nc(v.w, t3, qmax));
     } else {
         const float4 ql = quot4_exact(v, dv);
         int32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;

@@ -83,6 +83,21 @@ def test_ddp_qsgd_hook_on_gpu(world):
         check_hook_records(recs, world)
 
 
+@pytest.mark.parametrize("levels,two_scale", [((2, 4), True), ((2, 4, 6), False)])
+@pytest.mark.parametrize("world", [1, 2])
+def test_ddp_multiscale_hook_on_gpu(world, levels, two_scale):
+    """The two-/multi-scale DDP hook on cuda:0: W = 1 runs the one-pass encode
+    (gc_ms_encode_w1), W = 2 the mask pass with the q cache, the mask SUM and
+    the select from the cache; every bucket equals the oracle's reduction."""
+    from test_ddp_hook_gloo import check_hook_records
+
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(W.ddp_hook_world, args=(world, os.path.join(td, "init"), td, True, list(levels), two_scale),
+                 nprocs=world, join=True)
+        recs = [np.load(os.path.join(td, f"h{r}.npz"), allow_pickle=False) for r in range(world)]
+        check_hook_records(recs, world, levels=list(levels), order=1 if two_scale else 0)
+
+
 @pytest.mark.parametrize("local_size", [1, 2])
 def test_hip_reducers_through_node_topology(local_size):
     """gcodec.NodeTopology (two-level collectives: intra-node reduce-scatter,

@@ -32,9 +32,9 @@ def main(tag):
                 if c in m:
                     m[c.replace("SQ_", "frac_")] = m[c] / wc
         out["kernels"][k] = m
-    path = os.path.join(ROOT, "profiles", f"{tag}_k_sq.json")
-    with open(path, "w") as fh:
-        json.dump(out, fh, indent=1)
+    for name in (f"{tag}_k_sq.json", "pmc_sq.json"):  # pmc_sq.json: the latest, read by bench.py
+        with open(os.path.join(ROOT, "profiles", name), "w") as fh:
+            json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 
 

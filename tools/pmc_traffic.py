@@ -22,12 +22,17 @@ def _rows(pattern):
 
 
 KERNELS = ("k_qsgd_encode", "k_absmax", "k_qsgd_decode", "k_ms_fused_w1", "k_ms_mask_fast", "k_ms_select_fast",
+           "k_ms_select_cache",
            "k_ms_decode_fast", "k_mt_seq", "k_mt_jump", "k_mt_gen", "k_randk_gather", "k_decode_scatter1")
 
 
 def _short(name):
     for k in KERNELS:
         if k in name:
+            if k == "k_ms_mask_fast":  # <LM, KIND, NL, VAR, CBY>: CBY > 0 also writes the q cache
+                targs = name.split("<", 1)[1].split(">", 1)[0].split(",") if "<" in name else []
+                if len(targs) >= 5 and targs[4].strip() != "0":
+                    return k + "_cache"
             return k
     return name[:60]
 

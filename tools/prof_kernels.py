@@ -1,6 +1,6 @@
 """Workload for rocprofv3 counter passes over the round-2 kernels: the config-3
 multi-scale kernels on the ResNet50 bucket (one-pass W = 1 encode, the two W > 1
-passes, decode), the parallel MT19937 (1e8 draws), the small-K GlobalRandK step,
+passes, decode; the q-cache mask and cache select at W = 2 lanes), the parallel MT19937 (1e8 draws), the small-K GlobalRandK step,
 the headline absmax + encode (1e8, 4-bit) and its torch-parity form
 (MT19937 draws consumed by the generator kernel, then the lane pack).  Each runs `REPS` times."""
 import os
@@ -28,6 +28,12 @@ for _ in range(REPS):
     m2 = ms.encode_mask(nrm, x3, 1)
     w2 = ms.encode(nrm, x3, m2, 1)
     ms.decode(nrm, w2, m2, n3, 1, 1.0)
+# the W > 1 default (q_cache): mask pass + q cache cells, then the select from
+# the cache, at W = 2 lane sizing (one rank's mask: timing only)
+msc = gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen, q_cache=True)
+for _ in range(REPS):
+    m3 = msc.encode_mask(nrm, x3, 2)
+    w3 = msc.encode(nrm, x3, m3, 2)
 torch.cuda.synchronize()
 del x3
 st = torch.from_numpy(codec.mt19937_seed_state(42).view(np.int32)).to(dev)
