@@ -45,7 +45,8 @@ def _args():
     ap.add_argument("--settle", type=float, default=0.5,
                     help="seconds of untimed steps before the W warmup steps: MI355X clocks ramp over ~0.1-0.3 s "
                          "of sustained load (profiles/r01h_*: 181 us/step after 5 steps, 163 us after 1000)")
-    ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--n", "--numel", dest="n", type=int, default=100_000_000,
+                    help="bucket elements per rank (--numel under torchrun, whose parser takes --n as ambiguous)")
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-oracle sample budget (0 = skip)")
     ap.add_argument("--no-extras", action="store_true", help="skip decode / reduce-path / parity-mode legs")
@@ -397,30 +398,38 @@ def main():
 
     norms = (norm, torch.empty_like(norm))
 
-    def run_steps(k):
-        """k whole steps.  N > 1: software-pipelined over consecutive buckets, as
-        a bucketed DDP backward issues them: bucket t's max-norm and its async
-        all_reduce(MAX) are enqueued before bucket t-1's encode, so the RCCL
-        latency of the 4-byte MAX runs beside an encode instead of between the
-        two kernels.  Every bucket still runs absmax -> MAX -> encode with its own
-        global norm (two norm buffers; the encode waits on its bucket's MAX work
-        only).  The last bucket's encode is issued before returning, so k steps
-        are complete when the caller synchronises."""
-        if world == 1 or k == 0:
+    def run_steps(k, buckets=None):
+        """k whole steps over `buckets` ((x, words, lanes) triples, cycled; the
+        headline bucket by default).  N > 1: software-pipelined over consecutive
+        buckets, as a bucketed DDP backward issues them: bucket t's max-norm and
+        its async all_reduce(MAX) are enqueued before bucket t-1's encode, so the
+        RCCL latency of the 4-byte MAX runs beside an encode instead of between
+        the two kernels.  Every bucket still runs absmax -> MAX -> encode with its
+        own global norm (two norm buffers; the encode waits on its bucket's MAX
+        work only).  The last bucket's encode is issued before returning, so k
+        steps are complete when the caller synchronises."""
+        if world == 1 and buckets is None:
             for _ in range(k):
                 step()
             return
+        bks = buckets or [(x, words, lanes)]
         pend = None
         for t in range(k):
+            xb, wb, lb = bks[t % len(bks)]
             nb = norms[t & 1]
-            codec.absmax(x, out=nb)
-            work = dist.all_reduce(nb, op=dist.ReduceOp.MAX, async_op=True)
+            codec.absmax(xb, out=nb)
+            work = dist.all_reduce(nb, op=dist.ReduceOp.MAX, async_op=True) if world > 1 else None
             if pend is not None:
-                pend[1].wait()  # the current stream waits on bucket t-1's MAX (no host block on RCCL)
-                codec.qsgd_encode(x, pend[0], bits, gen.reserve(n), world, out=words, lanes=lanes)
-            pend = (nb, work)
-        pend[1].wait()
-        codec.qsgd_encode(x, pend[0], bits, gen.reserve(n), world, out=words, lanes=lanes)
+                _encode_pending(pend)
+            pend = (xb, wb, lb, nb, work)
+        if pend is not None:
+            _encode_pending(pend)
+
+    def _encode_pending(p):
+        px, pw, pl, pn, pwork = p
+        if pwork is not None:
+            pwork.wait()  # the current stream waits on this bucket's MAX (no host block on RCCL)
+        codec.qsgd_encode(px, pn, bits, gen.reserve(px.numel()), world, out=pw, lanes=pl)
 
     # clock settle (untimed), then the W warmup steps
     settle_steps = 0
@@ -451,6 +460,25 @@ def main():
         el = t.item()
     ms_step = el / K * 1e3
     value = world * n * K / el
+
+    # the pipelined issue order against the plain one on two different buckets
+    # (two slices of x with different norms, same draws): the packed words must
+    # be bit-identical, so no bucket ever encodes with another bucket's norm
+    m = max(1, min(n // 2, 1 << 22))
+    lm = codec.qsgd_layout(m, bits, world)
+    xa, xb = x[:m], x[m:2 * m]
+    wp = [torch.empty(lm.plane_words, dtype=torch.int32, device=dev) for _ in range(4)]
+    off = gen.offset
+    run_steps(3, [(xa, wp[0], lm), (xb, wp[1], lm)])  # a, b, a: wp[0] ends with the third bucket
+    gen.offset = off
+    for xs, ws in ((xa, wp[2]), (xb, wp[3]), (xa, wp[2])):
+        codec.absmax(xs, out=norm)
+        if world > 1:
+            dist.all_reduce(norm, op=dist.ReduceOp.MAX)
+        codec.qsgd_encode(xs, norm, bits, gen.reserve(m), world, out=ws, lanes=lm)
+    torch.cuda.synchronize()
+    pipe_ok = bool(torch.equal(wp[0], wp[2]) and torch.equal(wp[1], wp[3]))
+    del wp
 
     # ---- per-kernel HIP-event timing: the timed loop replayed once more with
     # events bracketing every absmax and encode launch (on the current stream,
@@ -495,6 +523,7 @@ def main():
                    "pipelining": ("bucket t's absmax + async RCCL MAX enqueued before bucket t-1's encode "
                                   "(double-buffered norm)" if world > 1 else None)},
         "clock_settle": {"seconds": args.settle, "steps": settle_steps},
+        "pipelined_issue_bit_identical": pipe_ok,
         "collectives": backend if world > 1 else None,
         "pct_hbm_peak_step": 100.0 * step_bytes * K / el / 1e9 / HBM_PEAK_GBS,
         "roofline": {"bound": "hbm", "kernel": "k_qsgd_encode", "achieved": achieved, "peak": HBM_PEAK_GBS,

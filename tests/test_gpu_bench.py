@@ -1,0 +1,53 @@
+"""bench.py's control flow on the GPU box: one rank, and two ranks over gloo
+sharing cuda:0 (the N > 1 path the driver runs over RCCL on an 8-GPU node:
+the pipelined norm MAX, the collectives of every leg).  Small buckets, no
+extras: this checks the JSON contract and that the pipelined issue order
+gives the same packed words as the plain one, not performance."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--numel", "4000000", "--steps", "4", "--warmup", "1", "--settle", "0", "--cpu-seconds", "0", "--no-extras"]
+
+
+def _line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert lines, out[-2000:]
+    return json.loads(lines[-1])
+
+
+def _check(d: dict, world: int):
+    assert d["metric"] == "grad-floats/sec encode+pack (device-resident), 100M fp32 bucket; % HBM peak"
+    assert d["n_gpus"] == world and d["steps"] == 4 and d["value"] > 0
+    assert d["pipelined_issue_bit_identical"] is True
+    assert d["roofline"]["bound"] == "hbm" and d["roofline"]["achieved"] > 0
+
+
+def test_bench_one_rank():
+    r = subprocess.run([sys.executable, "bench.py", *ARGS], cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    _check(_line(r.stdout), 1)
+
+
+def test_bench_two_ranks_gloo_pipelined():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, GC_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", *ARGS]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    _check(d, 2)
+    assert d["config"]["pipelining"] and d["collectives"] == "gloo"
