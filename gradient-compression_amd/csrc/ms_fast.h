@@ -214,22 +214,35 @@ __device__ __forceinline__ void cache_store(void *__restrict__ cache, uint32_t i
         p[2] = (T)c.z;
 }
 
-// the cells of elements i0..i0+3 (0 past n)
+// the cells of elements i0..i0+3 (0 past n), still packed: CBY = 1 in .x (byte
+// e = element e), CBY = 2 in .x / .y (halves).  Unpacked by cache_cells after
+// every plane's loads are issued: unpacking inside the load's branch made the
+// compiler wait on each load before issuing the next plane's.
 template <int CBY>
-__device__ __forceinline__ uint4 cache_load(const void *__restrict__ cache, uint32_t i0, uint32_t n)
+__device__ __forceinline__ uint2 cache_load(const void *__restrict__ cache, uint32_t i0, uint32_t n)
 {
     typedef typename CacheCell<CBY>::T T;
     const T *p = reinterpret_cast<const T *>(cache) + i0;
     if (i0 + 4 <= n) {
-        if constexpr (CBY == 1) {
-            const uint32_t u = *reinterpret_cast<const uint32_t *>(p);
-            return make_uint4(u & 0xffu, (u >> 8) & 0xffu, (u >> 16) & 0xffu, u >> 24);
-        } else {
-            const uint2 u = *reinterpret_cast<const uint2 *>(p);
-            return make_uint4(u.x & 0xffffu, u.x >> 16, u.y & 0xffffu, u.y >> 16);
-        }
+        if constexpr (CBY == 1)
+            return make_uint2(*reinterpret_cast<const uint32_t *>(p), 0u);
+        else
+            return *reinterpret_cast<const uint2 *>(p);
     }
-    return make_uint4(p[0], i0 + 1 < n ? p[1] : 0u, i0 + 2 < n ? p[2] : 0u, 0u);
+    const uint32_t c0 = p[0], c1 = i0 + 1 < n ? p[1] : 0u, c2 = i0 + 2 < n ? p[2] : 0u;
+    if constexpr (CBY == 1)
+        return make_uint2(c0 | (c1 << 8) | (c2 << 16), 0u);
+    else
+        return make_uint2(c0 | (c1 << 16), c2);
+}
+
+template <int CBY>
+__device__ __forceinline__ uint4 cache_cells(const uint2 &u)
+{
+    if constexpr (CBY == 1)
+        return make_uint4(u.x & 0xffu, (u.x >> 8) & 0xffu, (u.x >> 16) & 0xffu, u.x >> 24);
+    else
+        return make_uint4(u.x & 0xffffu, u.x >> 16, u.y & 0xffffu, u.y >> 16);
 }
 
 // ---------------------------------------------------------------------------
@@ -597,13 +610,14 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
         if (t < quads) {
             // every plane's cells and mask words are loaded before any is used
             // (short, latency-bound planes: no load -> use -> load chains)
-            uint4 c[PW], mw[PW][NL - 1];
+            uint2 c[PW];
+            uint4 mw[PW][NL - 1];
             uint32_t shm[PW];
 #pragma unroll
             for (int j = 0; j < PW; ++j) {
                 const uint32_t p = wave + 4u * j;
                 const uint32_t i0 = p * Mq + 4u * t;
-                c[j] = make_uint4(0u, 0u, 0u, 0u);
+                c[j] = make_uint2(0u, 0u);
                 shm[j] = 0;
 #pragma unroll
                 for (int f = 0; f < NL - 1; ++f)
@@ -621,6 +635,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
             const uint32_t msk = (1u << mk.w) - 1u;
 #pragma unroll
             for (int j = 0; j < PW; ++j) {
+                const uint4 cj = cache_cells<CBY>(c[j]);
                 uint4 m = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
                 for (int f = 0; f < NL - 1; ++f) {  // common level = #fields whose W-sum == W (mask_levels4_fast)
@@ -631,10 +646,10 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
                 }
                 const uint32_t p = wave + 4u * j;  // planes past LQ / n contribute c = 0
                 const uint32_t sh = p < (uint32_t)LQ ? p * wq : 0u;
-                acc.x += ((c[j].x >> (m.x * cb)) & cm) << sh;
-                acc.y += ((c[j].y >> (m.y * cb)) & cm) << sh;
-                acc.z += ((c[j].z >> (m.z * cb)) & cm) << sh;
-                acc.w += ((c[j].w >> (m.w * cb)) & cm) << sh;
+                acc.x += ((cj.x >> (m.x * cb)) & cm) << sh;
+                acc.y += ((cj.y >> (m.y * cb)) & cm) << sh;
+                acc.z += ((cj.z >> (m.z * cb)) & cm) << sh;
+                acc.w += ((cj.w >> (m.w * cb)) & cm) << sh;
             }
         }
         if (wave)

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void k_sel_cache_nomask(const uint8_t *__restr
                 const uint32_t i0 = p * Mq + 4u * t;
                 if (i0 >= n)
                     break;
-                const uint4 c = cache_load<1>(cache, i0, n);
+                const uint4 c = cache_cells<1>(cache_load<1>(cache, i0, n));
                 const uint32_t sh = p * wq;
                 acc.x += ((c.x >> cb) & cm) << sh;
                 acc.y += ((c.y >> cb) & cm) << sh;
