@@ -166,7 +166,9 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
                      gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen, q_cache=True)),
                     # the (4, 8) pair of the reference's logged runs; 8 bits take the
                     # generic kernels (the fast path needs every level <= 7 bits)
-                    ("twoscale_4_8", gcodec.QSGDMaxNormTwoScaleCompressor(dev, 4, 8, generator=gen))):
+                    ("twoscale_4_8", gcodec.QSGDMaxNormTwoScaleCompressor(dev, 4, 8, generator=gen)),
+                    ("twoscale_4_8_q_cache",
+                     gcodec.QSGDMaxNormTwoScaleCompressor(dev, 4, 8, generator=gen, q_cache=True))):
         nrm = torch.empty(1, device=dev)
         holder = {}
 

@@ -258,7 +258,6 @@ __device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_
                                             const RngArgs &rng, int32_t cq = 0, uint32_t cb = 0,
                                             uint4 *cv = nullptr)
 {
-    static_assert(!CACHE || (VAR & MSV_WIDE) == 0, "no q cache for wide levels");
     const float4 v = load4_nt_tail<0>(x, i0, n);
     RangeI rg;
     rg.add4(v);

@@ -329,7 +329,9 @@ static unsigned ms_grid(uint64_t quads)
 }
 
 // q cache geometry (ms_fast.h): cell bytes per element (0 = not supported:
-// outside the dense fast path, or the count fields of cb bits exceed 16 bits)
+// outside the dense wave-split kernels, or the count fields of cb bits exceed
+// 16 bits).  Levels of 8-24 bits (MSV_WIDE) cache too: the cell holds the
+// lane (q clamped to +-qmax, qmax = 2^bits[0] - 1), not the level's raw q.
 struct CacheGeom {
     uint32_t bytes, cb;
     int32_t qmax;
@@ -339,7 +341,7 @@ static CacheGeom ms_cache_geom(uint64_t n, const gc_levels *lv)
 {
     CacheGeom g{0, 0, 0};
     gc_lanes ql;
-    if (!ms_fast_ok(0, n, lv) || gc_ms_layout(n, lv, 1, &ql) != GC_OK)
+    if (!ms_fast_wide_ok(0, n, lv) || gc_ms_layout(n, lv, 1, &ql) != GC_OK)
         return g;
     const uint64_t span = 2ull * ql.offset;  // lane values 0 .. 2 qmax
     uint32_t cb = 0;
@@ -555,18 +557,22 @@ int gc_ms_mask_encode_cached(const float *x, uint64_t n, const float *norm, cons
     const MsFastArg fa = ms_fast_arg(levels);
     const uint32_t M = (uint32_t)mask_lanes->plane_words, w = mask_lanes->bits, fields = levels->count - 1;
     const unsigned g = ms_grid(M >> 2);
-#define GC_MFC(KIND_, NL_, CBY_)                                                                                      \
+    const bool wide = !ms_fast_ok(0, n, levels);
+#define GC_MFC(KIND_, NL_, VAR_, CBY_)                                                                                \
     GC_DISPATCH_L2(mask_lanes->per_word,                                                                             \
-                   hipLaunchKernelGGL((k_ms_mask_fast<LL, KIND_, NL_, 0, CBY_>), dim3(g), dim3(kBlock), 0, st, x,     \
+                   hipLaunchKernelGGL((k_ms_mask_fast<LL, KIND_, NL_, VAR_, CBY_>), dim3(g), dim3(kBlock), 0, st, x,  \
                                       (uint32_t)n, norm, la, fa, ra, M, w, fields, mask_words, cache, cg.qmax, cg.cb))
+#define GC_MFC_V(KIND_, NL_, CBY_) \
+    if (wide) { GC_MFC(KIND_, NL_, MSV_WIDE, CBY_); } else { GC_MFC(KIND_, NL_, 0, CBY_); }
 #define GC_MFC_K(NL_, CBY_) \
-    if (rng->kind == GC_RNG_PHILOX) { GC_MFC(0, NL_, CBY_); } else { GC_MFC(1, NL_, CBY_); }
+    if (rng->kind == GC_RNG_PHILOX) { GC_MFC_V(0, NL_, CBY_); } else { GC_MFC_V(1, NL_, CBY_); }
     if (levels->count == 2) {
         if (cg.bytes == 1) { GC_MFC_K(2, 1) } else { GC_MFC_K(2, 2) }
     } else {
         if (cg.bytes == 1) { GC_MFC_K(3, 1) } else { GC_MFC_K(3, 2) }
     }
 #undef GC_MFC_K
+#undef GC_MFC_V
 #undef GC_MFC
     return launch_status(what);
 }

@@ -136,7 +136,7 @@ class _MultiScalePacked(_Base):
     compress(mask), which reads the cache (compressors.py:778-817).  Here
     encode_mask writes the thermometer mask lanes and, when the backend has a
     packed form of the cache for these levels (codec.ms_cache_bytes > 0: dense
-    x, 2-3 levels of <= 7 bits), the cache as one 1-2 byte cell per element;
+    x, 2-3 levels of <= 24 bits), the cache as one 1-2 byte cell per element;
     encode then reads the cells at the common level instead of x and the
     draws.  Without a cache encode recomputes the chosen level from the same
     reserved draws.  Either way the words are identical.  q_cache=None (the

@@ -264,8 +264,8 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
 /* q cache — compressors.py:778-797 compress_cache (every level's sign*xi, kept
  * between compress_mask and compress) in packed form: one cell of
  * *bytes_per_element (1 or 2) bytes per element holding every level's select
- * lane.  0 when these levels / n have no cache form (dense fast path only: 2 or
- * 3 levels of <= 7 bits, n < 2^32, count * bit_length(2 qmax) <= 16). */
+ * lane.  0 when these levels / n have no cache form (dense wave-split kernels
+ * only: 2 or 3 levels of <= 24 bits, n < 2^32, count * bit_length(2 qmax) <= 16). */
 int gc_ms_cache_bytes(uint64_t n, const gc_levels *levels, uint32_t *bytes_per_element);
 /* gc_ms_mask_encode (dense, 16-byte aligned x) that also writes the cells into
  * cache[n * bytes_per_element] (16-byte aligned) */

@@ -486,7 +486,8 @@ def test_ms_fast_path_edges_vs_oracle(levels, world):
 
 
 @pytest.mark.parametrize("levels,cell", [((2, 4), 1), ((1, 3), 1), ((3, 7), 1), ((1, 2, 3), 2), ((2, 4, 6), 2),
-                                         ((4, 7), 2), ((3, 4, 5), 2), ((5, 6, 7), 0), ((2, 8), 0)])
+                                         ((4, 7), 2), ((3, 4, 5), 2), ((5, 6, 7), 0), ((2, 8), 1), ((4, 8), 2),
+                                         ((3, 9, 12), 2), ((2, 16), 1), ((6, 10), 2), ((9, 10), 0)])
 @pytest.mark.parametrize("world", [1, 2, 8])
 def test_ms_q_cache_vs_oracle(levels, cell, world):
     """q cache (compress_cache kept as packed cells): the cached mask kernel
