@@ -95,8 +95,12 @@ def lane_layout(n: int, value_range: int, world: int = 1, offset: int = 0) -> _l
     return ln
 
 
-def levels_struct(levels) -> _lib.gc_levels:
-    lv = sorted(int(b) for b in levels)
+def _levels_key(levels) -> tuple:
+    return tuple(sorted(int(b) for b in levels))
+
+
+@functools.lru_cache(maxsize=256)
+def _levels_struct(lv: tuple) -> _lib.gc_levels:
     if not 1 <= len(lv) <= _lib.GC_MAX_LEVELS:
         raise _lib.GCodecError(_lib.GC_EINVAL, f"1..{_lib.GC_MAX_LEVELS} levels supported")
     s = _lib.gc_levels()
@@ -106,12 +110,24 @@ def levels_struct(levels) -> _lib.gc_levels:
     return s
 
 
-def ms_layouts(n: int, levels, world: int = 1):
-    lv = levels_struct(levels)
+def levels_struct(levels) -> _lib.gc_levels:
+    """The sorted level list as a gc_levels (cached; callers treat it as read-only)."""
+    return _levels_struct(_levels_key(levels))
+
+
+@functools.lru_cache(maxsize=512)
+def _ms_layouts(n: int, lv: tuple, world: int):
+    s = _levels_struct(lv)
     ql, ml = _lib.gc_lanes(), _lib.gc_lanes()
-    check(_lib.load().gc_ms_layout(n, C.byref(lv), world, C.byref(ql)), "gc_ms_layout")
-    check(_lib.load().gc_ms_mask_layout(n, C.byref(lv), world, C.byref(ml)), "gc_ms_mask_layout")
+    check(_lib.load().gc_ms_layout(n, C.byref(s), world, C.byref(ql)), "gc_ms_layout")
+    check(_lib.load().gc_ms_mask_layout(n, C.byref(s), world, C.byref(ml)), "gc_ms_mask_layout")
     return ql, ml
+
+
+def ms_layouts(n: int, levels, world: int = 1):
+    """(q lanes, mask lanes) of a multi-scale bucket (cached like qsgd_layout:
+    two ctypes round trips per call otherwise; read-only)."""
+    return _ms_layouts(int(n), _levels_key(levels), int(world))
 
 
 def mask_words_total(ml: _lib.gc_lanes, levels) -> int:

@@ -185,13 +185,13 @@ def test_segments_plan(shift):
 
 def test_ms_cache_bytes():
     """q cache cells (gc_ms_cache_bytes, host only): count * bit_length(2 qmax)
-    bits in 1 or 2 bytes on the dense fast path (2-3 levels of <= 7 bits)."""
+    bits in 1 or 2 bytes on the dense wave-split kernels (2-3 levels of <= 24 bits)."""
     from gcodec import codec
 
     n = 23_520_842
     for levels, cell in (((2, 4), 1), ((1, 3), 1), ((3, 7), 1), ((4, 7), 2), ((6, 7), 2), ((1, 2, 3), 2),
-                         ((2, 4, 6), 2), ((3, 4, 5), 2), ((5, 6, 7), 0), ((2, 8), 0), ((6, 10), 0),
-                         ((1, 2, 3, 4), 0), ((4,), 0)):
+                         ((2, 4, 6), 2), ((3, 4, 5), 2), ((5, 6, 7), 0), ((2, 8), 1), ((6, 10), 2),
+                         ((4, 8), 2), ((2, 24), 1), ((9, 10), 0), ((1, 2, 3, 4), 0), ((4,), 0)):
         assert codec.ms_cache_bytes(n, levels) == cell, levels
     assert codec.ms_cache_bytes(1 << 32, (2, 4)) == 0  # beyond the fast path's 32-bit indices
     assert codec.ms_cache_bytes(0, (2, 4)) == 1
