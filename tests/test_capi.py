@@ -215,3 +215,27 @@ def test_product_package_never_reaches_the_oracle():
                         if pat.search(line):
                             offenders.append(f"{p}:{i}: {line.strip()}")
     assert not offenders, "\n".join(offenders)
+
+
+def test_ms_layouts_cached_and_exact():
+    """codec.ms_layouts / levels_struct are cached per (n, sorted levels, W):
+    the cached structs equal a fresh gc_ms_layout / gc_ms_mask_layout call,
+    and the key distinguishes world sizes and level order-insensitively."""
+    import ctypes as C
+
+    from gcodec import _lib, codec
+
+    lib = _lib.load()
+    for n, levels, world in ((23_520_842, (2, 4), 1), (23_520_842, (4, 2), 8), (1000, (2, 4, 6), 2)):
+        ql, ml = codec.ms_layouts(n, levels, world)
+        assert codec.ms_layouts(n, list(levels), world)[0] is ql  # cache hit, list or tuple
+        lv = _lib.gc_levels()
+        lv.count = len(levels)
+        for i, b in enumerate(sorted(levels)):
+            lv.bits[i] = b
+        q2, m2 = _lib.gc_lanes(), _lib.gc_lanes()
+        assert lib.gc_ms_layout(n, C.byref(lv), world, C.byref(q2)) == 0
+        assert lib.gc_ms_mask_layout(n, C.byref(lv), world, C.byref(m2)) == 0
+        for a, b in ((ql, q2), (ml, m2)):
+            assert bytes(a) == bytes(b)
+    assert codec.ms_layouts(1000, (2, 4), 1)[0] is not codec.ms_layouts(1000, (2, 4), 2)[0]
