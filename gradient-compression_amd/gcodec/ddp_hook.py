@@ -131,7 +131,7 @@ def _multiscale(state: QSGDHookState, x, n, norm) -> torch.futures.Future:
         # has one for these levels, and the select reads it instead of x and
         # the draws (no Philox in the select; _MultiScalePacked's q_cache)
         cbytes = getattr(codec, "ms_cache_bytes", None)
-        nb = cbytes(n, levels) if cbytes is not None and x.data_ptr() % 16 == 0 else 0
+        nb = cbytes(n, levels) if W > 1 and cbytes is not None and x.data_ptr() % 16 == 0 else 0
         ck = {"cache": torch.empty(n * nb, dtype=torch.uint8, device=x.device)} if nb else {}
         mask = codec.ms_mask_encode(x, norm, levels, rng, W, **ck)
         # the mask SUM is enqueued in line (with RCCL the stream waits on it, the
