@@ -95,6 +95,26 @@ def _valu_insts(kernel: str):
         return None, None
 
 
+def _pg_evidence(torch, dist, dev, local: int, sum_bytes: int) -> dict:
+    """What the process group itself reports at N > 1 (not the launcher's env):
+    its size and backend, the RCCL version, and every rank's (rank, local rank,
+    device, PCI bus id) gathered over the group."""
+    props = torch.cuda.get_device_properties(dev)
+    bus = "%04x:%02x:%02x" % (getattr(props, "pci_domain_id", 0), getattr(props, "pci_bus_id", 0),
+                              getattr(props, "pci_device_id", 0))
+    mine = {"rank": dist.get_rank(), "local_rank": local, "device": str(dev), "pci_bus_id": bus,
+            "name": props.name}
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, mine)
+    try:
+        ver = ".".join(str(v) for v in torch.cuda.nccl.version())
+    except Exception as e:  # noqa: BLE001 — report, never fail the bench
+        ver = f"unavailable: {type(e).__name__}"
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "rccl_version": ver,
+            "ranks": ranks, "distinct_devices": len({(r["pci_bus_id"], r["device"]) for r in ranks}),
+            "bytes_per_rccl_sum": sum_bytes}
+
+
 def cpu_baseline(n: int, bits: int, budget_s: float):
     """The CPU oracle (oracle/gcodec_oracle.c) running the reference's CPU
     algorithm on the same 100M-element bucket: max-norm, one MT19937 draw per
@@ -131,8 +151,103 @@ def cpu_baseline(n: int, bits: int, budget_s: float):
                       f"threads, the draws serial ({100 * t_mt / t_tot:.0f}% of the time)"}
 
 
+def pcie_inclusive(torch, codec, gen, x, n, bits, world, lanes, K):
+    """Host-to-host rates (never `value`): pinned host x -> H2D -> absmax +
+    encode -> D2H packed words, and H2D words -> decode -> D2H floats.
+    serial_*: one bucket at a time on one stream (latency).  *_ms: buckets
+    back to back with the copies on their own streams and double-buffered
+    device/host buffers, so bucket t's D2H runs while bucket t+1's H2D is on
+    the link (PCIe is full duplex) and the kernels hide under the copies: the
+    per-bucket cost is then the larger copy, not the sum."""
+    M = lanes.plane_words
+    dev = x.device
+    xh = torch.empty(n, dtype=torch.float32, pin_memory=True)
+    xh.copy_(x)
+    wh = [torch.empty(M, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+    dh = [torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(2)]
+    xd = [torch.empty_like(x) for _ in range(2)]
+    wd = [torch.empty(M, dtype=torch.int32, device=dev) for _ in range(2)]
+    nd = [torch.empty(1, dtype=torch.float32, device=dev) for _ in range(2)]
+    comp = torch.cuda.current_stream(dev)
+    up, down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ev = {k: [torch.cuda.Event() for _ in range(2)] for k in ("in", "kern", "out")}
+
+    def encode_bucket(t):
+        b = t & 1
+        with torch.cuda.stream(up):
+            up.wait_event(ev["kern"][b])  # the encode that last read xd[b] is done
+            xd[b].copy_(xh, non_blocking=True)
+            ev["in"][b].record(up)
+        comp.wait_event(ev["in"][b])
+        comp.wait_event(ev["out"][b])  # wd[b] has left for the host
+        codec.absmax(xd[b], out=nd[b])
+        codec.qsgd_encode(xd[b], nd[b], bits, gen.reserve(n), world, out=wd[b], lanes=lanes)
+        ev["kern"][b].record(comp)
+        with torch.cuda.stream(down):
+            down.wait_event(ev["kern"][b])
+            wh[b].copy_(wd[b], non_blocking=True)
+            ev["out"][b].record(down)
+
+    def decode_bucket(t):
+        b = t & 1
+        with torch.cuda.stream(up):
+            up.wait_event(ev["kern"][b])
+            wd[b].copy_(wh[b], non_blocking=True)
+            ev["in"][b].record(up)
+        comp.wait_event(ev["in"][b])
+        comp.wait_event(ev["out"][b])  # xd[b] (the floats) has left for the host
+        codec.qsgd_decode(wd[b], n, nd[b], bits, world, 1.0 / world, out=xd[b], lanes=lanes)
+        ev["kern"][b].record(comp)
+        with torch.cuda.stream(down):
+            down.wait_event(ev["kern"][b])
+            dh[b].copy_(xd[b], non_blocking=True)
+            ev["out"][b].record(down)
+
+    def serial_encode():
+        xd[0].copy_(xh, non_blocking=True)
+        codec.absmax(xd[0], out=nd[0])
+        codec.qsgd_encode(xd[0], nd[0], bits, gen.reserve(n), world, out=wd[0], lanes=lanes)
+        wh[0].copy_(wd[0], non_blocking=True)
+
+    def serial_decode():
+        wd[0].copy_(wh[0], non_blocking=True)
+        codec.qsgd_decode(wd[0], n, nd[0], bits, world, 1.0 / world, out=xd[0], lanes=lanes)
+        dh[0].copy_(xd[0], non_blocking=True)
+
+    def wall_ms(fn, k):
+        for e in ev.values():
+            for i in range(2):
+                e[i].record(comp)
+        fn(0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in range(1, k + 1):
+            fn(t)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / k * 1e3
+
+    pk = max(6, K // 2)
+    enc_ms = wall_ms(encode_bucket, pk)
+    dec_ms = wall_ms(decode_bucket, pk)
+    ser_e = _events(torch, serial_encode, max(3, K // 4))
+    ser_d = _events(torch, serial_decode, max(3, K // 4))
+    # the link alone: the same H2D / D2H copies with no kernels
+    h2d_ms = _events(torch, lambda: xd[0].copy_(xh, non_blocking=True), 3)
+    d2h_ms = _events(torch, lambda: dh[0].copy_(xd[0], non_blocking=True), 3)
+    res = {"encode_grad_floats_per_s": n / (enc_ms * 1e-3), "encode_ms": enc_ms,
+           "decode_grad_floats_per_s": n / (dec_ms * 1e-3), "decode_ms": dec_ms,
+           "serial_encode_ms": ser_e, "serial_decode_ms": ser_d,
+           "h2d_gbs": 4 * n / (h2d_ms * 1e-3) / 1e9, "d2h_gbs": 4 * n / (d2h_ms * 1e-3) / 1e9,
+           "note": "pinned host buffers, hipMemcpyAsync.  *_ms: buckets back to back, H2D / kernels / D2H on "
+                   "three streams with double buffers (bucket t's D2H under bucket t+1's H2D); serial_*: "
+                   "one bucket at a time on one stream"}
+    del xh, wh, dh, xd, wd
+    return res
+
+
 def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     """BASELINE.json configs 3-5 (parity cases; not the headline `value`)."""
+    from gcodec import shapes
     res = {}
     reps = max(5, K // 2)
 
@@ -234,7 +349,6 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     del x3
 
     # fused TensorBuffer / setgrad on the ResNet50 list (161 tensors)
-    from gcodec import shapes
     sizes = shapes.resnet50_sizes()
     base = torch.randn(sum(sizes) + 4 * len(sizes), device=dev, generator=g).mul_(0.01)
     grads, pos = [], 0
@@ -306,9 +420,26 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
         comp.decode(nrm4, w, K4, world, 1.0 / world, idx=idx, out=x4)
 
     t3 = sync_ms(rk_step_3, reps=max(200, reps))
+    # the reducer step itself (reducer.py:697-766) on the VGG16 tensor list: flatten
+    # (+ norm) -> device index pop -> encode -> SUM -> decode-scatter -> setgrad (x1/W
+    # of all n coordinates: the reference keeps the local gradient of the rest)
+    sizes4 = shapes.vgg16_sizes()
+    gin4 = list(torch.split(x4, sizes4))
+    gout4 = [torch.empty_like(t_) for t_ in gin4]
+    red4 = gcodec.GlobalRandKMaxNormReducer(dev, seed=42, K=K4, quantization_level=4, generator=gen)
+    t_red = sync_ms(lambda: red4.reduce(gin4, gout4), reps=max(200, reps))
+    segs_in, segs_out = codec.Segments(gin4), codec.Segments(gout4)
+    flat4 = torch.empty(n4, device=dev)
+    red_kernels = {"flatten_absmax": _events(torch, lambda: codec.segments_flatten_absmax(segs_in, flat4), 50),
+                   "setgrad_scatter": _events(torch, lambda: codec.segments_scatter(flat4, segs_out, 1.0 / world), 50)}
+    del gin4, gout4, red4, segs_in, segs_out, flat4
     gpu_us = sum(kt4.values()) * 1e3
     res["config4_grandk_k10000"] = {
         "n": n4, "K": K4, "us_per_step": t * 1e3, "us_per_step_three_launch_codec_calls": t3 * 1e3,
+        "reducer_us_per_step": t_red * 1e3,
+        "reducer_kernels_us": {k: v * 1e3 for k, v in red_kernels.items()},
+        "reducer_step": "GlobalRandKMaxNormReducer.reduce(54 VGG16 tensors): fused flatten + norm, device index "
+                        "pop (one permutation upload per refill), the codec step above, setgrad of all n",
         "step": ("gather+absmax+encode (1 launch), decode-scatter" if rk.fused else
                  "gather+absmax, MAX, encode(gathered), SUM(words), decode-scatter"),
         "kernels_us": {k: v * 1e3 for k, v in kt4.items()},
@@ -482,25 +613,20 @@ def main():
     pipe_ok = bool(torch.equal(wp[0], wp[2]) and torch.equal(wp[1], wp[3]))
     del wp
 
-    # ---- per-kernel HIP-event timing: the timed loop replayed once more with
-    # events bracketing every absmax and encode launch (on the current stream,
-    # the one the codec launches on), so each kernel runs in the state it runs
-    # in inside a step; the timed loop itself stays free of event markers
-    # (4 markers per step cost ~14 us of step time, profiles/r01r_*)
-    reps = max(K, 10)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(reps)]
-    for e in ev:
-        e[0].record()
-        codec.absmax(x, out=norm)
-        e[1].record()
-        if world > 1:
-            dist.all_reduce(norm, op=dist.ReduceOp.MAX)
-        e[2].record()
-        encode_step()
-        e[3].record()
+    # ---- per-kernel HIP-event timing (roofline.achieved): each kernel in its own
+    # back-to-back loop, one event pair around the loop on the stream the codec
+    # launches on (torch's current stream).  No markers between launches: an
+    # event pair per launch inflated the kernel times by ~13 % at the driver's
+    # 20 steps, so the sum no longer fitted the timed step.  The
+    # encode loop reuses one global norm (the MAX is off this loop at N > 1)
+    # and consumes fresh draws every launch, exactly as in the step.
+    reps = max(K, 200)
     torch.cuda.synchronize()
-    ms_absmax = sum(e[0].elapsed_time(e[1]) for e in ev) / reps
-    ms_encode = sum(e[2].elapsed_time(e[3]) for e in ev) / reps
+    ms_absmax = _events(torch, lambda: codec.absmax(x, out=norm), reps)
+    if world > 1:
+        dist.all_reduce(norm, op=dist.ReduceOp.MAX)
+    ms_encode = _events(torch, encode_step, reps)
+    ms_step_events = _events(torch, step, reps) if world == 1 else None
     enc_bytes = 4 * n + 4 * M  # read x once, write the packed words
     achieved = enc_bytes / (ms_encode * 1e-3) / 1e9
     step_bytes = 8 * n + 4 * M  # + the max-norm read of x
@@ -534,7 +660,14 @@ def main():
                      "traffic_source": _traffic("k_qsgd_encode", n, bits)[1],
                      "bytes_per_launch": enc_bytes, "ms_per_launch": ms_encode},
         "kernels_ms": {"k_absmax": ms_absmax, "k_qsgd_encode": ms_encode},
+        "kernel_timing": {"method": f"back-to-back loop of {reps} launches per kernel, one HIP event pair "
+                                    "around each loop on the codec's stream",
+                          "absmax_plus_encode_ms": ms_absmax + ms_encode,
+                          "step_events_ms": ms_step_events,
+                          "fits_timed_step": ms_absmax + ms_encode <= ms_step},
     }
+    if world > 1:
+        out["process_group"] = _pg_evidence(torch, dist, dev, local, 4 * M)
 
     if not args.no_extras:
         # decode of the (W-summed) words, 1/W folded in
@@ -615,33 +748,9 @@ def main():
             except Exception as e:  # noqa: BLE001 — report, never fail the headline bench
                 out["reduce_path_2x_nodes"] = f"failed: {type(e).__name__}: {e}"
 
-        # PCIe-inclusive: the reference's path starts and ends in host memory;
-        # pinned buffers, hipMemcpyAsync (torch non_blocking copies) on the same stream
-        xh = torch.empty(n, dtype=torch.float32, pin_memory=True)
-        xh.copy_(x)
-        wh = torch.empty(M, dtype=torch.int32, pin_memory=True)
-        dh = torch.empty(n, dtype=torch.float32, pin_memory=True)
-        xd = torch.empty_like(x)
-
-        def pcie_encode():
-            xd.copy_(xh, non_blocking=True)
-            codec.absmax(xd, out=norm)
-            codec.qsgd_encode(xd, norm, bits, gen.reserve(n), world, out=words, lanes=lanes)
-            wh.copy_(words, non_blocking=True)
-
-        def pcie_decode():
-            words.copy_(wh, non_blocking=True)
-            codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
-            dh.copy_(dec, non_blocking=True)
-
-        pk = max(3, K // 4)
-        ms_pe = _events(torch, pcie_encode, pk)
-        ms_pd = _events(torch, pcie_decode, pk)
-        out["pcie_inclusive"] = {
-            "encode_grad_floats_per_s": n / (ms_pe * 1e-3), "encode_ms": ms_pe,
-            "decode_grad_floats_per_s": n / (ms_pd * 1e-3), "decode_ms": ms_pd,
-            "note": "pinned host x -> H2D -> absmax+encode -> D2H packed words; and H2D words -> decode -> D2H floats"}
-        del xh, wh, dh, xd, dec
+        del dec
+        # PCIe-inclusive: the reference's path starts and ends in host memory
+        out["pcie_inclusive"] = pcie_inclusive(torch, codec, gen, x, n, bits, world, lanes, K)
 
         # reference-parity mode: torch CPU-generator (MT19937) stream, generated on the
         # GPU by the jumped parallel generators, then the encode from those draws;

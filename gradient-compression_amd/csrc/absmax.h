@@ -7,11 +7,20 @@
 // a preceding hipMemsetAsync).  With a workspace: no memset launch — every
 // block stores its partial (sc1) and takes a ticket (agent-scope atomic add);
 // the block that draws the last ticket reduces the partials (sc1 loads),
-// writes *norm and re-arms the ticket.  Fence-free: a per-block release fence
-// (buffer_wbl2) measured 2x slower than the memset it removes.
-// Same-address atomics serialise (~88/us, MI355X_MICROARCH.md 'dequeue'), so
-// grids above 256 blocks take a two-level ticket: one per 64-block group,
-// then one for the group winners.
+// writes *norm and re-arms the ticket.
+//
+// The hand-off is fence-free and rests on a gfx950 hardware property, not on
+// the HIP memory model: every partial is stored sc1 (write-through past the
+// XCD L2) and drained (s_waitcnt vmcnt(0)) before its block's relaxed
+// agent-scope ticket add, and the last block reads the partials with sc1
+// loads (L1 bypassed) only after its add returned — row 1 of the sc1 hand-off
+// table of MI355X_MICROARCH.md ("measured on gfx950 / ROCm 7.2, not an
+// architectural guarantee").  The release / acquire form the model asks for
+// costs a buffer_wbl2 per block (~1.7 us each, same guide) and a buffer_inv in
+// the last block; it measured 2x slower than the memset it removes
+// (include/gcodec.h states the assumption).  Same-address atomics serialise
+// (~88/us, MI355X_MICROARCH.md 'dequeue'), so launchers cap the grid at
+// kAbsmaxMaxBlocks = 256 tickets.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -22,12 +31,10 @@
 namespace gc {
 
 constexpr unsigned kAbsmaxThreads = 1024;  // product block size
-constexpr unsigned kAbsmaxMaxBlocks = 4096;
-constexpr unsigned kAbsmaxGroup = 64;      // blocks per first-level ticket
-// workspace (uint32 words): [0] ticket, [16 (1 + g)] group tickets (own lines),
-// [kWsGpart + g] group partials, [kWsPart + b] block partials
-constexpr unsigned kWsGpart = 16 * (1 + kAbsmaxMaxBlocks / kAbsmaxGroup);
-constexpr unsigned kWsPart = kWsGpart + kAbsmaxMaxBlocks / kAbsmaxGroup;
+constexpr unsigned kAbsmaxMaxBlocks = 256;  // one ticket per block, one 256-add chain
+// workspace (uint32 words): [0] ticket (a 128-byte line of its own),
+// [kWsPart + b] block partials
+constexpr unsigned kWsPart = 32;
 constexpr unsigned kAbsmaxWsWords = kWsPart + kAbsmaxMaxBlocks;
 
 __device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
@@ -82,50 +89,21 @@ __device__ __forceinline__ void absmax_finish(uint32_t m, uint32_t *__restrict__
             atomicMax(out, m);
         return;
     } else {
-        const uint32_t nb = gridDim.x;
-        const bool two = nb > 256;
+        const uint32_t nb = gridDim.x;  // <= kAbsmaxMaxBlocks (launchers)
         if (threadIdx.x == 0) {
             // sc1 store, drained, then the agent-scope ticket: the fence-free
             // hand-off of MI355X_MICROARCH.md (row 1 of the sc1 table)
             sc1_store(&ws[kWsPart + blockIdx.x], m);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (two) {
-                const uint32_t g = blockIdx.x / kAbsmaxGroup;
-                const uint32_t gsize = min(kAbsmaxGroup, nb - g * kAbsmaxGroup);
-                last = __hip_atomic_fetch_add(&ws[16 * (1 + g)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                       gsize - 1;
-            } else {
-                last = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
-            }
+            last = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
         }
         __syncthreads();  // the other waves load only after the last add returned
         if (!last)
             return;
-        if (two) {  // this block closes its group
-            const uint32_t g = blockIdx.x / kAbsmaxGroup;
-            const uint32_t gsize = min(kAbsmaxGroup, nb - g * kAbsmaxGroup);
-            const uint32_t ng = (nb + kAbsmaxGroup - 1) / kAbsmaxGroup;
-            const uint32_t gm = block_max_sc1<BT>(&ws[kWsPart + g * kAbsmaxGroup], gsize, part);
-            if (threadIdx.x == 0) {
-                sc1_store(&ws[kWsGpart + g], gm);
-                sc1_store(&ws[16 * (1 + g)], 0u);  // re-arm the group ticket
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                last = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
-            }
-            __syncthreads();
-            if (!last)
-                return;
-            const uint32_t r = block_max_sc1<BT>(&ws[kWsGpart], ng, part);
-            if (threadIdx.x == 0) {
-                *out = r;
-                sc1_store(&ws[0], 0u);
-            }
-        } else {
-            const uint32_t r = block_max_sc1<BT>(&ws[kWsPart], nb, part);
-            if (threadIdx.x == 0) {
-                *out = r;
-                sc1_store(&ws[0], 0u);
-            }
+        const uint32_t r = block_max_sc1<BT>(&ws[kWsPart], nb, part);
+        if (threadIdx.x == 0) {
+            *out = r;
+            sc1_store(&ws[0], 0u);  // re-arm
         }
     }
 }

@@ -24,7 +24,7 @@ namespace gc {
 
 // max-norm: k_absmax (absmax.h).  Product grid: kAbsmaxGrid blocks of
 // kAbsmaxThreads (one per CU: 16 waves x 4 float4 loads in flight = 64 KB per CU).
-constexpr unsigned kAbsmaxGrid = 256;
+constexpr unsigned kAbsmaxGrid = kAbsmaxMaxBlocks;  // 256: the one-level ticket's cap
 constexpr unsigned kEncodeGrid = 12288;  // blocks of the dense encode (see launch_encode)
 constexpr unsigned kDecodeGrid = 16384;  // blocks of the dense decode (see qsgd_decode)
 
@@ -201,10 +201,10 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_dequantize(const QT *__restrict
 // ---------------------------------------------------------------------------
 // four consecutive words per thread: one 4-byte (int8) / 16-byte (int32) load
 // per plane (plane starts are 4-word aligned, check_lanes)
-template <typename QT>
+template <typename QT, bool VEC>
 __device__ __forceinline__ int4 load_q4(const QT *__restrict__ q, uint64_t i, uint64_t n)
 {
-    if (i + 3 < n) {
+    if (VEC && i + 3 < n) {
         if constexpr (sizeof(QT) == 1) {
             const uint32_t u = *reinterpret_cast<const uint32_t *>(q + i);
             return make_int4((int8_t)u, (int8_t)(u >> 8), (int8_t)(u >> 16), (int8_t)(u >> 24));
@@ -216,7 +216,8 @@ __device__ __forceinline__ int4 load_q4(const QT *__restrict__ q, uint64_t i, ui
                      i + 3 < n ? (int32_t)q[i + 3] : 0);
 }
 
-template <int L, typename QT>
+// VEC: q aligned to the vector load (4 B int8, 16 B int32); else scalar loads
+template <int L, typename QT, bool VEC>
 __global__ __launch_bounds__(kBlock) void k_lane_pack4(const QT *__restrict__ q, uint64_t n, int32_t off, uint32_t w,
                                                        uint64_t M, uint32_t *__restrict__ words)
 {
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(kBlock) void k_lane_pack4(const QT *__restrict__ q,
             const uint64_t i = (uint64_t)k * M + 4 * t;
             if (i >= n)
                 break;
-            const int4 v = load_q4(q, i, n);
+            const int4 v = load_q4<QT, VEC>(q, i, n);
             const uint32_t sh = (uint32_t)k * w;
             acc.x |= (uint32_t)(v.x + off) << sh;
             acc.y |= i + 1 < n ? (uint32_t)(v.y + off) << sh : 0u;
@@ -596,6 +597,7 @@ int gc_lane_pack(const void *q, uint32_t q_dtype, const gc_lanes *lanes, uint32_
         return rc;
     GC_REQUIRE(q_dtype == GC_I8 || q_dtype == GC_I32, "gc_lane_pack: q_dtype must be GC_I8 or GC_I32");
     GC_REQUIRE(words && (lanes->n == 0 || q), "gc_lane_pack: null pointer");
+    GC_REQUIRE(aligned16(words), "gc_lane_pack: words must be 16-byte aligned (word quads are stored as uint4)");
     if (lanes->plane_words == 0)
         return GC_OK;
     hipStream_t st = as_stream(stream);
@@ -608,15 +610,27 @@ int gc_lane_pack(const void *q, uint32_t q_dtype, const gc_lanes *lanes, uint32_
                                          st, reinterpret_cast<const int8_t *>(q), lanes->n, off, lanes->bits,
                                          lanes->plane_words, words));
     } else if (q_dtype == GC_I8) {
-        GC_DISPATCH_L(lanes->per_word,
-                      hipLaunchKernelGGL((k_lane_pack4<LL, int8_t>), dim3(grid), dim3(kBlock), 0, st,
-                                         reinterpret_cast<const int8_t *>(q), lanes->n, off, lanes->bits,
-                                         lanes->plane_words, words));
+        if ((reinterpret_cast<uintptr_t>(q) & 3u) == 0)
+            GC_DISPATCH_L(lanes->per_word,
+                          hipLaunchKernelGGL((k_lane_pack4<LL, int8_t, true>), dim3(grid), dim3(kBlock), 0, st,
+                                             reinterpret_cast<const int8_t *>(q), lanes->n, off, lanes->bits,
+                                             lanes->plane_words, words))
+        else
+            GC_DISPATCH_L(lanes->per_word,
+                          hipLaunchKernelGGL((k_lane_pack4<LL, int8_t, false>), dim3(grid), dim3(kBlock), 0, st,
+                                             reinterpret_cast<const int8_t *>(q), lanes->n, off, lanes->bits,
+                                             lanes->plane_words, words))
     } else {
-        GC_DISPATCH_L(lanes->per_word,
-                      hipLaunchKernelGGL((k_lane_pack4<LL, int32_t>), dim3(grid), dim3(kBlock), 0, st,
-                                         reinterpret_cast<const int32_t *>(q), lanes->n, off, lanes->bits,
-                                         lanes->plane_words, words));
+        if ((reinterpret_cast<uintptr_t>(q) & 15u) == 0)
+            GC_DISPATCH_L(lanes->per_word,
+                          hipLaunchKernelGGL((k_lane_pack4<LL, int32_t, true>), dim3(grid), dim3(kBlock), 0, st,
+                                             reinterpret_cast<const int32_t *>(q), lanes->n, off, lanes->bits,
+                                             lanes->plane_words, words))
+        else
+            GC_DISPATCH_L(lanes->per_word,
+                          hipLaunchKernelGGL((k_lane_pack4<LL, int32_t, false>), dim3(grid), dim3(kBlock), 0, st,
+                                             reinterpret_cast<const int32_t *>(q), lanes->n, off, lanes->bits,
+                                             lanes->plane_words, words))
     }
     return launch_status("gc_lane_pack");
 }

@@ -30,7 +30,8 @@ namespace gc {
 
 constexpr unsigned kRkThreads = 1024;
 constexpr uint64_t kRkFusedMax = 16384;  // K of the fused path: uint16 lanes in 32 KB of LDS
-constexpr unsigned kRkMaxBlocks = 256;   // one-level ticket (absmax.h)
+constexpr uint32_t kRkFusedMaxBits = 15; // lane values 0 .. 2 (2^b - 1) fit 16 bits
+constexpr unsigned kRkMaxBlocks = kAbsmaxMaxBlocks;  // one-level ticket (absmax.h)
 
 template <bool FUSED, int KIND>
 __global__ __launch_bounds__(kRkThreads) void k_randk_gather(const float *__restrict__ x, const int64_t *__restrict__ idx,
@@ -168,6 +169,9 @@ int gc_randk_encode_w1(const float *x, const int64_t *idx, uint64_t k, float *xk
                "gc_randk_encode_w1: lanes not made by gc_qsgd_layout(k, bits, 1)");
     GC_REQUIRE(k <= kRkFusedMax, "gc_randk_encode_w1: K = %llu above %llu", (unsigned long long)k,
                (unsigned long long)kRkFusedMax);
+    // lanes are staged as uint16 in LDS: a lane value reaches 2 s = 2^(b+1) - 2
+    GC_REQUIRE(bits <= kRkFusedMaxBits, "gc_randk_encode_w1: %u bits above %u (16-bit LDS lanes; use "
+               "gc_randk_gather_absmax + gc_qsgd_encode)", bits, kRkFusedMaxBits);
     GC_REQUIRE(rng && (rng->kind == GC_RNG_PHILOX || (rng->kind == GC_RNG_STREAM && rng->stream)),
                "gc_randk_encode_w1: bad rng");
     GC_REQUIRE(words, "gc_randk_encode_w1: null words");

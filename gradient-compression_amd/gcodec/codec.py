@@ -196,6 +196,12 @@ def qsgd_decode(words, n, norm, bits, world=1, alpha=1.0, idx=None, out=None, la
 # small-K GlobalRandK (reducer.py:717-754)
 # ---------------------------------------------------------------------------
 RANDK_FUSED_MAX = 16384      # K of the one-launch W = 1 encode (gc_randk_encode_w1)
+RANDK_FUSED_MAX_BITS = 15    # its lanes are staged as uint16 in LDS (values up to 2 (2^b - 1))
+
+
+def randk_fused_ok(k: int, bits: int, world: int = 1) -> bool:
+    """Whether gc_randk_encode_w1 takes this step (W = 1, K and b within its LDS staging)."""
+    return world == 1 and k <= RANDK_FUSED_MAX and bits <= RANDK_FUSED_MAX_BITS
 RANDK_GATHER_MAX = 256 * 1024  # K of gc_randk_gather_absmax
 
 
@@ -266,7 +272,7 @@ class RandKStep:
         self.words = torch.empty(self.lanes.plane_words, dtype=torch.int32, device=dev)
         self.norm = torch.empty(1, dtype=torch.float32, device=dev)
         self.xk = torch.empty(self.k, dtype=torch.float32, device=dev)
-        self.fused = self.world == 1 and self.k <= RANDK_FUSED_MAX
+        self.fused = randk_fused_ok(self.k, self.bits, self.world)
         self._rng = _lib.gc_rng(_lib.GC_RNG_PHILOX, 0, 0, 0, None)
         self._ws = {}
         lib = _lib.load()
@@ -520,12 +526,22 @@ def ms_mask_encode(x, norm, levels, rng, world=1, idx=None, out=None, cache=None
     return out
 
 
+MS_FUSED_MAX_R = 8  # ms_fast.h kMsFusedMaxR: q words per mask word of the coupled W = 1 layout
+
+
 def ms_w1_ok(x, levels) -> bool:
     """Whether gc_ms_encode_w1 (the one-pass W = 1 multi-scale encode) takes
-    this bucket: dense 16-byte aligned fp32 x, n < 2^32, 2 or 3 levels of <= 24 bits."""
+    this bucket — exactly the C entry point's preconditions: dense 16-byte
+    aligned fp32 x, n < 2^32, 2 or 3 levels of <= 24 bits, and a q lane of at
+    most 8 bits (r = 32 / lanes-per-word <= 8 q words per mask word: two levels
+    with a lower level of <= 7 bits, three with <= 6).  Otherwise callers run
+    the mask + select passes."""
     lv = sorted(int(b) for b in levels)
-    return (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.data_ptr() % 16 == 0
-            and x.numel() < 2 ** 32 and len(lv) in (2, 3) and lv[-1] <= 24)
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.data_ptr() % 16 == 0
+            and x.numel() < 2 ** 32 and len(lv) in (2, 3) and lv[-1] <= 24):
+        return False
+    ql, _ = ms_layouts(x.numel(), lv, 1)
+    return 32 // ql.per_word <= MS_FUSED_MAX_R
 
 
 def ms_encode_w1(x, norm, levels, rng, mask_out=None, out=None):

@@ -230,10 +230,19 @@ class GlobalRandKMaxNormReducer(Reducer):
         self._K = K
         self._indices_queue = []
 
-    def _next_indices(self, n):
+    def _next_indices(self, n, device):
+        """reducer.py:717-722: on refill set_seed, torch.randperm(n) (CPU
+        generator, the reference's permutation) split into K-chunks, popped
+        from the end.  The permutation goes to the device ONCE per refill (one
+        8n-byte copy every ceil(n/K) steps: 118 MB per 1,473 steps for VGG16)
+        and the queue holds device slices, so a step does no host->device
+        index copy (the reference copies its numpy chunk every step, 722-723)."""
         if not self._indices_queue:
             set_seed(self._seed, self._gen)
-            self._indices_queue = list(torch.randperm(n).split(self._K))
+            perm = torch.randperm(n)
+            if perm.device != device:
+                perm = perm.pin_memory().to(device, non_blocking=True) if device.type == "cuda" else perm.to(device)
+            self._indices_queue = list(perm.split(self._K))
         return self._indices_queue.pop()
 
     def _randk_compressor(self):
@@ -244,10 +253,10 @@ class GlobalRandKMaxNormReducer(Reducer):
         comp = self._randk_compressor()
         flat, _ = self._flat_pack(grad_in)
         n = flat.buffer.numel()
-        idx = self._next_indices(n).to(flat.buffer.device, non_blocking=True)
+        idx = self._next_indices(n, flat.buffer.device)
         k = idx.numel()
         codec = self._codec
-        if W == 1 and hasattr(codec, "randk_encode_w1") and k <= codec.RANDK_FUSED_MAX:
+        if hasattr(codec, "randk_fused_ok") and codec.randk_fused_ok(k, self._quantization_level, W):
             # gather + max-norm + encode in one launch (the MAX over one rank is the identity)
             with self._timer("reduce.compress", verbosity=2):
                 words, norm = comp.encode_w1(flat.buffer, idx)
@@ -349,7 +358,7 @@ class GlobalRandKMaxNormTwoScaleReducer(QSGDMaxNormTwoScaleReducer):
         comp = self._make()
         flat, _ = self._flat_pack(grad_in)
         n = flat.buffer.numel()
-        idx = self._next_indices(n).to(flat.buffer.device, non_blocking=True)
+        idx = self._next_indices(n, flat.buffer.device)
         k = idx.numel()
         norm, mask, words, bits = self._reduce_scales(comp, flat, idx, k)
         with self._timer("reduce.decompress", verbosity=2):

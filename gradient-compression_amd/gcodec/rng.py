@@ -80,7 +80,14 @@ class Generator:
     default still draw independent uniforms — the reference seeds every rank's
     torch generator with seed + rank (model_dispatcher.py:59, trainer.py:158).
     Identical draws on every rank would correlate the ranks' rounding errors
-    instead of averaging them down with W."""
+    instead of averaging them down with W.
+
+    A caller that already follows the reference's seeding (seed + rank per
+    rank, trainer.py:158) passes the BASE seed to a per_rank generator, or
+    uses per_rank=False with its own seed + rank; passing seed + rank to a
+    per_rank generator keys the stream with seed + 2 rank.  The process-wide
+    default_generator is per_rank; gcodec.manual_seed(seed, per_rank=False)
+    switches it to the caller's key."""
 
     def __init__(self, seed: int = 42, mode: str = "philox", per_rank: bool = False):
         self.per_rank = per_rank
@@ -119,9 +126,14 @@ class Generator:
 default_generator = Generator(per_rank=True)
 
 
-def manual_seed(seed: int, mode: str | None = None) -> Generator:
+def manual_seed(seed: int, mode: str | None = None, per_rank: bool | None = None) -> Generator:
+    """Seed the default generator.  per_rank (kept when None) adds the process
+    rank to the Philox key: pass the base seed with per_rank=True, or the
+    caller's own seed + rank with per_rank=False (see Generator)."""
     if mode is not None:
         default_generator.set_mode(mode)
+    if per_rank is not None:
+        default_generator.per_rank = bool(per_rank)
     return default_generator.manual_seed(seed)
 
 

@@ -156,11 +156,13 @@ def ddp_hook_world(rank, world, init_file, out_dir, use_gpu, levels=None, two_sc
     def hook(st, bucket):
         x_in = bucket.buffer().detach().cpu().numpy().copy()
         off = st.gen.offset
+        slot = len(rec)  # the call order (bucket order), not the order the futures complete in
+        rec.append(None)
         fut = qsgd_hook(st, bucket)
 
         def keep(f):
             out = f.value()
-            rec.append((x_in, off, out.detach().cpu().numpy().copy()))
+            rec[slot] = (x_in, off, out.detach().cpu().numpy().copy())
             return out
 
         return fut.then(keep)
@@ -245,5 +247,60 @@ def default_generator_world(rank, world, init_file, out_dir):
     ref = O.qsgd_encode(x, O.absmax(x), 4, world, O.philox_rng(r.seed, off))
     np.savez(os.path.join(out_dir, f"g{rank}.npz"), words=words.numpy(), key=np.int64(r.seed),
              oracle=ref.view(np.int32))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+HOOK_CASES = {"qsgd": dict(bits=4), "ts": dict(levels=[2, 4], two_scale=True), "ms": dict(levels=[2, 4]),
+              "ms3": dict(levels=[2, 4, 6])}
+
+
+class _Bucket:
+    def __init__(self, t):
+        self._t = t
+
+    def buffer(self):
+        return self._t
+
+
+def hook_vs_reference(rank, world, init_file, fixture, out_dir, use_gpu):
+    """gcodec.ddp_hook.qsgd_hook on ONE bucket holding the whole gradient in
+    TensorBuffer order (what DDP hands the hook when bucket_cap_mb covers the
+    model and the bucket order is the reference's), torch-mode RNG, on the
+    reducers' golden grads: the result must equal the reference reducers'
+    grad_out (reducer.py:498-554, 1454-1531, 1636-1715)."""
+    import gcodec
+    from gcodec.ddp_hook import QSGDHookState, qsgd_hook
+
+    if use_gpu:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        codec = None
+    else:
+        import oracle_codec as codec
+
+        dev = torch.device("cpu")
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    z = np.load(fixture, allow_pickle=False)
+    res = {}
+    for name, kw in HOOK_CASES.items():
+        state = QSGDHookState(generator=gcodec.Generator(0, "torch"), codec=codec, **kw)
+        torch.manual_seed(SEED + rank)
+        for step in range(2):
+            gin = []
+            i = 0
+            while f"r{rank}/{name}/s{step}/in{i}" in z.files:
+                gin.append(torch.from_numpy(z[f"r{rank}/{name}/s{step}/in{i}"].copy()))
+                i += 1
+            flat = torch.cat([g.reshape(-1) for g in gin]).to(dev)
+            out = qsgd_hook(state, _Bucket(flat)).wait()
+            if use_gpu:
+                torch.cuda.synchronize()
+            out = out.cpu()
+            pos = 0
+            for i, g in enumerate(gin):
+                res[f"{name}/s{step}/out{i}"] = out[pos:pos + g.numel()].reshape(g.shape).numpy()
+                pos += g.numel()
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()

@@ -70,3 +70,32 @@ def test_ddp_multiscale_hook_matches_oracle(world, levels, two_scale):
                  nprocs=world, join=True)
         recs = [np.load(os.path.join(td, f"h{r}.npz"), allow_pickle=False) for r in range(world)]
         check_hook_records(recs, world, levels=list(levels), order=1 if two_scale else 0)
+
+
+def check_hook_vs_reference(world, td):
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"reducers_w{world}.npz")
+    ref = np.load(gold, allow_pickle=False)
+    for r in range(world):
+        got = np.load(os.path.join(td, f"r{r}.npz"), allow_pickle=False)
+        for name in W.HOOK_CASES:
+            for step in range(2):
+                i = 0
+                while f"{name}/s{step}/out{i}" in got.files:
+                    a, b = got[f"{name}/s{step}/out{i}"], ref[f"r{r}/{name}/s{step}/out{i}"]
+                    assert a.tobytes() == b.tobytes(), f"rank {r} {name} step {step} tensor {i}"
+                    i += 1
+                assert i > 0
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_single_bucket_hook_matches_reference_reducers(world):
+    """The hook on one bucket = the whole gradient in TensorBuffer order equals
+    the REFERENCE reducers (reducers_w{1,2}.npz) bit for bit (oracle codec on
+    CPU, torch-mode RNG).  With several buckets the hook scales each bucket by
+    its own max-norm, which the reference (one monolithic bucket) never does:
+    DESIGN §6 / INTEGRATION §5."""
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"reducers_w{world}.npz")
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(W.hook_vs_reference, args=(world, os.path.join(td, "init"), gold, td, False), nprocs=world,
+                 join=True)
+        check_hook_vs_reference(world, td)

@@ -110,3 +110,18 @@ def test_hip_reducers_through_node_topology(local_size):
         mp.spawn(W.hip_reducer_vs_reference, args=(world, os.path.join(td, "init"), fixture, td, local_size),
                  nprocs=world, join=True)
         _check_vs_reference(world, td)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_single_bucket_hook_matches_reference_reducers_gpu(world):
+    """gcodec.ddp_hook.qsgd_hook with the HIP codec on one bucket holding the
+    whole gradient (TensorBuffer order), torch-mode RNG: == the REFERENCE
+    reducers' grad_out (reducers_w{1,2}.npz) for QSGD-MN, two-scale and
+    multi-scale [2,4] / [2,4,6] (W = 1: one-pass encode; W = 2: q cache)."""
+    from test_ddp_hook_gloo import check_hook_vs_reference
+
+    fixture = os.path.join(GOLD, f"reducers_w{world}.npz")
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(W.hook_vs_reference, args=(world, os.path.join(td, "init"), fixture, td, True), nprocs=world,
+                 join=True)
+        check_hook_vs_reference(world, td)

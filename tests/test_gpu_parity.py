@@ -583,6 +583,23 @@ def test_lane_pack_unpack_kernels(n):
         assert np.array_equal(back.cpu().numpy(), q * world)
 
 
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_lane_pack_misaligned_q(shift):
+    """q slices at every misalignment of the vector loads (int8 4 B, int32 16 B)
+    take the scalar-load kernel; misaligned words are refused (GC_EINVAL)."""
+    n, s = 70_001, 15
+    q = np.random.default_rng(shift).integers(-s, s + 1, n + shift).astype(np.int32)
+    ln = codec.qsgd_layout(n, 4, 1)
+    exp = O.lane_pack(q[shift:], s, ln.bits, ln.per_word, ln.plane_words)
+    for dt in (torch.int8, torch.int32):
+        qd = dev(q).to(dt)[shift:]
+        assert qd.data_ptr() % (4 if dt == torch.int8 else 16)
+        assert bits_eq(u32(codec.lane_pack(qd, ln)), exp)
+    wbuf = torch.empty(ln.plane_words + 4, dtype=torch.int32, device=DEV)
+    with pytest.raises(gcodec.GCodecError):
+        codec.lane_pack(dev(q[:n]).to(torch.int8), ln, out=wbuf[shift:])
+
+
 def test_bytepack_kernels_match_reference_vectors():
     p = os.path.join(GOLD, "packers.npz")
     if not os.path.exists(p):

@@ -2,7 +2,13 @@
 multi-scale kernels on the ResNet50 bucket (one-pass W = 1 encode, the two W > 1
 passes, decode; the q-cache mask and cache select at W = 2 lanes), the parallel MT19937 (1e8 draws), the small-K GlobalRandK step,
 the headline absmax + encode (1e8, 4-bit) and its torch-parity form
-(MT19937 draws consumed by the generator kernel, then the lane pack).  Each runs `REPS` times."""
+(MT19937 draws consumed by the generator kernel, then the lane pack).  Each runs `REPS` times.
+
+Steady state: a clock settle first (SETTLE seconds of config-3 steps, as
+bench.py's --settle), and every kernel name is launched at ONE size only, so a
+kernel's rocprof average / spread describes one workload (k_absmax: the
+ResNet50 bucket; the 1e8 headline kernels are profiled over bench.py itself,
+tools/profile.sh)."""
 import os
 import sys
 
@@ -15,7 +21,10 @@ import torch  # noqa: E402
 import gcodec  # noqa: E402
 from gcodec import codec  # noqa: E402
 
-REPS = int(os.environ.get("REPS", "5"))
+import time  # noqa: E402
+
+REPS = int(os.environ.get("REPS", "20"))
+SETTLE = float(os.environ.get("SETTLE", "0.5"))
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(11)
 n3 = 23_520_842
@@ -23,7 +32,14 @@ x3 = torch.randn(n3, device=dev, generator=g).mul_(0.01)
 gen = gcodec.Generator(5, "philox")
 ms = gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen)
 nrm = codec.absmax(x3)
+t0 = time.perf_counter()
+while time.perf_counter() - t0 < SETTLE:  # clocks ramp over ~0.1-0.3 s of sustained load
+    for _ in range(20):
+        codec.absmax(x3, out=nrm)
+        ms.encode_w1(nrm, x3)
+    torch.cuda.synchronize()
 for _ in range(REPS):
+    codec.absmax(x3, out=nrm)
     m, w = ms.encode_w1(nrm, x3)
     m2 = ms.encode_mask(nrm, x3, 1)
     w2 = ms.encode(nrm, x3, m2, 1)
@@ -54,9 +70,7 @@ del x4
 n = 100_000_000
 x = torch.randn(n, device=dev, generator=g).mul_(0.01)
 words = torch.empty(codec.qsgd_layout(n, 4, 1).plane_words, dtype=torch.int32, device=dev)
-for _ in range(REPS):
-    codec.absmax(x, out=nrm)
-    codec.qsgd_encode(x, nrm, 4, gen.reserve(n), 1, out=words)
+nrm = x.abs().max().reshape(1)  # torch's reduction: k_absmax stays at one size in this profile
 torch.cuda.synchronize()
 torch.manual_seed(42)  # torch-parity mode: draws -> encode from the draws; and the fused form
 tgen = gcodec.Generator(0, "torch")
