@@ -667,159 +667,223 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
 // W = 1: mask + select in ONE pass (compressors.py:778-817 with the MIN
 // all-reduce of reducer.py:1680 over a single rank, the identity: the common
 // level is the rank's own).  Per 4 elements: the levels 1..NL-1 decide the
-// mask (mask_plane), the chosen level's rounding is kept, and level 0's draw
-// block is computed only when an element stays at level 0 — the same draws,
+// mask, the chosen level's rounding is kept, and level 0's draw block is
+// computed only when an element stays at level 0 — the same draws,
 // arithmetic and decisions as mask_plane + select_plane, so both streams are
-// bit-identical to the two-pass encode.  The coupled W = 1 layouts
-// (gc_ms_mask_layout) make mask plane P = h + r k the q lane k of q words
-// h Mm + pos: the block that owns mask quad t owns q quads t + h Mm/4 whole.
+// bit-identical to the two-pass encode.
+//
+// Work split: the coupled W = 1 layouts (gc_ms_mask_layout) make mask plane
+// P = h + r k the q lane k of q words h Mm + pos, so a block of r waves owns
+// 64 mask word quads, and wave h owns q stream h: it walks the Lq planes
+// P = h + r k of its quad column and assembles its q words in registers — no
+// LDS traffic for the q lanes; only the mask words (one bit per plane) are
+// OR-ed across the r waves.  The plane index is wave-uniform (scalar).
 // ---------------------------------------------------------------------------
+// fast path of 4 elements: the level m of each (uint4) and T at that level
+// (T >> 24 = -xi, ms_t).  Levels above 0 may exceed 7 bits: their T saturates
+// (v_cvt_flr_i32_f32 clamps) once |Ls| > 2^31, i.e. xi >= 128 > maxv, which is
+// exactly "not this level"; a level is only ever chosen with xi <= maxv <= 127.
 template <int KIND, int NL, int VAR = 0>
-__device__ __forceinline__ void fused_plane(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
-                                            uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
-                                            const RngArgs &rng, int32_t qmax, uint4 &m, uint4 &ln)
+__device__ __forceinline__ void fused_quad_fast(const float4 &v, uint32_t i0, const DivNorm &dv, const MsFastArg &fa,
+                                                const RngArgs &rng, uint4 &m, int4 &T)
 {
-    RangeI rg;
-    rg.add4(v);
+    const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
     m = make_uint4(0u, 0u, 0u, 0u);
-    if ((VAR & MSV_WIDE) == 0 && dv.fast && !rg.slow(lo2, hi2)) {
-        const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
-        int32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;  // T at the element's level
+    T = make_int4(0, 0, 0, 0);
 #pragma unroll
-        for (int l = 1; l < NL; ++l) {
-            const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
-            const gc_f2 S = {fa.S24[l], fa.S24[l]};
-            const gc_f2 a = q01 * S, b = q23 * S;
-            const int32_t u0 = ms_t(a.x, r.x), u1 = ms_t(a.y, r.y), u2 = ms_t(b.x, r.z), u3 = ms_t(b.y, r.w);
-            if (u0 >= fa.thr) { m.x = l; t0 = u0; }
-            if (u1 >= fa.thr) { m.y = l; t1 = u1; }
-            if (u2 >= fa.thr) { m.z = l; t2 = u2; }
-            if (u3 >= fa.thr) { m.w = l; t3 = u3; }
-        }
-        if (m.x == 0u || m.y == 0u || m.z == 0u || m.w == 0u) {  // level 0's draws only when needed
-            const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
-            const gc_f2 S = {fa.S24[0], fa.S24[0]};
-            const gc_f2 a = q01 * S, b = q23 * S;
-            t0 = m.x == 0u ? ms_t(a.x, r.x) : t0;
-            t1 = m.y == 0u ? ms_t(a.y, r.y) : t1;
-            t2 = m.z == 0u ? ms_t(b.x, r.z) : t2;
-            t3 = m.w == 0u ? ms_t(b.y, r.w) : t3;
-        }
-        ln = make_uint4(lane_of_t_nc(v.x, t0, qmax), lane_of_t_nc(v.y, t1, qmax), lane_of_t_nc(v.z, t2, qmax),
-                        lane_of_t_nc(v.w, t3, qmax));
-    } else {
-        const float4 ql = quot4_exact(v, dv);
-        int32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-#pragma unroll
-        for (int l = 1; l < NL; ++l) {
-            const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
-            const float s = lv.s[l];
-            const int32_t x0 = xi_from_q(ql.x, s, r.x), x1 = xi_from_q(ql.y, s, r.y);
-            const int32_t x2 = xi_from_q(ql.z, s, r.z), x3 = xi_from_q(ql.w, s, r.w);
-            if (x0 <= lv.maxv) { m.x = l; q0 = sgn_of(v.x) * x0; }
-            if (x1 <= lv.maxv) { m.y = l; q1 = sgn_of(v.y) * x1; }
-            if (x2 <= lv.maxv) { m.z = l; q2 = sgn_of(v.z) * x2; }
-            if (x3 <= lv.maxv) { m.w = l; q3 = sgn_of(v.w) * x3; }
-        }
-        if (m.x == 0u || m.y == 0u || m.z == 0u || m.w == 0u) {
-            const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
-            const float s = lv.s[0];
-            q0 = m.x == 0u ? sgn_of(v.x) * xi_from_q(ql.x, s, r.x) : q0;
-            q1 = m.y == 0u ? sgn_of(v.y) * xi_from_q(ql.y, s, r.y) : q1;
-            q2 = m.z == 0u ? sgn_of(v.z) * xi_from_q(ql.z, s, r.z) : q2;
-            q3 = m.w == 0u ? sgn_of(v.w) * xi_from_q(ql.w, s, r.w) : q3;
-        }
-        ln = make_uint4(lane_of_q(q0, qmax), lane_of_q(q1, qmax), lane_of_q(q2, qmax), lane_of_q(q3, qmax));
+    for (int l = 1; l < NL; ++l) {
+        const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
+        const gc_f2 S = {fa.S24[l], fa.S24[l]};
+        const gc_f2 a = q01 * S, b = q23 * S;
+        const int32_t u0 = ms_t(a.x, r.x), u1 = ms_t(a.y, r.y), u2 = ms_t(b.x, r.z), u3 = ms_t(b.y, r.w);
+        const bool c0 = u0 >= fa.thr, c1 = u1 >= fa.thr, c2 = u2 >= fa.thr, c3 = u3 >= fa.thr;
+        m.x = c0 ? (uint32_t)l : m.x;
+        m.y = c1 ? (uint32_t)l : m.y;
+        m.z = c2 ? (uint32_t)l : m.z;
+        m.w = c3 ? (uint32_t)l : m.w;
+        T.x = c0 ? u0 : T.x;
+        T.y = c1 ? u1 : T.y;
+        T.z = c2 ? u2 : T.z;
+        T.w = c3 ? u3 : T.w;
     }
-    if (i0 + 4 > n) {  // elements past n: level 0, lane 0
-        m.y = i0 + 1 < n ? m.y : 0u;
-        m.z = i0 + 2 < n ? m.z : 0u;
-        m.w = i0 + 3 < n ? m.w : 0u;
-        ln.y = i0 + 1 < n ? ln.y : 0u;
-        ln.z = i0 + 2 < n ? ln.z : 0u;
-        ln.w = i0 + 3 < n ? ln.w : 0u;
+    if (m.x == 0u || m.y == 0u || m.z == 0u || m.w == 0u) {  // level 0's draws only when needed
+        const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
+        const gc_f2 S = {fa.S24[0], fa.S24[0]};
+        const gc_f2 a = q01 * S, b = q23 * S;
+        T.x = m.x == 0u ? ms_t(a.x, r.x) : T.x;
+        T.y = m.y == 0u ? ms_t(a.y, r.y) : T.y;
+        T.z = m.z == 0u ? ms_t(b.x, r.z) : T.z;
+        T.w = m.w == 0u ? ms_t(b.y, r.w) : T.w;
+    }
+}
+
+// generic path of 4 elements (range-check failures, norms outside the
+// Markstein range, MSV_WIDE): levels and signed q at them
+template <int KIND, int NL, int VAR = 0>
+__device__ __forceinline__ void fused_quad_slow(const float4 &v, uint32_t i0, const DivNorm &dv, const LevelsArg &lv,
+                                                const RngArgs &rng, uint4 &m, int4 &q)
+{
+    const float4 ql = quot4_exact(v, dv);
+    m = make_uint4(0u, 0u, 0u, 0u);
+    q = make_int4(0, 0, 0, 0);
+#pragma unroll
+    for (int l = 1; l < NL; ++l) {
+        const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
+        const float s = lv.s[l];
+        const int32_t x0 = xi_from_q(ql.x, s, r.x), x1 = xi_from_q(ql.y, s, r.y);
+        const int32_t x2 = xi_from_q(ql.z, s, r.z), x3 = xi_from_q(ql.w, s, r.w);
+        if (x0 <= lv.maxv) { m.x = l; q.x = sgn_of(v.x) * x0; }
+        if (x1 <= lv.maxv) { m.y = l; q.y = sgn_of(v.y) * x1; }
+        if (x2 <= lv.maxv) { m.z = l; q.z = sgn_of(v.z) * x2; }
+        if (x3 <= lv.maxv) { m.w = l; q.w = sgn_of(v.w) * x3; }
+    }
+    if (m.x == 0u || m.y == 0u || m.z == 0u || m.w == 0u) {
+        const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
+        const float s = lv.s[0];
+        q.x = m.x == 0u ? sgn_of(v.x) * xi_from_q(ql.x, s, r.x) : q.x;
+        q.y = m.y == 0u ? sgn_of(v.y) * xi_from_q(ql.y, s, r.y) : q.y;
+        q.z = m.z == 0u ? sgn_of(v.z) * xi_from_q(ql.z, s, r.z) : q.z;
+        q.w = m.w == 0u ? sgn_of(v.w) * xi_from_q(ql.w, s, r.w) : q.w;
     }
 }
 
 constexpr uint32_t kMsFusedMaxR = 8;  // q words per mask word at W = 1: 32 / (q lanes per word) <= 8
 
-// planes: r * Lq mask planes in use; kdiv = ceil(2^16 / r) (P / r = (P * kdiv) >> 16 for P < 32)
-// WPB waves per block take the mask planes P = wave, wave + WPB, ...
-template <int KIND, int NL, int VAR = 0, int WPB = 4>
-__global__ __launch_bounds__(64 * WPB) void k_ms_fused_w1(const float *__restrict__ x, uint32_t n,
-                                                        const float *__restrict__ normp, LevelsArg lv, MsFastArg fa,
-                                                        RngArgs rng, uint32_t Mm, uint32_t r, uint32_t kdiv,
-                                                        uint32_t planes, uint32_t wq, int32_t qmax,
-                                                        uint32_t *__restrict__ mask_words, uint32_t *__restrict__ words)
+// one plane of the fused encode: levels into the mask fields, the lane into
+// the wave's q word accumulators.  Fast lanes: acc -= (T >> 24) * (+-2^sh)
+// (word = Cw - acc, as enc_tile_int; the 24-bit multiplier keeps sh <= 15 by
+// splitting the lanes into lo (k < H) and hi (k >= H, shifted by H wq at the
+// end)); generic lanes: pl += q << (k wq) (modular: lane = qmax + q).
+template <int KIND, int NL, int VAR>
+__device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                              uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                              const RngArgs &rng, uint32_t bitP, int32_t sgk, uint32_t shk,
+                                              uint4 (&macc)[NL - 1], int4 &acc, uint4 &pl)
+{
+    RangeI rg;
+    rg.add4(v);
+    uint4 m;
+    if ((VAR & MSV_WIDE) == 0 && dv.fast && !rg.slow(lo2, hi2)) {
+        int4 T;
+        fused_quad_fast<KIND, NL, VAR>(v, i0, dv, fa, rng, m, T);
+        acc.x += __mul24(T.x >> 24, med3_i32(__float_as_int(v.x), -sgk, sgk));
+        acc.y += __mul24(T.y >> 24, med3_i32(__float_as_int(v.y), -sgk, sgk));
+        acc.z += __mul24(T.z >> 24, med3_i32(__float_as_int(v.z), -sgk, sgk));
+        acc.w += __mul24(T.w >> 24, med3_i32(__float_as_int(v.w), -sgk, sgk));
+    } else {
+        int4 q;
+        fused_quad_slow<KIND, NL, VAR>(v, i0, dv, lv, rng, m, q);
+        pl.x += (uint32_t)q.x << shk;
+        pl.y += (uint32_t)q.y << shk;
+        pl.z += (uint32_t)q.z << shk;
+        pl.w += (uint32_t)q.w << shk;
+    }
+    if (i0 + 4 > n) {  // elements past n: no mask bit (their x = 0 adds no lane)
+        m.x = i0 < n ? m.x : 0u;
+        m.y = i0 + 1 < n ? m.y : 0u;
+        m.z = i0 + 2 < n ? m.z : 0u;
+        m.w = i0 + 3 < n ? m.w : 0u;
+    }
+#pragma unroll
+    for (int f = 0; f < NL - 1; ++f) {
+        macc[f].x |= m.x > (uint32_t)f ? bitP : 0u;
+        macc[f].y |= m.y > (uint32_t)f ? bitP : 0u;
+        macc[f].z |= m.z > (uint32_t)f ? bitP : 0u;
+        macc[f].w |= m.w > (uint32_t)f ? bitP : 0u;
+    }
+}
+
+__device__ __forceinline__ float4 load4_guard(const float *__restrict__ x, uint32_t i0, uint32_t n)
+{
+    return i0 < n ? load4_nt_tail<0>(x, i0, n) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+// blockDim = 64 r (r <= kMsFusedMaxR waves); wave h walks planes h + r k, k < Lq.
+template <int KIND, int NL, int VAR = 0>
+__global__ __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *__restrict__ x, uint32_t n,
+                                                                 const float *__restrict__ normp, LevelsArg lv,
+                                                                 MsFastArg fa, RngArgs rng, uint32_t Mm, uint32_t r,
+                                                                 uint32_t Lq, uint32_t wq, int32_t qmax,
+                                                                 uint32_t *__restrict__ mask_words,
+                                                                 uint32_t *__restrict__ words)
 {
     const float norm = *normp;
     const DivNorm dv = make_div(norm);
     const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
     const uint32_t quads = Mm >> 2;
-    __shared__ uint4 part[WPB - 1][kMsQuadsPerBlock];
-    // the tile's q words, [h][element e of the quad][quad]: every wave ORs its
-    // planes' lanes in (disjoint bit fields); bank = quad, conflict-free
-    __shared__ uint32_t qs[kMsFusedMaxR][4][kMsQuadsPerBlock];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    uint32_t *qflat = &qs[0][0][0];
+    const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t H = Lq >> 1;  // lanes k < H in lo, k >= H in hi
+    uint32_t Cw = 0;
+    for (uint32_t k = 0; k < Lq; ++k)
+        Cw += (uint32_t)qmax << (k * wq);
+    // the last plane of this wave holding any element (uniform): P = h + r k < ceil(n / Mm)
+    const uint32_t pend = (uint32_t)(((uint64_t)n + Mm - 1) / Mm);
+    const uint32_t kend = pend > h ? min(Lq, (pend - h + r - 1) / r) : 0u;
+    __shared__ uint4 part[kMsFusedMaxR - 1][NL - 1][kMsQuadsPerBlock];
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
-        for (uint32_t i = threadIdx.x; i < r * 4u * kMsQuadsPerBlock; i += 64u * WPB)
-            qflat[i] = 0u;
-        __syncthreads();
         const uint32_t t = tb + lane;
-        uint4 acc[NL - 1] = {};
-        if (t < quads) {
-            // not unrolled: one copy of the per-plane body (with both rounding
-            // paths inlined) keeps the kernel's code and scalar registers small;
-            // the next plane's x is loaded before this plane's math (two loads in flight)
-            uint32_t P = wave;
-            uint32_t i0 = P * Mm + 4u * t;
-            float4 vn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (P < planes && i0 < n)
-                vn = load4_nt_tail<0>(x, i0, n);
-#pragma unroll 1
-            for (int j = 0; j < 32 / WPB; ++j) {
-                if (P >= planes || i0 >= n)
-                    break;
+        uint4 macc[NL - 1] = {};
+        int4 lo = make_int4(0, 0, 0, 0), hi = make_int4(0, 0, 0, 0);
+        uint4 pl = make_uint4(0u, 0u, 0u, 0u);
+        if (t < quads && kend > 0) {
+            // two planes in flight: plane k + 1's x is loaded before plane k's math
+            uint32_t i0 = h * Mm + 4u * t;
+            const uint32_t step = r * Mm;
+            float4 vn = load4_guard(x, i0, n);
+            auto plane = [&](uint32_t k, uint32_t sh, int4 &a) {
                 const float4 v = vn;
-                const uint32_t Pn = P + WPB, i0n = i0 + WPB * Mm;
-                if (Pn < planes && i0n < n)
-                    vn = load4_nt_tail<0>(x, i0n, n);
-                uint4 m, ln;
-                fused_plane<KIND, NL, VAR>(v, n, i0, dv, lo2, hi2, lv, fa, rng, qmax, m, ln);
-                mask_bits<NL>(acc, m, P);
-                const uint32_t k = (P * kdiv) >> 16, h = P - k * r;
-                const uint32_t sh = k * wq;
-                atomicOr(&qs[h][0][lane], ln.x << sh);
-                atomicOr(&qs[h][1][lane], ln.y << sh);
-                atomicOr(&qs[h][2][lane], ln.z << sh);
-                atomicOr(&qs[h][3][lane], ln.w << sh);
-                P = Pn;
+                const uint32_t i0n = i0 + step;
+                if (k + 1 < kend)
+                    vn = load4_guard(x, i0n, n);
+                fused_plane_r<KIND, NL, VAR>(v, n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (h + r * k), 1 << sh, k * wq,
+                                             macc, a, pl);
                 i0 = i0n;
-            }
+            };
+            const uint32_t kmid = min(H, kend);
+#pragma unroll 1
+            for (uint32_t k = 0; k < kmid; ++k)
+                plane(k, k * wq, lo);
+#pragma unroll 1
+            for (uint32_t k = H; k < kend; ++k)
+                plane(k, (k - H) * wq, hi);
         }
+        // q words of stream h: quad t at j0 = h Mm + 4t, lane k = element j0 + e + k Mq
+        if (t < quads) {
+            const uint32_t hs = H * wq;
+            const uint64_t j0 = (uint64_t)h * Mm + 4u * t, Mq = (uint64_t)r * Mm;
+            uint4 C = make_uint4(Cw, Cw, Cw, Cw);
+            if (j0 + 3 + (uint64_t)(Lq - 1) * Mq >= n) {  // lanes of elements past n stay 0
+                C = make_uint4(0u, 0u, 0u, 0u);
+                for (uint32_t k = 0; k < Lq; ++k) {
+                    const uint64_t e = j0 + (uint64_t)k * Mq;
+                    const uint32_t c = (uint32_t)qmax << (k * wq);
+                    C.x += e < n ? c : 0u;
+                    C.y += e + 1 < n ? c : 0u;
+                    C.z += e + 2 < n ? c : 0u;
+                    C.w += e + 3 < n ? c : 0u;
+                }
+            }
+            st_nt4u(words + j0, make_uint4(C.x - ((uint32_t)lo.x + ((uint32_t)hi.x << hs)) + pl.x,
+                                           C.y - ((uint32_t)lo.y + ((uint32_t)hi.y << hs)) + pl.y,
+                                           C.z - ((uint32_t)lo.z + ((uint32_t)hi.z << hs)) + pl.z,
+                                           C.w - ((uint32_t)lo.w + ((uint32_t)hi.w << hs)) + pl.w));
+        }
+        // mask words: OR of the r waves' plane bits
+        if (h)
 #pragma unroll
-        for (int f = 0; f < NL - 1; ++f) {
-            if (wave)
-                part[wave - 1][lane] = acc[f];
-            __syncthreads();
-            if (wave == 0 && t < quads) {
-                uint4 o = acc[f];
+            for (int f = 0; f < NL - 1; ++f)
+                part[h - 1][f][lane] = macc[f];
+        __syncthreads();
+        if (h == 0 && t < quads) {
 #pragma unroll
-                for (int q = 0; q < WPB - 1; ++q) {
-                    const uint4 a = part[q][lane];
+            for (int f = 0; f < NL - 1; ++f) {
+                uint4 o = macc[f];
+                for (uint32_t q = 0; q + 1 < r; ++q) {
+                    const uint4 a = part[q][f][lane];
                     o = make_uint4(o.x | a.x, o.y | a.y, o.z | a.z, o.w | a.w);
                 }
                 st_nt4u(mask_words + (uint64_t)f * Mm + 4u * t, o);
             }
-            __syncthreads();
-        }
-        // q words: quad tq of the tile in q stream h sits at q position h Mm + 4 (tb + tq)
-        for (uint32_t i = threadIdx.x; i < r * kMsQuadsPerBlock; i += 64u * WPB) {
-            const uint32_t h = i / kMsQuadsPerBlock, tq = i % kMsQuadsPerBlock;
-            if (tb + tq < quads)
-                st_nt4u(words + (uint64_t)h * Mm + 4u * (tb + tq),
-                        make_uint4(qs[h][0][tq], qs[h][1][tq], qs[h][2][tq], qs[h][3][tq]));
         }
         __syncthreads();
     }

@@ -289,13 +289,17 @@ static MaskArg mask_arg(const uint32_t *w, const gc_lanes *ml, uint32_t count)
 }
 
 
-// dense fast path (ms_fast.h): aligned dense x, n < 2^32, every level <= 7 bits
+// dense fast path (ms_fast.h): aligned dense x, n < 2^32, the lowest level
+// <= 7 bits (its xi reaches s_0 and must fit the signed integer rounding), the
+// others <= 24 bits (s * 2^24 exact; their T saturates once xi >= 128, which
+// only ever means "not this level": fused_quad_fast)
 static bool ms_fast_ok(int mode, uint64_t n, const gc_levels *lv)
 {
-    return mode == 0 && n < (1ull << 32) && (lv->count == 2 || lv->count == 3) && lv->bits[lv->count - 1] <= 7;
+    return mode == 0 && n < (1ull << 32) && (lv->count == 2 || lv->count == 3) && lv->bits[0] <= 7 &&
+           lv->bits[lv->count - 1] <= 24;
 }
 
-// levels of 8-24 bits: the same wave-split kernels with generic rounding (MSV_WIDE)
+// a lowest level of 8-24 bits: the same wave-split kernels with generic rounding (MSV_WIDE)
 static bool ms_fast_wide_ok(int mode, uint64_t n, const gc_levels *lv)
 {
     return mode == 0 && n < (1ull << 32) && (lv->count == 2 || lv->count == 3) && lv->bits[lv->count - 1] <= 24;
@@ -400,14 +404,12 @@ int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_leve
     const RngArgs ra = rng_args_ms(rng, n);
     const MsFastArg fa = ms_fast_arg(levels);
     const uint32_t Mm = (uint32_t)mask_lanes->plane_words;
-    const uint32_t planes = std::min(32u, r * q_lanes->per_word);
-    const uint32_t kdiv = (65536u + r - 1) / r;
     const unsigned g = ms_grid(Mm >> 2);
     const bool wide = !ms_fast_ok(mode, n, levels);
     const int32_t qmax = (int32_t)q_lanes->offset;
 #define GC_FW(KIND_, NL_, VAR_)                                                                                   \
-    hipLaunchKernelGGL((k_ms_fused_w1<KIND_, NL_, VAR_>), dim3(g), dim3(kBlock), 0, st, x, (uint32_t)n, norm, la, \
-                       fa, ra, Mm, r, kdiv, planes, q_lanes->bits, qmax, mask_words, words)
+    hipLaunchKernelGGL((k_ms_fused_w1<KIND_, NL_, VAR_>), dim3(g), dim3(64 * r), 0, st, x, (uint32_t)n, norm, la, \
+                       fa, ra, Mm, r, q_lanes->per_word, q_lanes->bits, qmax, mask_words, words)
     if (levels->count == 2) {
         if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 2, MSV_WIDE); } else { GC_FW(0, 2, 0); } }
         else { if (wide) { GC_FW(1, 2, MSV_WIDE); } else { GC_FW(1, 2, 0); } }
