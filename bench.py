@@ -613,20 +613,32 @@ def main():
     pipe_ok = bool(torch.equal(wp[0], wp[2]) and torch.equal(wp[1], wp[3]))
     del wp
 
-    # ---- per-kernel HIP-event timing (roofline.achieved): each kernel in its own
-    # back-to-back loop, one event pair around the loop on the stream the codec
-    # launches on (torch's current stream).  No markers between launches: an
+    # ---- per-kernel HIP-event timing (roofline.achieved), on the stream the
+    # codec launches on (torch's current stream), one event pair per loop (an
     # event pair per launch inflated the kernel times by ~13 % at the driver's
-    # 20 steps, so the sum no longer fitted the timed step.  The
-    # encode loop reuses one global norm (the MAX is off this loop at N > 1)
-    # and consumes fresh draws every launch, exactly as in the step.
+    # 20 steps).  The encode is timed as it runs IN the step: the
+    # local step loop (absmax -> encode with the global norm) minus the
+    # absmax-only loop.  In the step the encode follows a full read of x by the
+    # absmax and finds its tail in the 256 MB Infinity Cache; back to back
+    # (encode_isolated) it does not, and takes ~8 % longer.  So absmax +
+    # encode = the step's GPU time, which the timed step's wall clock bounds.
     reps = max(K, 200)
+    nrm_scratch = torch.empty_like(norm)
     torch.cuda.synchronize()
-    ms_absmax = _events(torch, lambda: codec.absmax(x, out=norm), reps)
     if world > 1:
-        dist.all_reduce(norm, op=dist.ReduceOp.MAX)
-    ms_encode = _events(torch, encode_step, reps)
-    ms_step_events = _events(torch, step, reps) if world == 1 else None
+        codec.absmax(x, out=norm)
+        dist.all_reduce(norm, op=dist.ReduceOp.MAX)  # the encode's global norm, held fixed
+    ms_absmax = _events(torch, lambda: codec.absmax(x, out=nrm_scratch), reps)
+
+    def step_local():  # absmax -> encode, the MAX left out (N > 1: the encode keeps the global norm)
+        codec.absmax(x, out=nrm_scratch if world > 1 else norm)
+        encode_step()
+
+    ms_step_events = _events(torch, step_local, reps)
+    ms_absmax2 = _events(torch, lambda: codec.absmax(x, out=nrm_scratch), reps)
+    ms_absmax = 0.5 * (ms_absmax + ms_absmax2)  # bracketing the step loop (clock drift)
+    ms_encode = ms_step_events - ms_absmax
+    ms_encode_iso = _events(torch, encode_step, reps)
     enc_bytes = 4 * n + 4 * M  # read x once, write the packed words
     achieved = enc_bytes / (ms_encode * 1e-3) / 1e9
     step_bytes = 8 * n + 4 * M  # + the max-norm read of x
@@ -660,10 +672,13 @@ def main():
                      "traffic_source": _traffic("k_qsgd_encode", n, bits)[1],
                      "bytes_per_launch": enc_bytes, "ms_per_launch": ms_encode},
         "kernels_ms": {"k_absmax": ms_absmax, "k_qsgd_encode": ms_encode},
-        "kernel_timing": {"method": f"back-to-back loop of {reps} launches per kernel, one HIP event pair "
-                                    "around each loop on the codec's stream",
-                          "absmax_plus_encode_ms": ms_absmax + ms_encode,
+        "kernel_timing": {"method": f"HIP event pairs around {reps}-launch loops on the codec's stream: "
+                                    "k_absmax = absmax-only loop (before and after), k_qsgd_encode = "
+                                    "(absmax -> encode) step loop - absmax loop, i.e. the encode as it runs in "
+                                    "the step",
                           "step_events_ms": ms_step_events,
+                          "k_qsgd_encode_isolated_ms": ms_encode_iso,
+                          "absmax_plus_encode_ms": ms_absmax + ms_encode,
                           "fits_timed_step": ms_absmax + ms_encode <= ms_step},
     }
     if world > 1:

@@ -62,8 +62,9 @@ enum : int {
     MSV_PERTHREAD = 1,  // one thread walks all planes of its word quad (no wave split)
     MSV_NORNG = 2,      // measurement only: draws = a hash of the element index (no Philox)
     MSV_NOSLOW = 4,     // measurement only: no generic fallback (assumes every quad is fast)
-    MSV_WIDE = 8,       // levels of 8-24 bits (s * 2^24 >= 2^31): the wave-split kernels with the
-                        // generic per-element rounding (quot4_exact + xi_from_q) on every quad
+    MSV_WIDE = 8,       // a lowest level of 8-24 bits: the wave-split kernels with the generic
+                        // per-element rounding (quot4_exact + xi_from_q) on every quad
+    MSV_NOPF = 16,      // lab: the one-pass kernel without the next-plane prefetch
 };
 
 template <int KIND, int VAR>
@@ -107,6 +108,15 @@ __device__ __forceinline__ uint4 mask_levels4_fast(const MaskArg &mk, const Fast
 
 // T = floor(-|RN(q * S24)|) + (r & 0xFFFFFF); T >> 24 = -xi (qsgd_encode.h)
 __device__ __forceinline__ int32_t ms_t(float Ls, uint32_t r) { return add_low24(r, cvt_flr_neg_abs(Ls)); }
+// the same as volatile asm: evaluated where written, so a select between two
+// T values stays a v_cndmask instead of per-element exec-masked branches
+__device__ __forceinline__ int32_t ms_t_v(float Ls, uint32_t r)
+{
+    int32_t f, o;
+    asm volatile("v_cvt_flr_i32_f32_e64 %0, -|%1|" : "=v"(f) : "v"(Ls));
+    asm volatile("v_mad_u32_u24 %0, %1, 1, %2" : "=v"(o) : "v"(r), "v"(f));
+    return o;
+}
 
 // signed Markstein quotient pair RN(x / norm)
 __device__ __forceinline__ gc_f2 quot2_signed(float a, float b, const DivNorm &d)
@@ -272,6 +282,15 @@ __device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_
     } else {
         ql = quot4_exact(v, dv);
     }
+    // cache lanes: +-1 signs shared by the levels (0 for +-0, whose T is >= 0
+    // so the lane is qmax either way)
+    int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    if (CACHE && fast) {
+        s0 = med3_i32(__float_as_int(v.x), -1, 1);
+        s1 = med3_i32(__float_as_int(v.y), -1, 1);
+        s2 = med3_i32(__float_as_int(v.z), -1, 1);
+        s3 = med3_i32(__float_as_int(v.w), -1, 1);
+    }
 #pragma unroll
     for (int l = CACHE ? 0 : 1; l < NL; ++l) {
         const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);  // one draw block per level, either path
@@ -287,10 +306,22 @@ __device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_
                 m.w = t3 >= fa.thr ? (uint32_t)l : m.w;
             }
             if constexpr (CACHE) {
-                c.x |= lane_of_t(v.x, t0, cq) << sh;
-                c.y |= lane_of_t(v.y, t1, cq) << sh;
-                c.z |= lane_of_t(v.z, t2, cq) << sh;
-                c.w |= lane_of_t(v.w, t3, cq) << sh;
+                // -q = (T >> 24) * sign; level 0 has |q| <= s_0 <= cq (no clamp); the
+                // levels above are clamped (an unchosen level's cell field is never
+                // read, but must not spill into the next field)
+                const int32_t n0 = __mul24(t0 >> 24, s0), n1 = __mul24(t1 >> 24, s1);
+                const int32_t n2 = __mul24(t2 >> 24, s2), n3 = __mul24(t3 >> 24, s3);
+                if (l == 0) {
+                    c.x |= (uint32_t)(cq - n0) << sh;
+                    c.y |= (uint32_t)(cq - n1) << sh;
+                    c.z |= (uint32_t)(cq - n2) << sh;
+                    c.w |= (uint32_t)(cq - n3) << sh;
+                } else {
+                    c.x |= (uint32_t)(cq - med3_i32(n0, -cq, cq)) << sh;
+                    c.y |= (uint32_t)(cq - med3_i32(n1, -cq, cq)) << sh;
+                    c.z |= (uint32_t)(cq - med3_i32(n2, -cq, cq)) << sh;
+                    c.w |= (uint32_t)(cq - med3_i32(n3, -cq, cq)) << sh;
+                }
             }
         } else {
             const float s = lv.s[l];
@@ -482,7 +513,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict
     }
     constexpr int PW = (LM + 3) / 4;  // planes per wave
     __shared__ uint4 part[3][kMsQuadsPerBlock];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
         const uint32_t t = tb + lane;
         uint4 acc[NL - 1] = {};
@@ -556,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_fast(const float *__restri
     }
     constexpr int PW = (LQ + 3) / 4;
     __shared__ uint4 part[3][kMsQuadsPerBlock];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
         const uint32_t t = tb + lane;
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
@@ -602,7 +633,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
     const uint32_t quads = Mq >> 2;
     constexpr int PW = (LQ + 3) / 4;
     __shared__ uint4 part[3][kMsQuadsPerBlock];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
         const uint32_t t = tb + lane;
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
@@ -710,10 +741,11 @@ __device__ __forceinline__ void fused_quad_fast(const float4 &v, uint32_t i0, co
         const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
         const gc_f2 S = {fa.S24[0], fa.S24[0]};
         const gc_f2 a = q01 * S, b = q23 * S;
-        T.x = m.x == 0u ? ms_t(a.x, r.x) : T.x;
-        T.y = m.y == 0u ? ms_t(a.y, r.y) : T.y;
-        T.z = m.z == 0u ? ms_t(b.x, r.z) : T.z;
-        T.w = m.w == 0u ? ms_t(b.y, r.w) : T.w;
+        const int32_t w0 = ms_t_v(a.x, r.x), w1 = ms_t_v(a.y, r.y), w2 = ms_t_v(b.x, r.z), w3 = ms_t_v(b.y, r.w);
+        T.x = m.x == 0u ? w0 : T.x;
+        T.y = m.y == 0u ? w1 : T.y;
+        T.z = m.z == 0u ? w2 : T.z;
+        T.w = m.w == 0u ? w3 : T.w;
     }
 }
 
@@ -763,7 +795,7 @@ __device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint3
     RangeI rg;
     rg.add4(v);
     uint4 m;
-    if ((VAR & MSV_WIDE) == 0 && dv.fast && !rg.slow(lo2, hi2)) {
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
         int4 T;
         fused_quad_fast<KIND, NL, VAR>(v, i0, dv, fa, rng, m, T);
         acc.x += __mul24(T.x >> 24, med3_i32(__float_as_int(v.x), -sgk, sgk));
@@ -829,12 +861,17 @@ __global__ __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *
             // two planes in flight: plane k + 1's x is loaded before plane k's math
             uint32_t i0 = h * Mm + 4u * t;
             const uint32_t step = r * Mm;
-            float4 vn = load4_guard(x, i0, n);
+            float4 vn = (VAR & MSV_NOPF) != 0 ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : load4_guard(x, i0, n);
             auto plane = [&](uint32_t k, uint32_t sh, int4 &a) {
-                const float4 v = vn;
                 const uint32_t i0n = i0 + step;
-                if (k + 1 < kend)
-                    vn = load4_guard(x, i0n, n);
+                float4 v;
+                if constexpr ((VAR & MSV_NOPF) != 0) {
+                    v = load4_guard(x, i0, n);
+                } else {
+                    v = vn;
+                    if (k + 1 < kend)
+                        vn = load4_guard(x, i0n, n);
+                }
                 fused_plane_r<KIND, NL, VAR>(v, n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (h + r * k), 1 << sh, k * wq,
                                              macc, a, pl);
                 i0 = i0n;
@@ -922,7 +959,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode_fast(const uint32_t *__res
         return;
     }
     constexpr int PW = (LQ + 3) / 4;
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
         const uint32_t t = tb + lane;
         if (t >= quads)

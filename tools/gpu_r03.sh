@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-3 GPU evidence in one gpurun call.  Every GPU step has its own time
 # limit; a timeout, signal or fault (exit >= 124) ends the script, and so does a
-# failing smoke.  MODE: all | tests | bench | prof
+# failing smoke.  MODE: all | tests | bench | prof | lab, or a comma list
+# (e.g. lab,tests,bench)
 #   smoke -> pytest -m gpu -> bench (the driver's exact command) -> rocprofv3
 #   --kernel-trace --stats of that same command -> N=2 gloo rehearsal ->
 #   FETCH/WRITE PMC passes over the bench -> steady-state kernel workload
@@ -14,6 +15,7 @@ mkdir -p "$OUT"
 TAG=${1:-r03}
 MODE=${2:-all}
 DRIVER="bench.py --gpus 1 --steps 20 --warmup 5"
+has() { [ "$MODE" = all ] || [[ ",$MODE," == *",$1,"* ]]; }
 run() {  # name, timeout, cmd...
   local name=$1 t=$2; shift 2
   echo "== $name: $*" | tee -a "$OUT/steps_$TAG.log"
@@ -24,18 +26,22 @@ run() {  # name, timeout, cmd...
   if [ $rc -ge 124 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return $rc
 }
-if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
+if has lab; then
+  [ -x tools/lab_ms ] && { run lab_ms 200 tools/lab_ms || true; }
+  [ -x tools/lab2 ] && { run lab2 200 tools/lab2 || true; }
+fi
+if has tests; then
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
   run pytest_gpu 1500 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 240 --timeout-method thread -p no:cacheprovider
 fi
-if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+if has bench; then
   run bench 400 python3 $DRIVER
   cd /tmp && export TMPDIR=/tmp
   run rocprof_driver 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG/driver" -o run -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5
   cd "$ROOT"
   run gloo2 300 env GC_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 3 --cpu-seconds 0
 fi
-if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
+if has prof; then
   cd /tmp && export TMPDIR=/tmp
   B="$ROOT/bench.py --steps 10 --warmup 3 --cpu-seconds 0 --no-extras"
   KREGEX='k_qsgd_encode|k_absmax|k_qsgd_decode'

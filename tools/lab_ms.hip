@@ -337,9 +337,37 @@ int main(int argc, char **argv)
                       hipLaunchKernelGGL(k_sel_cache_nomask, dim3((Mq / 4 + 63) / 64), dim3(256), 0, 0, cache, n32, Mq,
                                          ql.bits, 3u, wq2);
                   }, cbytes + qb, {}});
+    // one-pass W = 1 encode (k_ms_fused_w1): product entry point and lab variants
+    const uint32_t rr = 32u / ql.per_word;
+    uint32_t *mw3, *wq3;
+    CK(hipMalloc(&mw3, (size_t)Mm * 4 + 64));
+    CK(hipMalloc(&wq3, (size_t)Mq * 4 + 64));
+    auto p_w1 = [&] { GK(gc_ms_encode_w1(x, n, norm, &lv, &rng, &ml, &ql, mw2, wq2, nullptr)); };
+    auto v_w1 = [&](auto kern) {
+        return [=] {
+            hipLaunchKernelGGL(kern, dim3((Mm / 4 + 63) / 64), dim3(64 * rr), 0, 0, x, n32, norm, la, fa, ra, Mm, rr,
+                               ql.per_word, ql.bits, qmax, mw3, wq3);
+        };
+    };
+    p_w1();
+    cmp("one-pass mask == two-pass", mw, mw2, (size_t)Mm * 4);
+    cmp("one-pass words == two-pass", wq, wq2, (size_t)Mq * 4);
+    v_w1(k_ms_fused_w1<0, 2, MSV_NOPF>)();
+    cmp("one-pass NOPF mask", mw, mw3, (size_t)Mm * 4);
+    cmp("one-pass NOPF words", wq, wq3, (size_t)Mq * 4);
+    vs.push_back({"product one-pass W=1 (mask + select)", p_w1, xb + mb + qb, {}});
+    vs.push_back({"lab one-pass NOPF", v_w1(k_ms_fused_w1<0, 2, MSV_NOPF>), xb + mb + qb, {}});
+    vs.push_back({"lab one-pass NORNG", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG>), xb + mb + qb, {}});
+    vs.push_back({"lab one-pass NORNG|NOSLOW", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG | MSV_NOSLOW>), xb + mb + qb, {}});
     vs.push_back({"product decode order 0", p_dec(0), xb + mb + qb, {}});
     vs.push_back({"product decode order 1", p_dec(1), xb + mb + qb, {}});
     vs.push_back({"product absmax", [&] { gc_absmax_f32(x, nullptr, n, norm, nullptr, nullptr); }, xb, {}});
+    for (auto &v : vs) {  // each variant once, synchronised, named first (a fault names its variant)
+        printf("run-check %s\n", v.name);
+        fflush(stdout);
+        v.f();
+        CK(hipDeviceSynchronize());
+    }
     for (int rep = 0; rep < 5; ++rep)
         for (auto &v : vs)
             v.t.push_back(T.run(v.f, 30));
