@@ -64,7 +64,7 @@ enum : int {
     MSV_NOSLOW = 4,     // measurement only: no generic fallback (assumes every quad is fast)
     MSV_WIDE = 8,       // a lowest level of 8-24 bits: the wave-split kernels with the generic
                         // per-element rounding (quot4_exact + xi_from_q) on every quad
-    MSV_NOPF = 16,      // lab: the one-pass kernel without the next-plane prefetch
+    MSV_DEFER = 16,     // lab: the one-pass kernel with the generic path deferred to after the plane loop
 };
 
 template <int KIND, int VAR>
@@ -258,64 +258,59 @@ __device__ __forceinline__ uint4 cache_cells(const uint2 &u)
 // ---------------------------------------------------------------------------
 // per-plane work (4 elements i0..i0+3 of one plane)
 // ---------------------------------------------------------------------------
-// resolution levels (0 past n).  CACHE: also every level's lane value into
+// resolution levels of 4 elements as thermometer bits: mb[f] = bit or 0 per
+// element for [m > f] (0 past n).  CACHE: also every level's lane value into
 // *cv (field l at bit l*cb, clamped to +-cq), from the same draws and the same
 // fast / generic decision as select_plane, so a cell field equals the lane
-// the select would compute at that level.
+// the select would compute at that level.  The fast and generic paths are
+// whole branches (each with its own draws), so the common fast path carries
+// no per-level divergence.
 template <int KIND, int NL, int VAR = 0, bool CACHE = false>
-__device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_t n, uint32_t i0, const DivNorm &dv,
-                                            uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
-                                            const RngArgs &rng, int32_t cq = 0, uint32_t cb = 0,
-                                            uint4 *cv = nullptr)
+__device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                           uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                           const RngArgs &rng, uint32_t bit, uint4 (&mb)[NL - 1], int32_t cq = 0,
+                                           uint32_t cb = 0, uint4 *cv = nullptr)
 {
     const float4 v = load4_nt_tail<0>(x, i0, n);
     RangeI rg;
     rg.add4(v);
-    const bool fast = (VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)));
-    uint4 m = make_uint4(0u, 0u, 0u, 0u);
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
-    gc_f2 q01, q23;
-    float4 ql;
-    if (fast) {
-        q01 = quot2_signed(v.x, v.y, dv);
-        q23 = quot2_signed(v.z, v.w, dv);
-    } else {
-        ql = quot4_exact(v, dv);
-    }
-    // cache lanes: +-1 signs shared by the levels (0 for +-0, whose T is >= 0
-    // so the lane is qmax either way)
-    int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    if (CACHE && fast) {
-        s0 = med3_i32(__float_as_int(v.x), -1, 1);
-        s1 = med3_i32(__float_as_int(v.y), -1, 1);
-        s2 = med3_i32(__float_as_int(v.z), -1, 1);
-        s3 = med3_i32(__float_as_int(v.w), -1, 1);
-    }
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
+        const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+        // cache lanes: -q = (T >> 24) * sign (0 for +-0, whose T is >= 0)
+        int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        if constexpr (CACHE) {
+            s0 = med3_i32(__float_as_int(v.x), -1, 1);
+            s1 = med3_i32(__float_as_int(v.y), -1, 1);
+            s2 = med3_i32(__float_as_int(v.z), -1, 1);
+            s3 = med3_i32(__float_as_int(v.w), -1, 1);
+        }
+        bool k0 = false, k1 = false, k2 = false, k3 = false;  // some level >= l qualifies
 #pragma unroll
-    for (int l = CACHE ? 0 : 1; l < NL; ++l) {
-        const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);  // one draw block per level, either path
-        const uint32_t sh = (uint32_t)l * cb;
-        if (fast) {
+        for (int l = NL - 1; l >= (CACHE ? 0 : 1); --l) {
+            const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
             const gc_f2 S = {fa.S24[l], fa.S24[l]};
             const gc_f2 a = q01 * S, b = q23 * S;
             const int32_t t0 = ms_t(a.x, r.x), t1 = ms_t(a.y, r.y), t2 = ms_t(b.x, r.z), t3 = ms_t(b.y, r.w);
             if (l > 0) {
-                m.x = t0 >= fa.thr ? (uint32_t)l : m.x;
-                m.y = t1 >= fa.thr ? (uint32_t)l : m.y;
-                m.z = t2 >= fa.thr ? (uint32_t)l : m.z;
-                m.w = t3 >= fa.thr ? (uint32_t)l : m.w;
+                k0 = k0 || t0 >= fa.thr;
+                k1 = k1 || t1 >= fa.thr;
+                k2 = k2 || t2 >= fa.thr;
+                k3 = k3 || t3 >= fa.thr;
+                mb[l - 1] = make_uint4(k0 ? bit : 0u, k1 ? bit : 0u, k2 ? bit : 0u, k3 ? bit : 0u);
             }
             if constexpr (CACHE) {
-                // -q = (T >> 24) * sign; level 0 has |q| <= s_0 <= cq (no clamp); the
-                // levels above are clamped (an unchosen level's cell field is never
-                // read, but must not spill into the next field)
+                // level 0 has |q| <= s_0 <= cq (no clamp); the levels above are
+                // clamped (an unchosen level's field is never read, but must not
+                // spill into the next field)
+                const uint32_t sh = (uint32_t)l * cb;
                 const int32_t n0 = __mul24(t0 >> 24, s0), n1 = __mul24(t1 >> 24, s1);
                 const int32_t n2 = __mul24(t2 >> 24, s2), n3 = __mul24(t3 >> 24, s3);
                 if (l == 0) {
-                    c.x |= (uint32_t)(cq - n0) << sh;
-                    c.y |= (uint32_t)(cq - n1) << sh;
-                    c.z |= (uint32_t)(cq - n2) << sh;
-                    c.w |= (uint32_t)(cq - n3) << sh;
+                    c.x |= (uint32_t)(cq - n0);
+                    c.y |= (uint32_t)(cq - n1);
+                    c.z |= (uint32_t)(cq - n2);
+                    c.w |= (uint32_t)(cq - n3);
                 } else {
                     c.x |= (uint32_t)(cq - med3_i32(n0, -cq, cq)) << sh;
                     c.y |= (uint32_t)(cq - med3_i32(n1, -cq, cq)) << sh;
@@ -323,7 +318,13 @@ __device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_
                     c.w |= (uint32_t)(cq - med3_i32(n3, -cq, cq)) << sh;
                 }
             }
-        } else {
+        }
+    } else {
+        const float4 ql = quot4_exact(v, dv);
+        uint4 m = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int l = CACHE ? 0 : 1; l < NL; ++l) {
+            const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
             const float s = lv.s[l];
             const int32_t x0 = xi_from_q(ql.x, s, r.x), x1 = xi_from_q(ql.y, s, r.y);
             const int32_t x2 = xi_from_q(ql.z, s, r.z), x3 = xi_from_q(ql.w, s, r.w);
@@ -334,21 +335,41 @@ __device__ __forceinline__ uint4 mask_plane(const float *__restrict__ x, uint32_
                 m.w = x3 <= lv.maxv ? (uint32_t)l : m.w;
             }
             if constexpr (CACHE) {
+                const uint32_t sh = (uint32_t)l * cb;
                 c.x |= lane_of_q(sgn_of(v.x) * x0, cq) << sh;
                 c.y |= lane_of_q(sgn_of(v.y) * x1, cq) << sh;
                 c.z |= lane_of_q(sgn_of(v.z) * x2, cq) << sh;
                 c.w |= lane_of_q(sgn_of(v.w) * x3, cq) << sh;
             }
         }
+#pragma unroll
+        for (int f = 0; f < NL - 1; ++f)
+            mb[f] = make_uint4(m.x > (uint32_t)f ? bit : 0u, m.y > (uint32_t)f ? bit : 0u,
+                               m.z > (uint32_t)f ? bit : 0u, m.w > (uint32_t)f ? bit : 0u);
     }
     if (i0 + 4 > n) {
-        m.y = i0 + 1 < n ? m.y : 0u;
-        m.z = i0 + 2 < n ? m.z : 0u;
-        m.w = i0 + 3 < n ? m.w : 0u;
+#pragma unroll
+        for (int f = 0; f < NL - 1; ++f) {
+            mb[f].y = i0 + 1 < n ? mb[f].y : 0u;
+            mb[f].z = i0 + 2 < n ? mb[f].z : 0u;
+            mb[f].w = i0 + 3 < n ? mb[f].w : 0u;
+        }
     }
     if constexpr (CACHE)
         *cv = c;
-    return m;
+}
+
+// OR the per-element bits of mask_plane into the field accumulators
+template <int NL>
+__device__ __forceinline__ void mask_or(uint4 (&acc)[NL - 1], const uint4 (&mb)[NL - 1])
+{
+#pragma unroll
+    for (int f = 0; f < NL - 1; ++f) {
+        acc[f].x |= mb[f].x;
+        acc[f].y |= mb[f].y;
+        acc[f].z |= mb[f].z;
+        acc[f].w |= mb[f].w;
+    }
 }
 
 // thermometer bits [m > f] of 4 elements into the field accumulators
@@ -503,7 +524,9 @@ __global__ __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict
                 const uint32_t i0 = (uint32_t)j * M + 4u * t;
                 if (i0 >= n)
                     break;
-                mask_bits<NL>(acc, mask_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng), (uint32_t)j * w);
+                uint4 mb[NL - 1];
+                mask_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng, 1u << ((uint32_t)j * w), mb);
+                mask_or<NL>(acc, mb);
             }
 #pragma unroll
             for (int f = 0; f < NL - 1; ++f)
@@ -527,12 +550,14 @@ __global__ __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict
                 if (i0 >= n)
                     break;
                 if constexpr (CBY != 0) {
-                    uint4 cv;
-                    const uint4 m = mask_plane<KIND, NL, VAR, true>(x, n, i0, dv, lo2, hi2, lv, fa, rng, cq, cb, &cv);
+                    uint4 cv, mb[NL - 1];
+                    mask_plane<KIND, NL, VAR, true>(x, n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (p * w), mb, cq, cb, &cv);
                     cache_store<CBY>(cache, i0, n, cv);
-                    mask_bits<NL>(acc, m, p * w);
+                    mask_or<NL>(acc, mb);
                 } else {
-                    mask_bits<NL>(acc, mask_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng), p * w);
+                    uint4 mb[NL - 1];
+                    mask_plane<KIND, NL, VAR>(x, n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (p * w), mb);
+                    mask_or<NL>(acc, mb);
                 }
             }
         }
@@ -710,54 +735,67 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
 // LDS traffic for the q lanes; only the mask words (one bit per plane) are
 // OR-ed across the r waves.  The plane index is wave-uniform (scalar).
 // ---------------------------------------------------------------------------
-// fast path of 4 elements: the level m of each (uint4) and T at that level
-// (T >> 24 = -xi, ms_t).  Levels above 0 may exceed 7 bits: their T saturates
-// (v_cvt_flr_i32_f32 clamps) once |Ls| > 2^31, i.e. xi >= 128 > maxv, which is
-// exactly "not this level"; a level is only ever chosen with xi <= maxv <= 127.
+// fast path of 4 elements: the thermometer bits (field f = [m > f], as bitP
+// or 0) and -q at the chosen level m.  T at level l is ms_t (T >> 24 = -xi);
+// levels above 0 may exceed 7 bits: their T saturates (v_cvt_flr_i32_f32
+// clamps) once |Ls| > 2^31, i.e. xi >= 128 > maxv, which is exactly "not this
+// level"; a level is only ever chosen with xi <= maxv <= 127, so the chosen
+// T >> 24 is a sign-extended byte.  -q = (T >> 24) * sign(x) (0 for +-0,
+// whose T is >= 0 anyway).
 template <int KIND, int NL, int VAR = 0>
 __device__ __forceinline__ void fused_quad_fast(const float4 &v, uint32_t i0, const DivNorm &dv, const MsFastArg &fa,
-                                                const RngArgs &rng, uint4 &m, int4 &T)
+                                                const RngArgs &rng, uint32_t bitP, uint4 (&mb)[NL - 1], int4 &nq)
 {
     const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
-    m = make_uint4(0u, 0u, 0u, 0u);
-    T = make_int4(0, 0, 0, 0);
+    int4 T;
+    bool k0 = false, k1 = false, k2 = false, k3 = false;  // some level >= 1 qualifies
 #pragma unroll
-    for (int l = 1; l < NL; ++l) {
+    for (int l = NL - 1; l >= 1; --l) {  // the highest qualifying level wins
         const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
         const gc_f2 S = {fa.S24[l], fa.S24[l]};
         const gc_f2 a = q01 * S, b = q23 * S;
-        const int32_t u0 = ms_t(a.x, r.x), u1 = ms_t(a.y, r.y), u2 = ms_t(b.x, r.z), u3 = ms_t(b.y, r.w);
+        const int32_t u0 = ms_t_v(a.x, r.x), u1 = ms_t_v(a.y, r.y), u2 = ms_t_v(b.x, r.z), u3 = ms_t_v(b.y, r.w);
         const bool c0 = u0 >= fa.thr, c1 = u1 >= fa.thr, c2 = u2 >= fa.thr, c3 = u3 >= fa.thr;
-        m.x = c0 ? (uint32_t)l : m.x;
-        m.y = c1 ? (uint32_t)l : m.y;
-        m.z = c2 ? (uint32_t)l : m.z;
-        m.w = c3 ? (uint32_t)l : m.w;
-        T.x = c0 ? u0 : T.x;
-        T.y = c1 ? u1 : T.y;
-        T.z = c2 ? u2 : T.z;
-        T.w = c3 ? u3 : T.w;
+        if (l == NL - 1) {
+            T = make_int4(u0, u1, u2, u3);
+        } else {
+            T.x = k0 ? T.x : u0;
+            T.y = k1 ? T.y : u1;
+            T.z = k2 ? T.z : u2;
+            T.w = k3 ? T.w : u3;
+        }
+        k0 = k0 || c0;
+        k1 = k1 || c1;
+        k2 = k2 || c2;
+        k3 = k3 || c3;
+        // field f = l - 1: [m >= l] = some level >= l qualifies
+        mb[l - 1] = make_uint4(k0 ? bitP : 0u, k1 ? bitP : 0u, k2 ? bitP : 0u, k3 ? bitP : 0u);
     }
-    if (m.x == 0u || m.y == 0u || m.z == 0u || m.w == 0u) {  // level 0's draws only when needed
+    if (!(k0 && k1 && k2 && k3)) {  // level 0's draws only when an element stays there
         const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
         const gc_f2 S = {fa.S24[0], fa.S24[0]};
         const gc_f2 a = q01 * S, b = q23 * S;
         const int32_t w0 = ms_t_v(a.x, r.x), w1 = ms_t_v(a.y, r.y), w2 = ms_t_v(b.x, r.z), w3 = ms_t_v(b.y, r.w);
-        T.x = m.x == 0u ? w0 : T.x;
-        T.y = m.y == 0u ? w1 : T.y;
-        T.z = m.z == 0u ? w2 : T.z;
-        T.w = m.w == 0u ? w3 : T.w;
+        T.x = k0 ? T.x : w0;
+        T.y = k1 ? T.y : w1;
+        T.z = k2 ? T.z : w2;
+        T.w = k3 ? T.w : w3;
     }
+    nq.x = __mul24(T.x >> 24, med3_i32(__float_as_int(v.x), -1, 1));
+    nq.y = __mul24(T.y >> 24, med3_i32(__float_as_int(v.y), -1, 1));
+    nq.z = __mul24(T.z >> 24, med3_i32(__float_as_int(v.z), -1, 1));
+    nq.w = __mul24(T.w >> 24, med3_i32(__float_as_int(v.w), -1, 1));
 }
 
 // generic path of 4 elements (range-check failures, norms outside the
-// Markstein range, MSV_WIDE): levels and signed q at them
+// Markstein range, MSV_WIDE): the same bits and -q from the per-element rounding
 template <int KIND, int NL, int VAR = 0>
 __device__ __forceinline__ void fused_quad_slow(const float4 &v, uint32_t i0, const DivNorm &dv, const LevelsArg &lv,
-                                                const RngArgs &rng, uint4 &m, int4 &q)
+                                                const RngArgs &rng, uint32_t bitP, uint4 (&mb)[NL - 1], int4 &nq)
 {
     const float4 ql = quot4_exact(v, dv);
-    m = make_uint4(0u, 0u, 0u, 0u);
-    q = make_int4(0, 0, 0, 0);
+    uint4 m = make_uint4(0u, 0u, 0u, 0u);
+    int4 q = make_int4(0, 0, 0, 0);
 #pragma unroll
     for (int l = 1; l < NL; ++l) {
         const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
@@ -777,52 +815,59 @@ __device__ __forceinline__ void fused_quad_slow(const float4 &v, uint32_t i0, co
         q.z = m.z == 0u ? sgn_of(v.z) * xi_from_q(ql.z, s, r.z) : q.z;
         q.w = m.w == 0u ? sgn_of(v.w) * xi_from_q(ql.w, s, r.w) : q.w;
     }
+#pragma unroll
+    for (int f = 0; f < NL - 1; ++f)
+        mb[f] = make_uint4(m.x > (uint32_t)f ? bitP : 0u, m.y > (uint32_t)f ? bitP : 0u,
+                           m.z > (uint32_t)f ? bitP : 0u, m.w > (uint32_t)f ? bitP : 0u);
+    nq = make_int4(-q.x, -q.y, -q.z, -q.w);
 }
 
 constexpr uint32_t kMsFusedMaxR = 8;  // q words per mask word at W = 1: 32 / (q lanes per word) <= 8
 
-// one plane of the fused encode: levels into the mask fields, the lane into
-// the wave's q word accumulators.  Fast lanes: acc -= (T >> 24) * (+-2^sh)
-// (word = Cw - acc, as enc_tile_int; the 24-bit multiplier keeps sh <= 15 by
-// splitting the lanes into lo (k < H) and hi (k >= H, shifted by H wq at the
-// end)); generic lanes: pl += q << (k wq) (modular: lane = qmax + q).
-template <int KIND, int NL, int VAR>
-__device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
-                                              uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
-                                              const RngArgs &rng, uint32_t bitP, int32_t sgk, uint32_t shk,
-                                              uint4 (&macc)[NL - 1], int4 &acc, uint4 &pl)
+// one plane of the fused encode: the thermometer bits into the mask fields,
+// -q * 2^(k wq) into the wave's q word accumulator (word = C - acc, modular:
+// lane = qmax + q).  Elements past n have x = 0 (no lane) and no mask bit.
+template <int NL>
+__device__ __forceinline__ void fused_accumulate(uint32_t n, uint32_t i0, uint32_t sh, uint4 (&mb)[NL - 1],
+                                                 const int4 &nq, uint4 (&macc)[NL - 1], uint4 &acc)
 {
-    RangeI rg;
-    rg.add4(v);
-    uint4 m;
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
-        int4 T;
-        fused_quad_fast<KIND, NL, VAR>(v, i0, dv, fa, rng, m, T);
-        acc.x += __mul24(T.x >> 24, med3_i32(__float_as_int(v.x), -sgk, sgk));
-        acc.y += __mul24(T.y >> 24, med3_i32(__float_as_int(v.y), -sgk, sgk));
-        acc.z += __mul24(T.z >> 24, med3_i32(__float_as_int(v.z), -sgk, sgk));
-        acc.w += __mul24(T.w >> 24, med3_i32(__float_as_int(v.w), -sgk, sgk));
-    } else {
-        int4 q;
-        fused_quad_slow<KIND, NL, VAR>(v, i0, dv, lv, rng, m, q);
-        pl.x += (uint32_t)q.x << shk;
-        pl.y += (uint32_t)q.y << shk;
-        pl.z += (uint32_t)q.z << shk;
-        pl.w += (uint32_t)q.w << shk;
-    }
-    if (i0 + 4 > n) {  // elements past n: no mask bit (their x = 0 adds no lane)
-        m.x = i0 < n ? m.x : 0u;
-        m.y = i0 + 1 < n ? m.y : 0u;
-        m.z = i0 + 2 < n ? m.z : 0u;
-        m.w = i0 + 3 < n ? m.w : 0u;
+    if (i0 + 4 > n) {
+#pragma unroll
+        for (int f = 0; f < NL - 1; ++f) {
+            mb[f].x = i0 < n ? mb[f].x : 0u;
+            mb[f].y = i0 + 1 < n ? mb[f].y : 0u;
+            mb[f].z = i0 + 2 < n ? mb[f].z : 0u;
+            mb[f].w = i0 + 3 < n ? mb[f].w : 0u;
+        }
     }
 #pragma unroll
     for (int f = 0; f < NL - 1; ++f) {
-        macc[f].x |= m.x > (uint32_t)f ? bitP : 0u;
-        macc[f].y |= m.y > (uint32_t)f ? bitP : 0u;
-        macc[f].z |= m.z > (uint32_t)f ? bitP : 0u;
-        macc[f].w |= m.w > (uint32_t)f ? bitP : 0u;
+        macc[f].x |= mb[f].x;
+        macc[f].y |= mb[f].y;
+        macc[f].z |= mb[f].z;
+        macc[f].w |= mb[f].w;
     }
+    acc.x += (uint32_t)nq.x << sh;
+    acc.y += (uint32_t)nq.y << sh;
+    acc.z += (uint32_t)nq.z << sh;
+    acc.w += (uint32_t)nq.w << sh;
+}
+
+template <int KIND, int NL, int VAR>
+__device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                              uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                              const RngArgs &rng, uint32_t bitP, uint32_t sh,
+                                              uint4 (&macc)[NL - 1], uint4 &acc)
+{
+    RangeI rg;
+    rg.add4(v);
+    uint4 mb[NL - 1];
+    int4 nq;
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2))))
+        fused_quad_fast<KIND, NL, VAR>(v, i0, dv, fa, rng, bitP, mb, nq);
+    else
+        fused_quad_slow<KIND, NL, VAR>(v, i0, dv, lv, rng, bitP, mb, nq);
+    fused_accumulate<NL>(n, i0, sh, mb, nq, macc, acc);
 }
 
 __device__ __forceinline__ float4 load4_guard(const float *__restrict__ x, uint32_t i0, uint32_t n)
@@ -844,7 +889,6 @@ __global__ __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *
     const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
     const uint32_t quads = Mm >> 2;
     const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const uint32_t H = Lq >> 1;  // lanes k < H in lo, k >= H in hi
     uint32_t Cw = 0;
     for (uint32_t k = 0; k < Lq; ++k)
         Cw += (uint32_t)qmax << (k * wq);
@@ -855,38 +899,26 @@ __global__ __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
         const uint32_t t = tb + lane;
         uint4 macc[NL - 1] = {};
-        int4 lo = make_int4(0, 0, 0, 0), hi = make_int4(0, 0, 0, 0);
-        uint4 pl = make_uint4(0u, 0u, 0u, 0u);
+        uint4 acc = make_uint4(0u, 0u, 0u, 0u);
         if (t < quads && kend > 0) {
-            // two planes in flight: plane k + 1's x is loaded before plane k's math
             uint32_t i0 = h * Mm + 4u * t;
             const uint32_t step = r * Mm;
-            float4 vn = (VAR & MSV_NOPF) != 0 ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : load4_guard(x, i0, n);
-            auto plane = [&](uint32_t k, uint32_t sh, int4 &a) {
-                const uint32_t i0n = i0 + step;
-                float4 v;
-                if constexpr ((VAR & MSV_NOPF) != 0) {
-                    v = load4_guard(x, i0, n);
-                } else {
-                    v = vn;
-                    if (k + 1 < kend)
-                        vn = load4_guard(x, i0n, n);
-                }
-                fused_plane_r<KIND, NL, VAR>(v, n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (h + r * k), 1 << sh, k * wq,
-                                             macc, a, pl);
-                i0 = i0n;
+            // planes below pend - 1 are full for every lane (their end (P + 1) Mm
+            // <= (pend - 1) Mm < n): plain 16-byte loads, no per-lane guard
+            auto load = [&](uint32_t k, uint32_t i) {
+                return h + r * k + 1 < pend ? ld_nt(reinterpret_cast<const float4 *>(x + i)) : load4_guard(x, i, n);
             };
-            const uint32_t kmid = min(H, kend);
+            // one plane at a time (a next-plane register prefetch measured the
+            // same: the waves of the CU hide the load latency)
 #pragma unroll 1
-            for (uint32_t k = 0; k < kmid; ++k)
-                plane(k, k * wq, lo);
-#pragma unroll 1
-            for (uint32_t k = H; k < kend; ++k)
-                plane(k, (k - H) * wq, hi);
+            for (uint32_t k = 0; k < kend; ++k) {
+                fused_plane_r<KIND, NL, VAR>(load(k, i0), n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (h + r * k), k * wq,
+                                             macc, acc);
+                i0 += step;
+            }
         }
         // q words of stream h: quad t at j0 = h Mm + 4t, lane k = element j0 + e + k Mq
         if (t < quads) {
-            const uint32_t hs = H * wq;
             const uint64_t j0 = (uint64_t)h * Mm + 4u * t, Mq = (uint64_t)r * Mm;
             uint4 C = make_uint4(Cw, Cw, Cw, Cw);
             if (j0 + 3 + (uint64_t)(Lq - 1) * Mq >= n) {  // lanes of elements past n stay 0
@@ -900,10 +932,7 @@ __global__ __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *
                     C.w += e + 3 < n ? c : 0u;
                 }
             }
-            st_nt4u(words + j0, make_uint4(C.x - ((uint32_t)lo.x + ((uint32_t)hi.x << hs)) + pl.x,
-                                           C.y - ((uint32_t)lo.y + ((uint32_t)hi.y << hs)) + pl.y,
-                                           C.z - ((uint32_t)lo.z + ((uint32_t)hi.z << hs)) + pl.z,
-                                           C.w - ((uint32_t)lo.w + ((uint32_t)hi.w << hs)) + pl.w));
+            st_nt4u(words + j0, make_uint4(C.x - acc.x, C.y - acc.y, C.z - acc.z, C.w - acc.w));
         }
         // mask words: OR of the r waves' plane bits
         if (h)

@@ -749,6 +749,7 @@ def _torch_state_to(device) -> torch.Tensor:
     h[:624] = words
     h[624] = idx
     dst.copy_(hin, non_blocking=True)
+    _MT_LAST.pop(device.index, None)  # dst now follows this call, not the draw path's record
     return dst
 
 
@@ -809,15 +810,64 @@ def qsgd_encode_torch(x, norm, bits, world=1, out=None, lanes=None) -> torch.Ten
     return out
 
 
+_MT_SIDE = {}  # device index -> the side stream torch-mode draws are generated on
+_MT_LAST = {}  # device index -> (624 words, read index) last written back to torch == the device state
+
+
+def _mt_side(device) -> torch.cuda.Stream:
+    """High priority: the draw generation is the serial chain of the torch-mode
+    encode; the encodes it overlaps fill the CUs it leaves idle."""
+    s = _MT_SIDE.get(device.index)
+    if s is None:
+        lo, hi = torch.cuda.Stream.priority_range()
+        s = _MT_SIDE[device.index] = torch.cuda.Stream(device, priority=min(lo, hi))
+    return s
+
+
 def mt19937_draws(count: int, device) -> torch.Tensor:
     """`count` draws of torch's CPU generator, produced on `device`; torch's
-    generator state advances exactly as torch.bernoulli would advance it."""
+    generator state advances exactly as torch.bernoulli would advance it
+    (synchronously: the new state is in torch's generator when this returns).
+
+    The draws are generated on a side stream (gc_mt19937_generate_jumped: the
+    LDS-bound jump and the latency-bound generators) that the caller's stream
+    waits on, and the host waits only for that side stream, never for the
+    caller's queued work: the encode of call i (HBM-bound, on the caller's
+    stream) runs under the generation of call i + 1.  The state goes to the
+    device only when torch's generator differs from what the last call wrote
+    back (the device buffer already holds that state)."""
+    from .rng import set_torch_mt_state, torch_mt_state
+
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     if device.index is None:
         device = torch.device("cuda", torch.cuda.current_device())
-    st_dev = _torch_state_to(device)
-    out = mt19937_generate(st_dev, count)
-    _torch_state_back(st_dev)
+    words, idx = torch_mt_state()
+    bufs = _MT_PIN.get(device.index)
+    if bufs is None:
+        bufs = _MT_PIN[device.index] = (torch.empty(625, dtype=torch.int32).pin_memory(),
+                                        torch.empty(625, dtype=torch.int32).pin_memory(),
+                                        torch.empty(625, dtype=torch.int32, device=device))
+    hin, hout, dst = bufs
+    cur = torch.cuda.current_stream(device)
+    side = _mt_side(device)
+    last = _MT_LAST.get(device.index)
+    with torch.cuda.stream(side):
+        if last is None or last[1] != idx or not np.array_equal(last[0], words):
+            h = hin.numpy().view(np.uint32)  # free: the previous call waited for its copies
+            h[:624] = words
+            h[624] = idx
+            dst.copy_(hin, non_blocking=True)
+        out = mt19937_generate(dst, count)
+        hout.copy_(dst, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(side)
+    cur.wait_event(done)
+    out.record_stream(cur)
+    done.synchronize()
+    new = hout.numpy().view(np.uint32)
+    w2, i2 = new[:624].copy(), int(new[624])
+    set_torch_mt_state(w2, i2)
+    _MT_LAST[device.index] = (w2, i2)
     return out
 
 

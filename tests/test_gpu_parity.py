@@ -892,7 +892,7 @@ def test_randk_fused_w1_torch_stream_and_edges():
     assert bits_eq(u32(w2), O.qsgd_encode(x2[idx], np.float32(np.nan), bits, 1, O.philox_rng(3, 29)))
 
 
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("K", [7, 10_000, 262_144])
 def test_randk_gather_then_dense_encode(world, K):
     """W > 1 path: gc_randk_gather_absmax (subset + local norm, one launch),

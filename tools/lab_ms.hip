@@ -64,12 +64,14 @@ __global__ __launch_bounds__(256) void k_read_nt(const float4 *x, uint64_t n4, u
 
 // select-like pattern: L planes of x -> one packed word quad
 template <int L>
-__global__ __launch_bounds__(256) void k_rw_planar(const float *x, uint32_t M, uint32_t *words)
+__global__ __launch_bounds__(256) void k_rw_planar(const float *x, uint32_t M, uint32_t *words, uint32_t n)
 {
     for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < (M >> 2); t += gridDim.x * 256u) {
         uint4 acc = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int k = 0; k < L; ++k) {
+            if (k * M + 4 * t + 4 > n)  // planes past the bucket (the coupled W = 1 mask layout pads to 32)
+                break;
             const float4 v = ld_nt(reinterpret_cast<const float4 *>(x + k * M + 4 * t));
             acc.x ^= __float_as_uint(v.x);
             acc.y ^= __float_as_uint(v.y);
@@ -82,12 +84,13 @@ __global__ __launch_bounds__(256) void k_rw_planar(const float *x, uint32_t M, u
 
 // decode-like pattern: one word quad -> L planes of floats
 template <int L>
-__global__ __launch_bounds__(256) void k_wr_planar(const uint32_t *words, uint32_t M, float *out)
+__global__ __launch_bounds__(256) void k_wr_planar(const uint32_t *words, uint32_t M, float *out, uint32_t n)
 {
     for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < (M >> 2); t += gridDim.x * 256u) {
         const uint4 w = *reinterpret_cast<const uint4 *>(words + 4 * t);
 #pragma unroll
         for (int k = 0; k < L; ++k)
+            if (k * M + 4 * t + 4 <= n)  // padded planes end past the bucket
             st_nt4(out + k * M + 4 * t, make_float4((float)(w.x >> k), (float)(w.y >> k), (float)(w.z >> k),
                                                     (float)(w.w >> k)));
     }
@@ -291,13 +294,13 @@ int main(int argc, char **argv)
                       hipLaunchKernelGGL(k_read_nt, dim3(4096), dim3(256), 0, 0, (const float4 *)x, n / 4, scratch);
                   }, xb, {}});
     vs.push_back({"roof: 10 planes -> words (select pattern)", [&] {
-                      hipLaunchKernelGGL(k_rw_planar<10>, dim3(grid(Mq / 4)), dim3(256), 0, 0, x, Mq, wq2);
+                      hipLaunchKernelGGL(k_rw_planar<10>, dim3(grid(Mq / 4)), dim3(256), 0, 0, x, Mq, wq2, n32);
                   }, xb + qb, {}});
     vs.push_back({"roof: 32 planes -> words (mask pattern)", [&] {
-                      hipLaunchKernelGGL(k_rw_planar<32>, dim3(grid(Mm / 4)), dim3(256), 0, 0, x, Mm, mw2);
+                      hipLaunchKernelGGL(k_rw_planar<32>, dim3(grid(Mm / 4)), dim3(256), 0, 0, x, Mm, mw2, n32);
                   }, xb + mb, {}});
     vs.push_back({"roof: words -> 10 planes (decode pattern)", [&] {
-                      hipLaunchKernelGGL(k_wr_planar<10>, dim3(grid(Mq / 4)), dim3(256), 0, 0, wq, Mq, out2);
+                      hipLaunchKernelGGL(k_wr_planar<10>, dim3(grid(Mq / 4)), dim3(256), 0, 0, wq, Mq, out2, n32);
                   }, xb + qb, {}});
     vs.push_back({"product mask encode", p_mask, xb + mb, {}});
     vs.push_back({"lab mask split", v_mask64(k_ms_mask_fast<32, 0, 2, 0>, mw2), xb + mb, {}});
@@ -352,11 +355,8 @@ int main(int argc, char **argv)
     p_w1();
     cmp("one-pass mask == two-pass", mw, mw2, (size_t)Mm * 4);
     cmp("one-pass words == two-pass", wq, wq2, (size_t)Mq * 4);
-    v_w1(k_ms_fused_w1<0, 2, MSV_NOPF>)();
-    cmp("one-pass NOPF mask", mw, mw3, (size_t)Mm * 4);
-    cmp("one-pass NOPF words", wq, wq3, (size_t)Mq * 4);
+    v_w1(k_ms_fused_w1<0, 2, MSV_NORNG>)();  // (lab variant: a different stream, run for the timing only)
     vs.push_back({"product one-pass W=1 (mask + select)", p_w1, xb + mb + qb, {}});
-    vs.push_back({"lab one-pass NOPF", v_w1(k_ms_fused_w1<0, 2, MSV_NOPF>), xb + mb + qb, {}});
     vs.push_back({"lab one-pass NORNG", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG>), xb + mb + qb, {}});
     vs.push_back({"lab one-pass NORNG|NOSLOW", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG | MSV_NOSLOW>), xb + mb + qb, {}});
     vs.push_back({"product decode order 0", p_dec(0), xb + mb + qb, {}});

@@ -46,3 +46,19 @@ for cnt in (10_000_000, 23_520_842 * 2, 100_000_000):
         torch.cuda.synchronize()
         print(f"mt19937 {cnt} draws, J = {J} ({-(-cnt // J)} generators): "
               f"{(time.perf_counter() - t0) / REPS * 1e3:.3f} ms")
+
+# the draw-buffer path with the generators on the side stream: the encode of
+# call i runs under the generation of call i + 1, so the balance of jump and
+# generator time moves; per-call time for a few generator counts
+orig = codec.mt_generator_draws
+for G in (256, 320, 383, 448, 512, 640):
+    codec.mt_generator_draws = lambda c, G=G: 624 * max(1, -(-c // (624 * G)))
+    call = lambda: codec.qsgd_encode(x, nm, 4, gen.reserve(n), 1, out=words, lanes=lanes)  # noqa: E731
+    call()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(REPS):
+        call()
+    torch.cuda.synchronize()
+    print(f"buffer path, {G} generators: {(time.perf_counter() - t0) / REPS * 1e3:.3f} ms per call")
+codec.mt_generator_draws = orig
