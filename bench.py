@@ -776,7 +776,7 @@ def main():
         pgen.reserve(n)  # warm: builds the jump table once per process
         codec.qsgd_encode_torch(x, nm, bits, 1, out=words, lanes=lanes)
         torch.cuda.synchronize()
-        reps_mt = 5
+        reps_mt = 10
         t0 = time.perf_counter()
         for _ in range(reps_mt):  # draw buffer: 4n bytes of draws, then the full-chip encode reads them
             codec.qsgd_encode(x, nm, bits, pgen.reserve(n), 1, out=words, lanes=lanes)
@@ -798,9 +798,11 @@ def main():
             "mt19937_parallel_ms": ms_gen, "mt19937_parallel_draws_per_s": n / (ms_gen * 1e-3),
             "mt19937_serial_draws_per_s": 10_000_000 / (ms_ser * 1e-3),
             "note": "torch-CPU-generator (MT19937) draws, bit-exact with compressors.py: jump-ahead parallel "
-                    "generators (gc_mt19937_generate_jumped) -> encode from the draws; includes the torch "
-                    "state hand-off (H2D + D2H sync) per call.  fused_*: the generator kernel quantizes "
-                    "with its own draws (gc_qsgd_quantize_mt19937, no draw buffer) + lane pack"}
+                    "generators on a high-priority side stream (gc_mt19937_generate_phase_j) -> encode from the "
+                    "draws on the caller's stream; back-to-back calls: the next same-size call's draws are "
+                    "generated speculatively behind this call's and used only if torch's generator is untouched; "
+                    "torch's state is written back synchronously every call.  fused_*: the generator kernel "
+                    "quantizes with its own draws (gc_qsgd_quantize_mt19937, no draw buffer) + lane pack"}
         del draws
 
     if not args.no_extras:

@@ -445,9 +445,11 @@ size_t gc_mt19937_workspace_size_j(uint64_t count, uint64_t J)
 size_t gc_mt19937_workspace_size(uint64_t count) { return gc_mt19937_workspace_size_j(count, GC_MT_JUMP_DRAWS); }
 
 // seq -> jump -> gen<MODE> for `count` draws of state_dev, generators of J draws
+// (phase bit 1: seq + jump, bit 2: gen; the two halves of one run must be
+// enqueued in order on one stream with the same arguments)
 static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens,
                   uint64_t J, void *out, uint64_t count, void *workspace, gc_stream_t stream, const float *x,
-                  const float *norm, float s)
+                  const float *norm, float s, int phase = 3)
 {
     GC_REQUIRE(state_dev && workspace, "%s: null state/workspace", what);
     GC_REQUIRE(count == 0 || out, "%s: null out", what);
@@ -461,10 +463,14 @@ static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_
     GC_REQUIRE(gens <= 0x7fffffffull / kMtJumpSplit, "%s: count too large", what);
     hipStream_t st = as_stream(stream);
     uint32_t *ws = reinterpret_cast<uint32_t *>(workspace);
-    hipLaunchKernelGGL(k_mt_seq, dim3(1), dim3(256), 0, st, state_dev, ws);
-    if (gens > 1)
-        hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)((gens - 1) * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st, table_dev,
-                           ws, (uint32_t)(gens - 1));
+    if (phase & 1) {
+        hipLaunchKernelGGL(k_mt_seq, dim3(1), dim3(256), 0, st, state_dev, ws);
+        if (gens > 1)
+            hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)((gens - 1) * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st,
+                               table_dev, ws, (uint32_t)(gens - 1));
+    }
+    if (!(phase & 2))
+        return launch_status(what);
     if (mode == 0)
         hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, J, count, out,
                            state_dev, x, norm, s);
@@ -482,6 +488,14 @@ int gc_mt19937_generate_jumped_j(uint32_t *state_dev, const uint32_t *table_dev,
 {
     return mt_run("gc_mt19937_generate_jumped", 0, state_dev, table_dev, table_gens, J, out, count, workspace, stream,
                   nullptr, nullptr, 0.0f);
+}
+
+int gc_mt19937_generate_phase_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                uint32_t *out, uint64_t count, void *workspace, int phase, gc_stream_t stream)
+{
+    GC_REQUIRE(phase >= 1 && phase <= 3, "gc_mt19937_generate_phase_j: phase must be 1, 2 or 3");
+    return mt_run("gc_mt19937_generate_phase_j", 0, state_dev, table_dev, table_gens, J, out, count, workspace, stream,
+                  nullptr, nullptr, 0.0f, phase);
 }
 
 int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,

@@ -132,10 +132,14 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_decode(const uint32_t *__restri
 
 // GlobalRandK scatter for small K (reducer.py:754 buffer[idx] = dec):
 // out[idx[i]] = RN(RN(c * (lane_i - W*s)) * alpha), one element per thread
+// SEG: out is the per-parameter tensor list (a gc_segments table): the scatter
+// lands in grad_out directly (reducer.py:754 + 759-761 without the flat bucket)
+template <bool SEG = false>
 __global__ __launch_bounds__(kBlock) void k_decode_scatter1(const uint32_t *__restrict__ words,
                                                            const int64_t *__restrict__ idx, uint32_t n,
                                                            const float *__restrict__ normp, float s, int32_t sub,
-                                                           uint32_t w, uint32_t M, float alpha, float *__restrict__ out)
+                                                           uint32_t w, uint32_t M, float alpha, float *__restrict__ out,
+                                                           SegArg sg = SegArg{})
 {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n)
@@ -147,7 +151,12 @@ __global__ __launch_bounds__(kBlock) void k_decode_scatter1(const uint32_t *__re
     const uint32_t mask = (1u << w) - 1u;
     const int32_t Q = (int32_t)((wd >> (plane * w)) & mask) - sub;
     const float d = c * (float)Q;
-    out[id] = d * alpha;
+    if constexpr (SEG) {
+        const SegPos p = seg_find(sg, (uint64_t)id);
+        p.r.ptr[(uint64_t)id - p.r.start] = d * alpha;
+    } else {
+        out[id] = d * alpha;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -471,7 +480,7 @@ static int qsgd_decode(const char *what, const uint32_t *words, const int64_t *i
     } else if (mode == 2) {
         if (n < (1ull << 32) && lanes->bits < 32 && lanes->plane_words < (1ull << 32)) {
             // one element per thread: the word and the index load in one round trip
-            hipLaunchKernelGGL(k_decode_scatter1, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+            hipLaunchKernelGGL(k_decode_scatter1<false>, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                                words, idx, (uint32_t)n, norm, sf, sub, lanes->bits, (uint32_t)lanes->plane_words,
                                alpha, out);
         } else {
@@ -495,6 +504,29 @@ int gc_qsgd_decode_segments(const uint32_t *words, uint64_t n, const float *norm
 {
     GC_REQUIRE(segs, "gc_qsgd_decode_segments: null segments");
     return qsgd_decode("gc_qsgd_decode_segments", words, nullptr, n, norm, bits, lanes, alpha, nullptr, segs, stream);
+}
+
+int gc_qsgd_decode_scatter_segments(const uint32_t *words, const int64_t *idx, uint64_t k, const float *norm,
+                                    uint32_t bits, const gc_lanes *lanes, float alpha, const gc_segments *segs,
+                                    gc_stream_t stream)
+{
+    const char *what = "gc_qsgd_decode_scatter_segments";
+    int rc;
+    if ((rc = check_bits(bits, what)) || (rc = check_lanes(lanes, k, what)))
+        return rc;
+    const uint32_t s = (1u << bits) - 1u;
+    GC_REQUIRE(lanes->offset == s && lanes->range == 2ull * s, "%s: lanes not made by gc_qsgd_layout", what);
+    GC_REQUIRE(segs && norm && words && (k == 0 || idx), "%s: null pointer", what);
+    GC_REQUIRE(k < (1ull << 32) && lanes->bits < 32 && lanes->plane_words < (1ull << 32), "%s: K too large", what);
+    SegArg sg{};
+    if ((rc = seg_arg(segs, segs->n, &sg, what)))
+        return rc;
+    if (k == 0)
+        return GC_OK;
+    hipLaunchKernelGGL(k_decode_scatter1<true>, dim3((unsigned)((k + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       as_stream(stream), words, idx, (uint32_t)k, norm, (float)s, (int32_t)(lanes->world * s),
+                       lanes->bits, (uint32_t)lanes->plane_words, alpha, nullptr, sg);
+    return launch_status(what);
 }
 
 int gc_qsgd_quantize(const float *x, uint64_t n, const float *norm, uint32_t bits, const gc_rng *rng,

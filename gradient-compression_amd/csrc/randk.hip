@@ -25,6 +25,7 @@
 #include "gc_host.h"
 #include "qsgd_encode.h"
 #include "absmax.h"
+#include "segments.h"
 
 namespace gc {
 
@@ -33,19 +34,29 @@ constexpr uint64_t kRkFusedMax = 16384;  // K of the fused path: uint16 lanes in
 constexpr uint32_t kRkFusedMaxBits = 15; // lane values 0 .. 2 (2^b - 1) fit 16 bits
 constexpr unsigned kRkMaxBlocks = kAbsmaxMaxBlocks;  // one-level ticket (absmax.h)
 
-template <bool FUSED, int KIND>
+// SEG: x is the reference's TensorBuffer as a gc_segments table (the gather
+// reads each index's element straight from its per-parameter tensor: no
+// flattened bucket; reducer.py:722-723 gathers from the flattened one)
+template <bool FUSED, int KIND, bool SEG = false>
 __global__ __launch_bounds__(kRkThreads) void k_randk_gather(const float *__restrict__ x, const int64_t *__restrict__ idx,
                                                             uint32_t k, float *__restrict__ xk, uint32_t *__restrict__ ws,
                                                             float *__restrict__ normp, float s, int32_t qmax, uint32_t w,
                                                             uint32_t L, uint32_t M, RngArgs rng,
-                                                            uint32_t *__restrict__ words)
+                                                            uint32_t *__restrict__ words, SegArg sg = SegArg{})
 {
     __shared__ uint32_t part[kRkThreads / 64];
     __shared__ int last;
     const uint32_t i = blockIdx.x * kRkThreads + threadIdx.x;
     uint32_t m = 0;
     if (i < k) {
-        const float v = x[idx[i]];
+        float v;
+        if constexpr (SEG) {
+            const uint64_t e = (uint64_t)idx[i];
+            const SegPos p = seg_find(sg, e);
+            v = p.r.ptr[e - p.r.start];
+        } else {
+            v = x[idx[i]];
+        }
         if constexpr (FUSED)
             sc1_store(reinterpret_cast<uint32_t *>(xk) + i, __float_as_uint(v));  // read by the last block
         else
@@ -120,10 +131,14 @@ size_t gc_randk_workspace_size(void) { return gc_absmax_workspace_size(); }
 
 static int randk_gather(const char *what, const float *x, const int64_t *idx, uint64_t k, float *xk, float *norm,
                         const gc_lanes *lanes, uint32_t bits, const gc_rng *rng, uint32_t *words, void *workspace,
-                        gc_stream_t stream)
+                        gc_stream_t stream, const gc_segments *segs = nullptr)
 {
-    GC_REQUIRE(x && idx && norm && workspace && (k == 0 || xk), "%s: null pointer", what);
+    GC_REQUIRE((x || segs) && idx && norm && workspace && (k == 0 || xk), "%s: null pointer", what);
     GC_REQUIRE(k < (1ull << 31), "%s: K too large", what);
+    SegArg sg{};
+    int rc;
+    if (segs && (rc = seg_arg(segs, segs->n, &sg, what)))
+        return rc;
     if (k == 0)
         return hipMemsetAsync(norm, 0, sizeof(float), as_stream(stream)) == hipSuccess ? GC_OK : launch_status(what);
     const unsigned blocks = (unsigned)((k + kRkThreads - 1) / kRkThreads);
@@ -132,9 +147,15 @@ static int randk_gather(const char *what, const float *x, const int64_t *idx, ui
     hipStream_t st = as_stream(stream);
     uint32_t *ws = reinterpret_cast<uint32_t *>(workspace);
     RngArgs ra{};
+#define GC_RKG(F_, K_, ...)                                                                                       \
+    do {                                                                                                          \
+        if (segs)                                                                                                 \
+            hipLaunchKernelGGL((k_randk_gather<F_, K_, true>), dim3(blocks), dim3(kRkThreads), 0, st, __VA_ARGS__, sg); \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_randk_gather<F_, K_, false>), dim3(blocks), dim3(kRkThreads), 0, st, __VA_ARGS__, sg); \
+    } while (0)
     if (!words) {
-        hipLaunchKernelGGL((k_randk_gather<false, 0>), dim3(blocks), dim3(kRkThreads), 0, st, x, idx, (uint32_t)k, xk,
-                           ws, norm, 0.0f, 0, 0u, 0u, 0u, ra, nullptr);
+        GC_RKG(false, 0, x, idx, (uint32_t)k, xk, ws, norm, 0.0f, 0, 0u, 0u, 0u, ra, nullptr);
         return launch_status(what);
     }
     const uint32_t s = (1u << bits) - 1u;
@@ -144,12 +165,34 @@ static int randk_gather(const char *what, const float *x, const int64_t *idx, ui
     ra.n = k;
     const uint32_t M = (uint32_t)lanes->plane_words;
     if (rng->kind == GC_RNG_PHILOX)
-        hipLaunchKernelGGL((k_randk_gather<true, 0>), dim3(blocks), dim3(kRkThreads), 0, st, x, idx, (uint32_t)k, xk, ws,
-                           norm, (float)s, (int32_t)s, lanes->bits, lanes->per_word, M, ra, words);
+        GC_RKG(true, 0, x, idx, (uint32_t)k, xk, ws, norm, (float)s, (int32_t)s, lanes->bits, lanes->per_word, M, ra,
+               words);
     else
-        hipLaunchKernelGGL((k_randk_gather<true, 1>), dim3(blocks), dim3(kRkThreads), 0, st, x, idx, (uint32_t)k, xk, ws,
-                           norm, (float)s, (int32_t)s, lanes->bits, lanes->per_word, M, ra, words);
+        GC_RKG(true, 1, x, idx, (uint32_t)k, xk, ws, norm, (float)s, (int32_t)s, lanes->bits, lanes->per_word, M, ra,
+               words);
+#undef GC_RKG
     return launch_status(what);
+}
+
+static int randk_encode_w1_check(const char *what, uint64_t k, uint32_t bits, const gc_lanes *lanes, const gc_rng *rng,
+                                 uint32_t *words)
+{
+    int rc;
+    if ((rc = check_bits(bits, what)) || (rc = check_lanes(lanes, k, what)))
+        return rc;
+    const uint32_t s = (1u << bits) - 1u;
+    GC_REQUIRE(lanes->offset == s && lanes->range == 2ull * s && lanes->world == 1,
+               "%s: lanes not made by gc_qsgd_layout(k, bits, 1)", what);
+    GC_REQUIRE(k <= kRkFusedMax, "%s: K = %llu above %llu", what, (unsigned long long)k,
+               (unsigned long long)kRkFusedMax);
+    // lanes are staged as uint16 in LDS: a lane value reaches 2 s = 2^(b+1) - 2
+    GC_REQUIRE(bits <= kRkFusedMaxBits, "%s: %u bits above %u (16-bit LDS lanes; use the gather + gc_qsgd_encode)",
+               what, bits, kRkFusedMaxBits);
+    GC_REQUIRE(rng && (rng->kind == GC_RNG_PHILOX || (rng->kind == GC_RNG_STREAM && rng->stream)), "%s: bad rng", what);
+    GC_REQUIRE(words, "%s: null words", what);
+    if (k == 0 && lanes->plane_words)
+        return fail(GC_EINVAL, "%s: layout / K mismatch", what);
+    return GC_OK;
 }
 
 int gc_randk_gather_absmax(const float *x, const int64_t *idx, uint64_t k, float *xk, float *norm, void *workspace,
@@ -162,22 +205,33 @@ int gc_randk_encode_w1(const float *x, const int64_t *idx, uint64_t k, float *xk
                        const gc_lanes *lanes, const gc_rng *rng, uint32_t *words, void *workspace, gc_stream_t stream)
 {
     int rc;
-    if ((rc = check_bits(bits, "gc_randk_encode_w1")) || (rc = check_lanes(lanes, k, "gc_randk_encode_w1")))
+    if ((rc = randk_encode_w1_check("gc_randk_encode_w1", k, bits, lanes, rng, words)))
         return rc;
-    const uint32_t s = (1u << bits) - 1u;
-    GC_REQUIRE(lanes->offset == s && lanes->range == 2ull * s && lanes->world == 1,
-               "gc_randk_encode_w1: lanes not made by gc_qsgd_layout(k, bits, 1)");
-    GC_REQUIRE(k <= kRkFusedMax, "gc_randk_encode_w1: K = %llu above %llu", (unsigned long long)k,
-               (unsigned long long)kRkFusedMax);
-    // lanes are staged as uint16 in LDS: a lane value reaches 2 s = 2^(b+1) - 2
-    GC_REQUIRE(bits <= kRkFusedMaxBits, "gc_randk_encode_w1: %u bits above %u (16-bit LDS lanes; use "
-               "gc_randk_gather_absmax + gc_qsgd_encode)", bits, kRkFusedMaxBits);
-    GC_REQUIRE(rng && (rng->kind == GC_RNG_PHILOX || (rng->kind == GC_RNG_STREAM && rng->stream)),
-               "gc_randk_encode_w1: bad rng");
-    GC_REQUIRE(words, "gc_randk_encode_w1: null words");
     if (k == 0)
-        return lanes->plane_words ? fail(GC_EINVAL, "gc_randk_encode_w1: layout / K mismatch") : GC_OK;
+        return GC_OK;
     return randk_gather("gc_randk_encode_w1", x, idx, k, xk, norm, lanes, bits, rng, words, workspace, stream);
+}
+
+int gc_randk_gather_absmax_segments(const gc_segments *segs, const int64_t *idx, uint64_t k, float *xk, float *norm,
+                                    void *workspace, gc_stream_t stream)
+{
+    GC_REQUIRE(segs, "gc_randk_gather_absmax_segments: null segments");
+    return randk_gather("gc_randk_gather_absmax_segments", nullptr, idx, k, xk, norm, nullptr, 0, nullptr, nullptr,
+                        workspace, stream, segs);
+}
+
+int gc_randk_encode_w1_segments(const gc_segments *segs, const int64_t *idx, uint64_t k, float *xk, float *norm,
+                                uint32_t bits, const gc_lanes *lanes, const gc_rng *rng, uint32_t *words,
+                                void *workspace, gc_stream_t stream)
+{
+    int rc;
+    GC_REQUIRE(segs, "gc_randk_encode_w1_segments: null segments");
+    if ((rc = randk_encode_w1_check("gc_randk_encode_w1_segments", k, bits, lanes, rng, words)))
+        return rc;
+    if (k == 0)
+        return GC_OK;
+    return randk_gather("gc_randk_encode_w1_segments", nullptr, idx, k, xk, norm, lanes, bits, rng, words, workspace,
+                        stream, segs);
 }
 
 }  // extern "C"

@@ -138,6 +138,26 @@ __global__ __launch_bounds__(kAbsmaxThreads) void k_seg_scatter(SegArg sg, uint6
     }
 }
 
+// src tensors -> dst tensors of the same sizes, times alpha: the GRandK setgrad
+// (reducer.py:759-761: every coordinate, the selected ones overwritten after)
+__global__ __launch_bounds__(kAbsmaxThreads) void k_seg_copy(SegArg src, SegArg dst, uint64_t n, float alpha)
+{
+    OpScale op{alpha};
+    const uint64_t ranges = (n + kRange - 1) / kRange;
+    for (uint64_t c = blockIdx.x; c < ranges; c += gridDim.x) {
+        const uint64_t r0 = c * kRange, r1 = std::min(r0 + kRange, n);
+        SegPos p = seg_find(src, r0);
+        for (;;) {  // the tables share every segment boundary: record s of dst matches record s of src
+            const SegRec d = seg_rec(dst, p.s);
+            const uint64_t lo = std::max(r0, p.r.start), hi = std::min(r1, p.r.end);
+            seg_piece<true>(p.r.ptr + (lo - p.r.start), d.ptr + (lo - d.start), hi - lo, op);
+            if (hi >= r1)
+                break;
+            p.r = seg_rec(src, ++p.s);
+        }
+    }
+}
+
 int seg_arg(const gc_segments *segs, uint64_t n, SegArg *out, const char *what)
 {
     GC_REQUIRE(segs, "%s: null segments", what);
@@ -230,6 +250,23 @@ int gc_segments_flatten_absmax(const gc_segments *segs, float *flat, float *norm
     }
 #undef GC_SF
     return launch_status("gc_segments_flatten_absmax");
+}
+
+int gc_segments_copy(const gc_segments *src, const gc_segments *dst, float alpha, gc_stream_t stream)
+{
+    SegArg a{}, b{};
+    int rc;
+    GC_REQUIRE(src && dst, "gc_segments_copy: null segments");
+    if ((rc = seg_arg(src, src->n, &a, "gc_segments_copy")) || (rc = seg_arg(dst, src->n, &b, "gc_segments_copy")))
+        return rc;
+    GC_REQUIRE(src->count == dst->count, "gc_segments_copy: %llu vs %llu tensors", (unsigned long long)src->count,
+               (unsigned long long)dst->count);
+    const uint64_t n = src->n;
+    if (n == 0)
+        return GC_OK;
+    const unsigned grid = (unsigned)std::min<uint64_t>((n + kRange - 1) / kRange, 2048);
+    hipLaunchKernelGGL(k_seg_copy, dim3(grid), dim3(kAbsmaxThreads), 0, as_stream(stream), a, b, n, alpha);
+    return launch_status("gc_segments_copy");
 }
 
 int gc_segments_scatter(const float *flat, float alpha, const gc_segments *segs, gc_stream_t stream)

@@ -106,6 +106,8 @@ SIGNATURES = {
     "gc_segments_plan": (C.c_int, [P, P, u64, u32, P, P, u64, P]),
     "gc_segments_flatten_absmax": (C.c_int, [SEGSP, P, P, P, P]),
     "gc_segments_scatter": (C.c_int, [P, f32, SEGSP, P]),
+    "gc_segments_copy": (C.c_int, [SEGSP, SEGSP, f32, P]),
+    "gc_qsgd_decode_scatter_segments": (C.c_int, [P, P, u64, P, u32, LANESP, f32, SEGSP, P]),
     "gc_qsgd_decode_segments": (C.c_int, [P, u64, P, u32, LANESP, f32, SEGSP, P]),
     "gc_ms_mask_encode": (C.c_int, [P, P, u64, P, LEVP, RNGP, LANESP, P, P]),
     "gc_ms_select_encode": (C.c_int, [P, P, u64, P, LEVP, RNGP, P, LANESP, LANESP, P, P]),
@@ -128,9 +130,12 @@ SIGNATURES = {
     "gc_mt19937_jump_table_j": (C.c_int, [u64, u64, u64, P]),
     "gc_mt19937_workspace_size_j": (C.c_size_t, [u64, u64]),
     "gc_mt19937_generate_jumped_j": (C.c_int, [P, P, u64, u64, P, u64, P, P]),
+    "gc_mt19937_generate_phase_j": (C.c_int, [P, P, u64, u64, P, u64, P, C.c_int, P]),
     "gc_randk_workspace_size": (C.c_size_t, []),
     "gc_randk_gather_absmax": (C.c_int, [P, P, u64, P, P, P, P]),
     "gc_randk_encode_w1": (C.c_int, [P, P, u64, P, P, u32, LANESP, RNGP, P, P, P]),
+    "gc_randk_gather_absmax_segments": (C.c_int, [SEGSP, P, u64, P, P, P, P]),
+    "gc_randk_encode_w1_segments": (C.c_int, [SEGSP, P, u64, P, P, u32, LANESP, RNGP, P, P, P]),
     "gc_greedy4_pack": (i64, [P, u64, P, u64]),
     "gc_greedy4_unpack": (i64, [P, u64, P, u64]),
     "gc_greedy4_workspace_size": (C.c_size_t, [u64]),

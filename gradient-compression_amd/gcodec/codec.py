@@ -245,6 +245,56 @@ def randk_encode_w1(x, idx, bits, rng, xk=None, norm=None, out=None, lanes=None)
     return out, norm
 
 
+def randk_gather_absmax_segments(segs, idx, xk=None, norm=None):
+    """randk_gather_absmax with x given as the per-parameter tensors of segs:
+    each index is read from its tensor, so no flat bucket is built."""
+    dev = segs.device
+    idx = _idx(idx, dev)
+    k = idx.numel()
+    if xk is None:
+        xk = torch.empty(k, dtype=torch.float32, device=dev)
+    if norm is None:
+        norm = torch.empty(1, dtype=torch.float32, device=dev)
+    st = _stream(dev)
+    check(_lib.load().gc_randk_gather_absmax_segments(C.byref(segs.struct), _p(idx), k, _p(xk), _p(norm),
+                                                      _p(_absmax_ws(dev, st)), st),
+          "gc_randk_gather_absmax_segments")
+    return xk, norm
+
+
+def randk_encode_w1_segments(segs, idx, bits, rng, xk=None, norm=None, out=None, lanes=None):
+    """randk_encode_w1 reading the K indices from the tensors of segs."""
+    dev = segs.device
+    idx = _idx(idx, dev)
+    k = idx.numel()
+    lanes = lanes or qsgd_layout(k, bits, 1)
+    if xk is None:
+        xk = torch.empty(k, dtype=torch.float32, device=dev)
+    if norm is None:
+        norm = torch.empty(1, dtype=torch.float32, device=dev)
+    if out is None:
+        out = torch.empty(lanes.plane_words, dtype=torch.int32, device=dev)
+    r = rng.struct()
+    st = _stream(dev)
+    check(_lib.load().gc_randk_encode_w1_segments(C.byref(segs.struct), _p(idx), k, _p(xk), _p(norm), bits,
+                                                  C.byref(lanes), C.byref(r), _p(out), _p(_absmax_ws(dev, st)), st),
+          "gc_randk_encode_w1_segments")
+    return out, norm
+
+
+def qsgd_decode_scatter_segments(words, idx, norm, bits, segs, world=1, alpha=1.0, lanes=None):
+    """element idx[i] of the tensors of segs = RN(decode_i * alpha) + 0 (the
+    GlobalRandK decode-scatter, reducer.py:754, with the setgrad's 1/W)."""
+    dev = _dev(words)
+    idx = _idx(idx, dev)
+    k = idx.numel()
+    lanes = lanes or qsgd_layout(k, bits, world)
+    nt = norm_tensor(norm, dev)
+    check(_lib.load().gc_qsgd_decode_scatter_segments(_p(words), _p(idx), k, _p(nt), bits, C.byref(lanes),
+                                                      float(alpha), C.byref(segs.struct), _stream(dev)),
+          "gc_qsgd_decode_scatter_segments")
+
+
 class RandKStep:
     """A pre-resolved GlobalRandK encode / decode for a fixed bucket, K and lane
     layout (BASELINE config 4: K = 10,000 of a 14.7M bucket).  At this size the
@@ -407,6 +457,15 @@ def segments_scatter(flat: torch.Tensor, segs: Segments, alpha: float = 1.0):
     flat = _f32(flat, "segments_scatter")
     check(_lib.load().gc_segments_scatter(_p(flat), float(alpha), C.byref(segs.struct), _stream(segs.device)),
           "gc_segments_scatter")
+
+
+def segments_copy(src: Segments, dst: Segments, alpha: float = 1.0):
+    """dst tensor element = RN(src tensor element * alpha) + 0 for two lists of
+    the same tensor sizes (the GlobalRandK setgrad, reducer.py:759-761)."""
+    if [e[1] for e in src.key] != [e[1] for e in dst.key] or src.device != dst.device:
+        raise _lib.GCodecError(_lib.GC_EINVAL, "segments_copy: the two lists differ in tensor sizes or device")
+    check(_lib.load().gc_segments_copy(C.byref(src.struct), C.byref(dst.struct), float(alpha), _stream(src.device)),
+          "gc_segments_copy")
 
 
 def qsgd_decode_segments(words, norm, bits, segs: Segments, world=1, alpha=1.0, lanes=None):
@@ -729,7 +788,20 @@ def _mt_ws(dev, st, count: int, J: int) -> torch.Tensor:
     return ws
 
 
-_MT_PIN = {}  # device index -> (pinned host state in, pinned host state out, device state): 625 int32 each
+_MT_PIN = {}  # device index -> {path: (pinned state in, pinned states out, device state)}: 625 int32 each
+
+
+def _mt_bufs(device, path: str = "draws"):
+    """Per device and path ("draws": mt19937_draws, two out slots for its
+    speculative runs; "fused": the generator-quantize path): separate buffers,
+    so a run still queued on one path never writes what the other reads."""
+    d = _MT_PIN.setdefault(device.index, {})
+    b = d.get(path)
+    if b is None:
+        b = d[path] = (torch.empty(625, dtype=torch.int32).pin_memory(),
+                       [torch.empty(625, dtype=torch.int32).pin_memory() for _ in range(2)],
+                       torch.empty(625, dtype=torch.int32, device=device))
+    return b
 
 
 def _torch_state_to(device) -> torch.Tensor:
@@ -739,17 +811,11 @@ def _torch_state_to(device) -> torch.Tensor:
     from .rng import torch_mt_state
 
     words, idx = torch_mt_state()
-    bufs = _MT_PIN.get(device.index)
-    if bufs is None:
-        bufs = _MT_PIN[device.index] = (torch.empty(625, dtype=torch.int32).pin_memory(),
-                                        torch.empty(625, dtype=torch.int32).pin_memory(),
-                                        torch.empty(625, dtype=torch.int32, device=device))
-    hin, _, dst = bufs
+    hin, _, dst = _mt_bufs(device, "fused")
     h = hin.numpy().view(np.uint32)  # free: the previous call synchronised after its copy
     h[:624] = words
     h[624] = idx
     dst.copy_(hin, non_blocking=True)
-    _MT_LAST.pop(device.index, None)  # dst now follows this call, not the draw path's record
     return dst
 
 
@@ -759,7 +825,7 @@ def _torch_state_back(state_dev: torch.Tensor):
     the host before torch's generator is used again)."""
     from .rng import set_torch_mt_state
 
-    hout = _MT_PIN[state_dev.device.index][1]
+    hout = _mt_bufs(state_dev.device, "fused")[1][0]
     hout.copy_(state_dev, non_blocking=True)
     torch.cuda.current_stream(state_dev.device).synchronize()
     new = hout.numpy().view(np.uint32)
@@ -811,7 +877,10 @@ def qsgd_encode_torch(x, norm, bits, world=1, out=None, lanes=None) -> torch.Ten
 
 
 _MT_SIDE = {}  # device index -> the side stream torch-mode draws are generated on
-_MT_LAST = {}  # device index -> (624 words, read index) last written back to torch == the device state
+_MT_LAST = {}  # device index -> (624 words, read index) last written back to torch
+_MT_SPEC = {}  # device index -> the speculative run of the next same-size call
+MT_SPECULATE = True  # generate the draws of the next same-size torch-mode call ahead (mt19937_draws)
+MT_WAIT_NEXT_JUMPS = True  # consumers also wait for the speculative run's jumps (mt19937_draws)
 
 
 def _mt_side(device) -> torch.cuda.Stream:
@@ -824,51 +893,91 @@ def _mt_side(device) -> torch.cuda.Stream:
     return s
 
 
+class _MtRun:
+    """One enqueued generation: its draws, the pinned slot its final state goes
+    to, and events after its jumps and after that state copy."""
+
+    __slots__ = ("count", "out", "slot", "jumped", "done")
+
+
+def _mt_enqueue(dev, st_dev, count: int, hout, slot: int) -> _MtRun:
+    """On the current (side) stream: seq + jumps, an event, the generators
+    (out, and st_dev advanced by count draws), the state into hout[slot]."""
+    J = mt_generator_draws(count)
+    gens = -(-count // J)
+    table, tgens = _mt_jump_table(dev, gens - 1, J) if gens > 1 else (None, 0)
+    st = _stream(dev)
+    ws = _mt_ws(dev, st, count, J)
+    run = _MtRun()
+    run.count, run.slot = count, slot
+    run.out = torch.empty(count, dtype=torch.int32, device=dev)
+    lib = _lib.load()
+    check(lib.gc_mt19937_generate_phase_j(_p(st_dev), _p(table), tgens, J, _p(run.out), count, _p(ws), 1, st),
+          "gc_mt19937_generate_phase_j")
+    run.jumped = torch.cuda.Event()
+    run.jumped.record()
+    check(lib.gc_mt19937_generate_phase_j(_p(st_dev), _p(table), tgens, J, _p(run.out), count, _p(ws), 2, st),
+          "gc_mt19937_generate_phase_j")
+    hout[slot].copy_(st_dev, non_blocking=True)
+    run.done = torch.cuda.Event()
+    run.done.record()
+    return run
+
+
 def mt19937_draws(count: int, device) -> torch.Tensor:
     """`count` draws of torch's CPU generator, produced on `device`; torch's
     generator state advances exactly as torch.bernoulli would advance it
     (synchronously: the new state is in torch's generator when this returns).
 
-    The draws are generated on a side stream (gc_mt19937_generate_jumped: the
-    LDS-bound jump and the latency-bound generators) that the caller's stream
-    waits on, and the host waits only for that side stream, never for the
-    caller's queued work: the encode of call i (HBM-bound, on the caller's
-    stream) runs under the generation of call i + 1.  The state goes to the
-    device only when torch's generator differs from what the last call wrote
-    back (the device buffer already holds that state)."""
+    The draws are generated on a high-priority side stream
+    (gc_mt19937_generate_phase_j: the state's sequence and the LDS-bound jumps,
+    then the latency-bound generators); the host waits for that stream only,
+    never for the caller's queued work.  With MT_SPECULATE the next call's
+    draws (same count, continuing from this call's final state) are enqueued
+    right behind, so back-to-back calls find their draws generated or in
+    flight; a speculative run is used only if torch's generator is exactly
+    where the previous call left it and the count matches, else it is dropped
+    and the state is sent to the device again.  The caller's stream then
+    waits on the speculative run's jumps as well: its consumer (the encode,
+    HBM-bound) runs beside the latency-bound generators instead of competing
+    with the LDS-bound jumps."""
     from .rng import set_torch_mt_state, torch_mt_state
 
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     if device.index is None:
         device = torch.device("cuda", torch.cuda.current_device())
     words, idx = torch_mt_state()
-    bufs = _MT_PIN.get(device.index)
-    if bufs is None:
-        bufs = _MT_PIN[device.index] = (torch.empty(625, dtype=torch.int32).pin_memory(),
-                                        torch.empty(625, dtype=torch.int32).pin_memory(),
-                                        torch.empty(625, dtype=torch.int32, device=device))
-    hin, hout, dst = bufs
+    hin, hout, dst = _mt_bufs(device)
     cur = torch.cuda.current_stream(device)
     side = _mt_side(device)
     last = _MT_LAST.get(device.index)
+    untouched = last is not None and last[1] == idx and np.array_equal(last[0], words)
+    spec = _MT_SPEC.pop(device.index, None)
+    if count == 0:
+        if spec is not None:  # a dropped run still moves dst on: send the state next time
+            _MT_LAST.pop(device.index, None)
+        return torch.empty(0, dtype=torch.int32, device=device)
     with torch.cuda.stream(side):
-        if last is None or last[1] != idx or not np.array_equal(last[0], words):
-            h = hin.numpy().view(np.uint32)  # free: the previous call waited for its copies
-            h[:624] = words
-            h[624] = idx
-            dst.copy_(hin, non_blocking=True)
-        out = mt19937_generate(dst, count)
-        hout.copy_(dst, non_blocking=True)
-        done = torch.cuda.Event()
-        done.record(side)
-    cur.wait_event(done)
-    out.record_stream(cur)
-    done.synchronize()
-    new = hout.numpy().view(np.uint32)
+        if spec is not None and untouched and spec.count == count:
+            run = spec
+        else:
+            if spec is not None or not untouched:  # dst is not torch's state: send it
+                h = hin.numpy().view(np.uint32)  # free: earlier copies from it were waited for
+                h[:624] = words
+                h[624] = idx
+                dst.copy_(hin, non_blocking=True)
+            run = _mt_enqueue(device, dst, count, hout, spec.slot ^ 1 if spec is not None else 0)
+        nxt = _mt_enqueue(device, dst, count, hout, run.slot ^ 1) if MT_SPECULATE else None
+    cur.wait_event(nxt.jumped if nxt is not None and MT_WAIT_NEXT_JUMPS else run.done)
+    run.out.record_stream(cur)
+    if nxt is not None:
+        _MT_SPEC[device.index] = nxt
+    run.done.synchronize()
+    new = hout[run.slot].numpy().view(np.uint32)
     w2, i2 = new[:624].copy(), int(new[624])
     set_torch_mt_state(w2, i2)
     _MT_LAST[device.index] = (w2, i2)
-    return out
+    return run.out
 
 
 # ---------------------------------------------------------------------------

@@ -88,6 +88,16 @@ class GlobalRandKMaxNormCompressor(QSGDMaxNormCompressor):
         rng = self._reserve(idx.numel(), 1, tensor.device)
         return self.backend.randk_encode_w1(tensor, idx, self._quantization_level, rng, out=out)
 
+    def encode_w1_segments(self, segs, idx, out=None):
+        """encode_w1 with the tensor given as the per-parameter tensors of segs."""
+        rng = self._reserve(idx.numel(), 1, segs.device)
+        return self.backend.randk_encode_w1_segments(segs, idx, self._quantization_level, rng, out=out)
+
+    def decode_scatter_segments(self, norm, words, idx, segs, world=1, alpha=1.0):
+        """decode(..., idx=idx) writing element idx[i] straight into its tensor."""
+        return self.backend.qsgd_decode_scatter_segments(words, idx, norm, self._quantization_level, segs, world,
+                                                         alpha)
+
 
 class QSGDBPCompressor(_Base):
     """compressors.py:324-378 (kept commented out in the reference because it

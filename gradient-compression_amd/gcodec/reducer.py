@@ -248,9 +248,55 @@ class GlobalRandKMaxNormReducer(Reducer):
     def _randk_compressor(self):
         return self._compressor(C.GlobalRandKMaxNormCompressor, self._quantization_level)
 
+    def _reduce_segments(self, comp, in_segs, out_segs):
+        """The step with grad_in / grad_out addressed in place (no flat bucket):
+        gather + norm (+ encode at W = 1) read each index from its tensor, the
+        setgrad copies every coordinate tensor to tensor (x 1/W) and the
+        decode-scatter overwrites the K selected ones (reducer.py:754-761: the
+        same values, written once instead of via the bucket)."""
+        W = self.n_workers
+        idx = self._next_indices(in_segs.n, in_segs.device)
+        k = idx.numel()
+        codec = self._codec
+        if codec.randk_fused_ok(k, self._quantization_level, W):
+            with self._timer("reduce.compress", verbosity=2):
+                words, norm = comp.encode_w1_segments(in_segs, idx)
+        else:
+            with self._timer("reduce.norm", verbosity=2):
+                xk, local = codec.randk_gather_absmax_segments(in_segs, idx)
+                norm = self._all_reduce(local, dist.ReduceOp.MAX)
+            with self._timer("reduce.compress", verbosity=2):
+                words = comp.encode(norm, xk, world=W)
+        with self._timer("reduce.reduce.vector", verbosity=2):
+            self._all_reduce(words)
+        bits = self.n_bits(norm) + self.n_bits(words)
+        with self._timer("reduce.setgrad", verbosity=2):
+            codec.segments_copy(in_segs, out_segs, 1.0 / W)
+        with self._timer("reduce.decompress", verbosity=2):
+            comp.decode_scatter_segments(norm, words, idx, out_segs, world=W, alpha=1.0 / W)
+        return bits
+
+    def _segment_pair(self, grad_in, grad_out):
+        """(in, out) tables when both lists are fused-addressable with equal
+        tensor sizes and the subset fits the gather kernel, else None."""
+        codec = self._codec
+        if not hasattr(codec, "randk_gather_absmax_segments"):
+            return None
+        grad_in, grad_out = list(grad_in), list(grad_out)
+        if len(grad_in) != len(grad_out) or any(a.numel() != b.numel() for a, b in zip(grad_in, grad_out)):
+            return None
+        in_segs = self._segments(grad_in)
+        out_segs = self._segments(grad_out) if in_segs is not None else None
+        if out_segs is None or min(self._K, in_segs.n) > codec.RANDK_GATHER_MAX:
+            return None
+        return in_segs, out_segs
+
     def reduce(self, grad_in, grad_out):
         W = self.n_workers
         comp = self._randk_compressor()
+        pair = self._segment_pair(grad_in, grad_out)
+        if pair is not None:
+            return self._reduce_segments(comp, *pair)
         flat, _ = self._flat_pack(grad_in)
         n = flat.buffer.numel()
         idx = self._next_indices(n, flat.buffer.device)

@@ -189,6 +189,16 @@ int gc_randk_gather_absmax(const float *x, const int64_t *idx, uint64_t k, float
                            gc_stream_t stream);
 int gc_randk_encode_w1(const float *x, const int64_t *idx, uint64_t k, float *xk, float *norm, uint32_t bits,
                        const gc_lanes *lanes, const gc_rng *rng, uint32_t *words, void *workspace, gc_stream_t stream);
+/* the same two with x given as the per-parameter tensors (a gc_segments table,
+ * below): the reducer's gather reads every index from its tensor, so no
+ * flattened bucket is built for GlobalRandK (reducer.py:713-723 flattens the
+ * whole gradient, then gathers K of its elements) */
+typedef struct gc_segments gc_segments;
+int gc_randk_gather_absmax_segments(const gc_segments *segs, const int64_t *idx, uint64_t k, float *xk, float *norm,
+                                    void *workspace, gc_stream_t stream);
+int gc_randk_encode_w1_segments(const gc_segments *segs, const int64_t *idx, uint64_t k, float *xk, float *norm,
+                                uint32_t bits, const gc_lanes *lanes, const gc_rng *rng, uint32_t *words,
+                                void *workspace, gc_stream_t stream);
 
 /* ---- greedy 4-mode packer on the device --------------------------------------
  * The format of gc_greedy4_pack (Extension CPU/bitpacking.cpp:5-124) produced by
@@ -222,14 +232,14 @@ typedef struct gc_seg {
     float *ptr;        /* device base pointer of the tensor (contiguous fp32) */
     uint64_t reserved; /* 0 (records are 32 bytes) */
 } gc_seg;
-typedef struct gc_segments {
+struct gc_segments {
     uint64_t count;            /* tensors */
     uint64_t n;                /* total elements = seg[count-1].end */
     const gc_seg *seg;         /* device, count records; a sentinel is not needed */
     const uint32_t *chunk_seg; /* device, gc_segments_chunks(n, chunk_shift) entries */
     uint32_t chunk_shift;      /* 4..30 */
     uint32_t reserved;         /* 0 */
-} gc_segments;
+};
 uint64_t gc_segments_chunks(uint64_t n, uint32_t chunk_shift);
 /* host: (sizes[count], device ptrs[count]) -> seg[count], chunk_seg[chunk_capacity >=
  * gc_segments_chunks(n, chunk_shift)] (host buffers to upload); *n_out = total elements */
@@ -242,6 +252,14 @@ int gc_segments_flatten_absmax(const gc_segments *segs, float *flat, float *norm
 /* tensor element e = RN(flat[e] * alpha) + 0.0f — the setgrad loop `out[:] = 0; out.add_(g, alpha)`
  * (reducer.py:543-549, 755-761); the + 0 maps -0 to +0 exactly as the reference does */
 int gc_segments_scatter(const float *flat, float alpha, const gc_segments *segs, gc_stream_t stream);
+/* dst tensor element e = RN(src tensor element e * alpha) + 0.0f for two lists of the same tensor sizes
+ * (the GlobalRandK setgrad of every coordinate, reducer.py:759-761, tensor to tensor) */
+int gc_segments_copy(const gc_segments *src, const gc_segments *dst, float alpha, gc_stream_t stream);
+/* the GlobalRandK decode-scatter (gc_qsgd_decode with idx) into the tensors of segs:
+ * element idx[i] = RN(decode_i * alpha) (reducer.py:754 + 759-761) */
+int gc_qsgd_decode_scatter_segments(const uint32_t *words, const int64_t *idx, uint64_t k, const float *norm,
+                                    uint32_t bits, const gc_lanes *lanes, float alpha, const gc_segments *segs,
+                                    gc_stream_t stream);
 /* gc_qsgd_decode writing each element straight into its tensor (decode + 1/W + setgrad fused) */
 int gc_qsgd_decode_segments(const uint32_t *words, uint64_t n, const float *norm, uint32_t bits,
                             const gc_lanes *lanes, float alpha, const gc_segments *segs, gc_stream_t stream);
@@ -324,6 +342,12 @@ int gc_mt19937_jump_table_j(uint64_t J, uint64_t first, uint64_t count, uint32_t
 size_t gc_mt19937_workspace_size_j(uint64_t count, uint64_t J);
 int gc_mt19937_generate_jumped_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
                                  uint32_t *out, uint64_t count, void *workspace, gc_stream_t stream);
+/* the same run in two halves: phase 1 = the state's sequence + the jumps (the
+ * LDS-bound part), phase 2 = the generators (writes out and advances
+ * state_dev), phase 3 = both.  Enqueue 1 then 2 on one stream with identical
+ * arguments; an event between them marks the end of the jumps. */
+int gc_mt19937_generate_phase_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                uint32_t *out, uint64_t count, void *workspace, int phase, gc_stream_t stream);
 /* torch-mode QSGD quantize with the MT19937 draws consumed in-kernel (never
  * stored): q[i] = sign(x_i)*xi_i exactly as compressors.py:299-316 computes it
  * under torch.bernoulli (one draw per element, in order), as GC_I8 (bits <= 7)

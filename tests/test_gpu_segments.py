@@ -132,11 +132,51 @@ def test_segments_reject_bad_input():
         codec.qsgd_decode_segments(words, torch.ones(1, device=DEV), 4, segs, lanes=lanes)
 
 
+@pytest.mark.parametrize("k", [1, 1000, 16_384, 20_000])
+def test_randk_segments_equal_flat(k):
+    """The GlobalRandK kernels addressing the tensors in place (gather from
+    segments, encode at W = 1, decode-scatter into segments, tensor-to-tensor
+    setgrad) give the bits of the flat-bucket kernels."""
+    ts, ref = carve(RAGGED, seed=61)
+    segs = codec.Segments(ts, chunk_shift=5)
+    x = torch.from_numpy(ref).to(DEV)
+    x[::31] = -0.0
+    for t, (a, b) in zip(ts, zip(np.cumsum([0] + RAGGED[:-1]), np.cumsum(RAGGED))):
+        t.copy_(x[a:b])
+    g = torch.Generator().manual_seed(k)
+    idx = torch.randperm(segs.n, generator=g)[:k].to(DEV)
+    xk, nk = codec.randk_gather_absmax(x, idx)
+    xs, ns = codec.randk_gather_absmax_segments(segs, idx)
+    assert torch.equal(xk.view(torch.int32), xs.view(torch.int32)) and torch.equal(nk, ns)
+    bits = 4
+    if k <= codec.RANDK_FUSED_MAX:
+        w1, n1 = codec.randk_encode_w1(x, idx, bits, gcodec.Generator(3, "philox").reserve(k))
+        w2, n2 = codec.randk_encode_w1_segments(segs, idx, bits, gcodec.Generator(3, "philox").reserve(k))
+        assert torch.equal(w1, w2) and torch.equal(n1, n2)
+    else:
+        w1 = codec.qsgd_encode(xk, nk, bits, gcodec.Generator(3, "philox").reserve(k), 2)
+        w1 = w1 * 2
+    world = 1 if k <= codec.RANDK_FUSED_MAX else 2
+    # flat: scatter into the bucket, then setgrad x 1/W; segments: copy + decode-scatter
+    flat = x.clone()
+    codec.qsgd_decode(w1, k, nk, bits, world, 1.0, idx=idx, out=flat)
+    want = flat * np.float32(1.0 / world) + 0.0
+    outs = [torch.full_like(t, 7.0) for t in ts]
+    osegs = codec.Segments(outs, chunk_shift=7)
+    codec.segments_copy(segs, osegs, 1.0 / world)
+    codec.qsgd_decode_scatter_segments(w1, idx, nk, bits, osegs, world, 1.0 / world)
+    assert u32(torch.cat(outs)).tobytes() == u32(want).tobytes()
+    with pytest.raises(gcodec.GCodecError):  # different tensor sizes
+        codec.segments_copy(segs, codec.Segments(outs[:-1]))
+
+
 REDUCERS = [
     ("QSGDMaxNormReducer", dict(quantization_level=4)),
     ("QSGDMaxNormTwoScaleReducer", dict(lower_quantization_level=2, higher_quantization_level=4)),
     ("QSGDMaxNormMultiScaleReducer", dict(quantization_levels=[2, 4, 6])),
     ("GlobalRandKMaxNormReducer", dict(K=1000, quantization_level=4)),
+    ("GlobalRandKMaxNormReducer", dict(K=20_000, quantization_level=4)),  # gather + encode (K > fused max)
+    ("GlobalRandKMaxNormReducer", dict(K=1000, quantization_level=16)),   # b above the fused lanes
     ("GlobalRandKMaxNormTwoScaleReducer", dict(K=1000, lower_quantization_level=2, higher_quantization_level=4)),
 ]
 

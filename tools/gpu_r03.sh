@@ -36,6 +36,7 @@ if has tests; then
 fi
 if has bench; then
   run bench 400 python3 $DRIVER
+  run torch_mode 300 python tools/time_torch_mode.py
   cd /tmp && export TMPDIR=/tmp
   run rocprof_driver 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG/driver" -o run -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5
   cd "$ROOT"

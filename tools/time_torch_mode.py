@@ -62,3 +62,17 @@ for G in (256, 320, 383, 448, 512, 640):
     torch.cuda.synchronize()
     print(f"buffer path, {G} generators: {(time.perf_counter() - t0) / REPS * 1e3:.3f} ms per call")
 codec.mt_generator_draws = orig
+
+# speculation on / off, and what the consumer waits for (the next run's jumps
+# or just this run's draws)
+for spec, wj in ((True, True), (True, False), (False, False)):
+    codec.MT_SPECULATE, codec.MT_WAIT_NEXT_JUMPS = spec, wj
+    call = lambda: codec.qsgd_encode(x, nm, 4, gen.reserve(n), 1, out=words, lanes=lanes)  # noqa: E731
+    call()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(REPS):
+        call()
+    torch.cuda.synchronize()
+    print(f"buffer path, speculate={spec}, wait next jumps={wj}: {(time.perf_counter() - t0) / REPS * 1e3:.3f} ms per call")
+codec.MT_SPECULATE, codec.MT_WAIT_NEXT_JUMPS = True, True
