@@ -429,17 +429,27 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     red4 = gcodec.GlobalRandKMaxNormReducer(dev, seed=42, K=K4, quantization_level=4, generator=gen)
     t_red = sync_ms(lambda: red4.reduce(gin4, gout4), reps=max(200, reps))
     segs_in, segs_out = codec.Segments(gin4), codec.Segments(gout4)
-    flat4 = torch.empty(n4, device=dev)
-    red_kernels = {"flatten_absmax": _events(torch, lambda: codec.segments_flatten_absmax(segs_in, flat4), 50),
-                   "setgrad_scatter": _events(torch, lambda: codec.segments_scatter(flat4, segs_out, 1.0 / world), 50)}
-    del gin4, gout4, red4, segs_in, segs_out, flat4
+    rgen = gcodec.Generator(3, "philox")
+    if codec.randk_fused_ok(K4, 4, world):
+        red_kernels = {"gather_absmax_encode_from_tensors": _events(
+            torch, lambda: codec.randk_encode_w1_segments(segs_in, idx, 4, rgen.reserve(K4)), 50)}
+    else:
+        red_kernels = {"gather_absmax_from_tensors": _events(
+            torch, lambda: codec.randk_gather_absmax_segments(segs_in, idx), 50)}
+    red_kernels["setgrad_tensor_to_tensor"] = _events(
+        torch, lambda: codec.segments_copy(segs_in, segs_out, 1.0 / world), 50)
+    red_kernels["decode_scatter_into_tensors"] = _events(
+        torch, lambda: codec.qsgd_decode_scatter_segments(rk.words, idx, rk.norm, 4, segs_out, world, 1.0 / world),
+        50)
+    del gin4, gout4, red4, segs_in, segs_out
     gpu_us = sum(kt4.values()) * 1e3
     res["config4_grandk_k10000"] = {
         "n": n4, "K": K4, "us_per_step": t * 1e3, "us_per_step_three_launch_codec_calls": t3 * 1e3,
         "reducer_us_per_step": t_red * 1e3,
         "reducer_kernels_us": {k: v * 1e3 for k, v in red_kernels.items()},
-        "reducer_step": "GlobalRandKMaxNormReducer.reduce(54 VGG16 tensors): fused flatten + norm, device index "
-                        "pop (one permutation upload per refill), the codec step above, setgrad of all n",
+        "reducer_step": "GlobalRandKMaxNormReducer.reduce(54 VGG16 tensors), no flat bucket: device index pop "
+                        "(one permutation upload per refill), gather + norm + encode read from the tensors, "
+                        "setgrad of all n tensor to tensor (x 1/W), decode-scatter into grad_out",
         "step": ("gather+absmax+encode (1 launch), decode-scatter" if rk.fused else
                  "gather+absmax, MAX, encode(gathered), SUM(words), decode-scatter"),
         "kernels_us": {k: v * 1e3 for k, v in kt4.items()},

@@ -8,6 +8,7 @@ SUM); the bits are the uint32 lane words of include/gcodec.h.
 from __future__ import annotations
 
 import ctypes as C
+import operator
 import functools
 
 import numpy as np
@@ -392,6 +393,9 @@ class RandKStep:
 # ---------------------------------------------------------------------------
 # per-parameter tensors (reducer.py:46-68 TensorBuffer, 543-549 setgrad)
 # ---------------------------------------------------------------------------
+_dtype_of = operator.attrgetter("dtype")
+
+
 class Segments:
     """gc_segments for a list of contiguous fp32 tensors on one device: the
     reference's TensorBuffer (reducer.py:46-68) as a device table, so flatten,
@@ -434,7 +438,11 @@ class Segments:
 
     @staticmethod
     def key_of(tensors):
-        return tuple((t.data_ptr(), t.numel(), t.dtype, t.device) for t in tensors)
+        """(data pointers, sizes, dtypes, device indices) of a tensor list.
+        Per-attribute maps: a reducer step computes this for two lists of
+        ~50-160 tensors, and per-tensor tuples cost ~2x as much host time."""
+        return (tuple(map(torch.Tensor.data_ptr, tensors)), tuple(map(torch.Tensor.numel, tensors)),
+                frozenset(map(_dtype_of, tensors)), frozenset(map(torch.Tensor.get_device, tensors)))
 
 
 def segments_flatten_absmax(segs: Segments, flat: torch.Tensor | None = None, norm: torch.Tensor | None = None,
@@ -462,7 +470,7 @@ def segments_scatter(flat: torch.Tensor, segs: Segments, alpha: float = 1.0):
 def segments_copy(src: Segments, dst: Segments, alpha: float = 1.0):
     """dst tensor element = RN(src tensor element * alpha) + 0 for two lists of
     the same tensor sizes (the GlobalRandK setgrad, reducer.py:759-761)."""
-    if [e[1] for e in src.key] != [e[1] for e in dst.key] or src.device != dst.device:
+    if src.key[1] != dst.key[1] or src.device != dst.device:
         raise _lib.GCodecError(_lib.GC_EINVAL, "segments_copy: the two lists differ in tensor sizes or device")
     check(_lib.load().gc_segments_copy(C.byref(src.struct), C.byref(dst.struct), float(alpha), _stream(src.device)),
           "gc_segments_copy")

@@ -115,13 +115,15 @@ class Reducer:
         tensors = list(tensors)
         if not self._fused or make is None or not tensors:
             return None
-        if any(not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous() for t in tensors):
+        if not all(map(torch.Tensor.is_contiguous, tensors)):
             return None
         # keyed by the tensors' data pointers and sizes: a table stays valid while
         # the list it describes lives at the same addresses (the caching
         # allocator usually hands a re-created p.grad the same block every step);
         # LRU, so the stable send-buffer entry survives reallocated grad lists
         key = make.key_of(tensors)
+        if key[2] != _F32_ONLY or len(key[3]) != 1 or min(key[3]) < 0:  # fp32, one GPU
+            return None
         segs = self._seg_cache.get(key)
         if segs is None:
             if len(self._seg_cache) >= self.SEG_CACHE:
@@ -149,6 +151,9 @@ class Reducer:
             if local is None or idx is not None:
                 local = self._codec.absmax(flat.buffer, idx=idx)
             return self._all_reduce(local, dist.ReduceOp.MAX)
+
+
+_F32_ONLY = frozenset((torch.float32,))
 
 
 class TensorBuffer:
@@ -282,12 +287,9 @@ class GlobalRandKMaxNormReducer(Reducer):
         codec = self._codec
         if not hasattr(codec, "randk_gather_absmax_segments"):
             return None
-        grad_in, grad_out = list(grad_in), list(grad_out)
-        if len(grad_in) != len(grad_out) or any(a.numel() != b.numel() for a, b in zip(grad_in, grad_out)):
-            return None
         in_segs = self._segments(grad_in)
         out_segs = self._segments(grad_out) if in_segs is not None else None
-        if out_segs is None or min(self._K, in_segs.n) > codec.RANDK_GATHER_MAX:
+        if out_segs is None or in_segs.key[1] != out_segs.key[1] or min(self._K, in_segs.n) > codec.RANDK_GATHER_MAX:
             return None
         return in_segs, out_segs
 
