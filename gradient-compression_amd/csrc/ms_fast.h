@@ -853,17 +853,38 @@ __device__ __forceinline__ void fused_accumulate(uint32_t n, uint32_t i0, uint32
     acc.w += (uint32_t)nq.w << sh;
 }
 
+// the fast path's range check with fewer instructions than RangeI: the low
+// bound on 2 bits(x) - 2 (one v_lshl_add per element; +-0 wrap high), the high
+// bound on max |x| as a float (v_max3_f32 with |.| modifiers, no shift).  A NaN
+// x is ignored by the float max, so it may take the fast path; both paths give
+// it the same bits (T = cvt_flr(NaN) + r = r >= 0 qualifies the top level with
+// xi = 0, as the generic rounding's med3(NaN) = 0 does).
+struct RangeM {
+    uint32_t mn = 0xffffffffu;
+    float mx = 0.0f;
+    __device__ __forceinline__ void add4(const float4 &v)
+    {
+        const uint32_t a = 2u * __float_as_uint(v.x) - 2u, b = 2u * __float_as_uint(v.y) - 2u;
+        const uint32_t c = 2u * __float_as_uint(v.z) - 2u, e = 2u * __float_as_uint(v.w) - 2u;
+        mn = min(mn, min(min(a, b), min(c, e)));
+        float m;
+        asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(m) : "v"(v.x), "v"(v.y), "v"(v.z));
+        asm("v_max3_f32 %0, |%1|, %2, %3" : "=v"(mx) : "v"(v.w), "v"(m), "v"(mx));
+    }
+    __device__ __forceinline__ bool slow(uint32_t lo2, float norm) const { return (mn < lo2) | (mx > norm); }
+};
+
 template <int KIND, int NL, int VAR>
 __device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
                                               uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
                                               const RngArgs &rng, uint32_t bitP, uint32_t sh,
                                               uint4 (&macc)[NL - 1], uint4 &acc)
 {
-    RangeI rg;
+    RangeM rg;
     rg.add4(v);
     uint4 mb[NL - 1];
     int4 nq;
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2))))
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, dv.norm))))
         fused_quad_fast<KIND, NL, VAR>(v, i0, dv, fa, rng, bitP, mb, nq);
     else
         fused_quad_slow<KIND, NL, VAR>(v, i0, dv, lv, rng, bitP, mb, nq);

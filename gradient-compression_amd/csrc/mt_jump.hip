@@ -157,7 +157,7 @@ static_assert((kMtJumpBits - 1) / 4 + kMtJumpThreads - 1 < kMtJumpQuads, "copy l
 constexpr uint64_t kWsPart = kWsWin + kMtN;
 
 __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws,
-                                                           uint32_t jumps)
+                                                           uint32_t jumps, const uint32_t *__restrict__ end_coef)
 {
     __shared__ uint4 cp4[4 * kMtJumpQuads];  // copy r: word u = x_{k0 + u + r + 1}
     __shared__ alignas(16) uint32_t pos[kMtJumpBits + 8];  // byte offset of set bit kk in its copy: ((kk&3)*Q + (kk>>2)) * 16
@@ -165,7 +165,9 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
     uint32_t *cp = reinterpret_cast<uint32_t *>(cp4);
     const uint32_t gi = blockIdx.x / kMtJumpSplit, sp = blockIdx.x % kMtJumpSplit;
     const uint32_t k0 = sp * kMtJumpBits, tid = threadIdx.x;
-    const uint32_t *__restrict__ coef = table + (uint64_t)gi * kMtN + sp * kMtJumpWords;
+    // slot jumps - 1 is the end window when end_coef is given (k_mt_end)
+    const uint32_t *__restrict__ coef =
+        (end_coef && gi == jumps - 1 ? end_coef : table + (uint64_t)gi * kMtN) + sp * kMtJumpWords;
     uint32_t c = 0;
     if (tid < kMtJumpWords) {
         c = coef[tid];
@@ -306,8 +308,8 @@ static_assert(kMtPre == 4 && kMtRounds == 3, "mt_wait_row's count");
 __device__ __forceinline__ void mt_wait_row() { asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); }
 
 template <int MODE>
-__global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t J,
-                                                         uint64_t count,
+__global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t jumps,
+                                                         uint64_t J, uint64_t count,
                                                          void *__restrict__ out, uint32_t *__restrict__ state,
                                                          const float *__restrict__ x, const float *__restrict__ normp,
                                                          float s)
@@ -323,7 +325,7 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
             uint32_t v = 0;
 #pragma unroll
             for (uint32_t sp = 0; sp < kMtJumpSplit; ++sp)
-                v ^= ws[kWsPart + (sp * (gens - 1) + g - 1) * kMtN + i];
+                v ^= ws[kWsPart + (sp * jumps + g - 1) * kMtN + i];
             buf[0][i] = v;
         }
     const uint32_t ptr0 = ws[0];
@@ -422,12 +424,39 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-bound load outlives the workgroup
     }
     __syncthreads();
-    if (g == gens - 1) {  // the advanced state: the last block (aligned to the twist blocks) + read index
+    if (state && g == gens - 1) {  // the advanced state: the last block (aligned to the twist blocks) + read index
         for (uint32_t i = tid; i < kMtN; i += kMtGenThreads)
             state[i] = buf[twists & 1u][i];
         if (tid == 0)
             state[kMtN] = twists ? (uint32_t)(rest - (uint64_t)(twists - 1) * kMtN) : ptr0 + head;
     }
+}
+
+// the state after `count` draws without generating them: raw block B =
+// floor((idx + count - 1) / 624) of the caller's frame (block 0 = the state
+// itself) is the window at raw position 624 B, jumped by k_mt_jump's end slot
+// (coefficients x^(624 B - 1) mod P); the read index becomes idx + count - 624 B
+// (in 1 .. 624).  Written over the caller's state in place (k_mt_seq has
+// already copied it into the workspace), so the next call's sequence can start
+// while this call's generators still run.
+__global__ __launch_bounds__(256) void k_mt_end(uint32_t *__restrict__ ws, uint32_t jumps, uint64_t count,
+                                                uint64_t end_block, uint32_t *__restrict__ state)
+{
+    const uint32_t ptr0 = ws[0];
+    for (uint32_t i = threadIdx.x; i < kMtN; i += 256) {
+        uint32_t v;
+        if (end_block == 0) {
+            v = ws[kWsWin + i];
+        } else {
+            v = 0;
+#pragma unroll
+            for (uint32_t sp = 0; sp < kMtJumpSplit; ++sp)
+                v ^= ws[kWsPart + ((uint64_t)sp * jumps + jumps - 1) * kMtN + i];
+        }
+        state[i] = v;
+    }
+    if (threadIdx.x == 0)  // a caller whose end_block does not match idx gets an impossible index (> 624)
+        state[kMtN] = (uint32_t)(ptr0 + count - kMtN * end_block);
 }
 
 }  // namespace gc
@@ -439,7 +468,7 @@ extern "C" {
 size_t gc_mt19937_workspace_size_j(uint64_t count, uint64_t J)
 {
     const uint64_t gens = count && J ? (count + J - 1) / J : 1;
-    return 4 * (kWsPart + kMtJumpSplit * (gens - 1) * kMtN);
+    return 4 * (kWsPart + kMtJumpSplit * gens * kMtN);  // gens - 1 generator windows + the end window
 }
 
 size_t gc_mt19937_workspace_size(uint64_t count) { return gc_mt19937_workspace_size_j(count, GC_MT_JUMP_DRAWS); }
@@ -447,12 +476,15 @@ size_t gc_mt19937_workspace_size(uint64_t count) { return gc_mt19937_workspace_s
 // seq -> jump -> gen<MODE> for `count` draws of state_dev, generators of J draws
 // (phase bit 1: seq + jump, bit 2: gen; the two halves of one run must be
 // enqueued in order on one stream with the same arguments)
+// SPLIT (gc_mt19937_generate_split_j): phase 1 also jumps to the end state and
+// writes it over state_dev (k_mt_end); the generators then leave the state alone
 static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens,
                   uint64_t J, void *out, uint64_t count, void *workspace, gc_stream_t stream, const float *x,
-                  const float *norm, float s, int phase = 3)
+                  const float *norm, float s, int phase = 3, bool split = false, const uint32_t *end_coef = nullptr,
+                  uint64_t end_block = 0)
 {
     GC_REQUIRE(state_dev && workspace, "%s: null state/workspace", what);
-    GC_REQUIRE(count == 0 || out, "%s: null out", what);
+    GC_REQUIRE(count == 0 || out || !(phase & 2), "%s: null out", what);
     GC_REQUIRE(J > 0 && J % kMtN == 0, "%s: J = %llu is not a positive multiple of 624", what, (unsigned long long)J);
     if (count == 0)
         return GC_OK;
@@ -461,25 +493,31 @@ static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_
                "%s: jump table holds %llu generators, %llu draws need %llu", what, (unsigned long long)table_gens,
                (unsigned long long)count, (unsigned long long)(gens - 1));
     GC_REQUIRE(gens <= 0x7fffffffull / kMtJumpSplit, "%s: count too large", what);
+    const bool has_end = split && end_block > 0;
+    GC_REQUIRE(!has_end || end_coef, "%s: null end coefficients", what);
+    const uint32_t jumps = (uint32_t)(gens - 1 + (has_end ? 1 : 0));
     hipStream_t st = as_stream(stream);
     uint32_t *ws = reinterpret_cast<uint32_t *>(workspace);
     if (phase & 1) {
         hipLaunchKernelGGL(k_mt_seq, dim3(1), dim3(256), 0, st, state_dev, ws);
-        if (gens > 1)
-            hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)((gens - 1) * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st,
-                               table_dev, ws, (uint32_t)(gens - 1));
+        if (jumps > 0)
+            hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)(jumps * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st,
+                               table_dev, ws, jumps, has_end ? end_coef : nullptr);
+        if (split)
+            hipLaunchKernelGGL(k_mt_end, dim3(1), dim3(256), 0, st, ws, jumps, count, end_block, state_dev);
     }
     if (!(phase & 2))
         return launch_status(what);
+    uint32_t *gstate = split ? nullptr : state_dev;
     if (mode == 0)
-        hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, J, count, out,
-                           state_dev, x, norm, s);
+        hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
+                           J, count, out, gstate, x, norm, s);
     else if (mode == 1)
-        hipLaunchKernelGGL(k_mt_gen<1>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, J, count, out,
-                           state_dev, x, norm, s);
+        hipLaunchKernelGGL(k_mt_gen<1>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
+                           J, count, out, gstate, x, norm, s);
     else
-        hipLaunchKernelGGL(k_mt_gen<2>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, J, count, out,
-                           state_dev, x, norm, s);
+        hipLaunchKernelGGL(k_mt_gen<2>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
+                           J, count, out, gstate, x, norm, s);
     return launch_status(what);
 }
 
@@ -496,6 +534,16 @@ int gc_mt19937_generate_phase_j(uint32_t *state_dev, const uint32_t *table_dev, 
     GC_REQUIRE(phase >= 1 && phase <= 3, "gc_mt19937_generate_phase_j: phase must be 1, 2 or 3");
     return mt_run("gc_mt19937_generate_phase_j", 0, state_dev, table_dev, table_gens, J, out, count, workspace, stream,
                   nullptr, nullptr, 0.0f, phase);
+}
+
+int gc_mt19937_generate_split_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                const uint32_t *end_coef, uint64_t end_block, uint32_t *out, uint64_t count,
+                                void *workspace, int phase, gc_stream_t stream)
+{
+    GC_REQUIRE(phase >= 1 && phase <= 3, "gc_mt19937_generate_split_j: phase must be 1, 2 or 3");
+    GC_REQUIRE(count > 0, "gc_mt19937_generate_split_j: count must be positive");
+    return mt_run("gc_mt19937_generate_split_j", 0, state_dev, table_dev, table_gens, J, out, count, workspace, stream,
+                  nullptr, nullptr, 0.0f, phase, true, end_coef, end_block);
 }
 
 int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,

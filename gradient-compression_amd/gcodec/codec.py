@@ -884,51 +884,100 @@ def qsgd_encode_torch(x, norm, bits, world=1, out=None, lanes=None) -> torch.Ten
     return out
 
 
-_MT_SIDE = {}  # device index -> the side stream torch-mode draws are generated on
+_MT_SIDE = {}  # device index -> (jump stream, generator stream) the torch-mode draws are made on
 _MT_LAST = {}  # device index -> (624 words, read index) last written back to torch
 _MT_SPEC = {}  # device index -> the speculative run of the next same-size call
+_MT_END = {}   # (device index, end block B) -> device coefficients of x^(624 B - 1) mod P
+_MT_WSS = {}   # (device index, slot) -> workspace of the runs in that slot
+_MT_BUSY = {}  # (device index, slot) -> event after the last generators that read the slot's workspace
 MT_SPECULATE = True  # generate the draws of the next same-size torch-mode call ahead (mt19937_draws)
-MT_WAIT_NEXT_JUMPS = True  # consumers also wait for the speculative run's jumps (mt19937_draws)
+MT_WAIT_NEXT_JUMPS = False  # consumers also wait for the speculative run's jumps (mt19937_draws)
 
 
-def _mt_side(device) -> torch.cuda.Stream:
-    """High priority: the draw generation is the serial chain of the torch-mode
-    encode; the encodes it overlaps fill the CUs it leaves idle."""
+def _mt_side(device):
+    """Two high-priority streams: the jumps (LDS-bound; they also produce the
+    end state) and the generators (latency-bound).  The draw generation is the
+    serial chain of the torch-mode encode; the encodes it overlaps fill the
+    CUs it leaves idle, and the next call's jumps run beside this call's
+    generators."""
     s = _MT_SIDE.get(device.index)
     if s is None:
         lo, hi = torch.cuda.Stream.priority_range()
-        s = _MT_SIDE[device.index] = torch.cuda.Stream(device, priority=min(lo, hi))
+        s = _MT_SIDE[device.index] = (torch.cuda.Stream(device, priority=min(lo, hi)),
+                                      torch.cuda.Stream(device, priority=min(lo, hi)))
     return s
 
 
+def _mt_end_coef(dev, block: int):
+    """Coefficients of the jump to raw block `block` (x^(624 block - 1) mod P)
+    on the device, cached: a bucket size takes at most two end blocks."""
+    if block == 0:
+        return None
+    key = (dev.index, block)
+    t = _MT_END.get(key)
+    if t is None:
+        host = np.empty(624, dtype=np.uint32)
+        check(_lib.load().gc_mt19937_jump_table_j(624 * block, 1, 1, host.ctypes.data_as(C.c_void_p)),
+              "gc_mt19937_jump_table_j")
+        if len(_MT_END) >= 64:
+            _MT_END.clear()
+        t = _MT_END[key] = torch.from_numpy(host.view(np.int32)).to(dev)  # synchronous: ready on any stream
+    return t
+
+
+def _mt_ws_slot(dev, slot: int, count: int, J: int) -> torch.Tensor:
+    need = int(_lib.load().gc_mt19937_workspace_size_j(count, J))
+    key = (dev.index, slot)
+    ws = _MT_WSS.get(key)
+    if ws is None or ws.numel() < need:
+        busy = _MT_BUSY.get(key)
+        if busy is not None:
+            busy.synchronize()  # the old buffer may still be read by queued generators
+        ws = _MT_WSS[key] = torch.empty(need, dtype=torch.uint8, device=dev)
+    return ws
+
+
 class _MtRun:
-    """One enqueued generation: its draws, the pinned slot its final state goes
-    to, and events after its jumps and after that state copy."""
+    """One enqueued generation: its draws, the read index after it, the pinned
+    slot its end state goes to, and events after its jumps (p1), after that
+    state's copy to the host (state_ready) and after its generators (done)."""
 
-    __slots__ = ("count", "out", "slot", "jumped", "done")
+    __slots__ = ("count", "out", "slot", "idx_end", "p1", "state_ready", "done")
 
 
-def _mt_enqueue(dev, st_dev, count: int, hout, slot: int) -> _MtRun:
-    """On the current (side) stream: seq + jumps, an event, the generators
-    (out, and st_dev advanced by count draws), the state into hout[slot]."""
+def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int) -> _MtRun:
+    """Phase 1 on the jump stream: sequence + jumps + the end state (written
+    over st_dev, gc_mt19937_generate_split_j) and its copy into hout[slot];
+    phase 2 on the generator stream, after phase 1: the draws."""
     J = mt_generator_draws(count)
     gens = -(-count // J)
     table, tgens = _mt_jump_table(dev, gens - 1, J) if gens > 1 else (None, 0)
-    st = _stream(dev)
-    ws = _mt_ws(dev, st, count, J)
-    run = _MtRun()
-    run.count, run.slot = count, slot
-    run.out = torch.empty(count, dtype=torch.int32, device=dev)
+    block = (idx + count - 1) // 624
+    end = _mt_end_coef(dev, block)
+    js, gs = _mt_side(dev)
+    ws = _mt_ws_slot(dev, slot, count, J)
+    busy = _MT_BUSY.get((dev.index, slot))
     lib = _lib.load()
-    check(lib.gc_mt19937_generate_phase_j(_p(st_dev), _p(table), tgens, J, _p(run.out), count, _p(ws), 1, st),
-          "gc_mt19937_generate_phase_j")
-    run.jumped = torch.cuda.Event()
-    run.jumped.record()
-    check(lib.gc_mt19937_generate_phase_j(_p(st_dev), _p(table), tgens, J, _p(run.out), count, _p(ws), 2, st),
-          "gc_mt19937_generate_phase_j")
-    hout[slot].copy_(st_dev, non_blocking=True)
-    run.done = torch.cuda.Event()
-    run.done.record()
+    run = _MtRun()
+    run.count, run.slot, run.idx_end = count, slot, idx + count - 624 * block
+    with torch.cuda.stream(js):
+        if busy is not None:
+            js.wait_event(busy)  # that slot's previous generators have read the workspace
+        check(lib.gc_mt19937_generate_split_j(_p(st_dev), _p(table), tgens, J, _p(end), block, None, count, _p(ws),
+                                              1, _stream(dev)), "gc_mt19937_generate_split_j")
+        run.p1 = torch.cuda.Event()
+        run.p1.record()
+        hout[slot].copy_(st_dev, non_blocking=True)
+        run.state_ready = torch.cuda.Event()
+        run.state_ready.record()
+    with torch.cuda.stream(gs):
+        gs.wait_event(run.p1)
+        run.out = torch.empty(count, dtype=torch.int32, device=dev)
+        check(lib.gc_mt19937_generate_split_j(_p(st_dev), _p(table), tgens, J, _p(end), block, _p(run.out), count,
+                                              _p(ws), 2, _stream(dev)), "gc_mt19937_generate_split_j")
+        run.done = torch.cuda.Event()
+        run.done.record()
+    _MT_BUSY[(dev.index, slot)] = run.done
     return run
 
 
@@ -937,18 +986,18 @@ def mt19937_draws(count: int, device) -> torch.Tensor:
     generator state advances exactly as torch.bernoulli would advance it
     (synchronously: the new state is in torch's generator when this returns).
 
-    The draws are generated on a high-priority side stream
-    (gc_mt19937_generate_phase_j: the state's sequence and the LDS-bound jumps,
-    then the latency-bound generators); the host waits for that stream only,
-    never for the caller's queued work.  With MT_SPECULATE the next call's
-    draws (same count, continuing from this call's final state) are enqueued
-    right behind, so back-to-back calls find their draws generated or in
-    flight; a speculative run is used only if torch's generator is exactly
-    where the previous call left it and the count matches, else it is dropped
-    and the state is sent to the device again.  The caller's stream then
-    waits on the speculative run's jumps as well: its consumer (the encode,
-    HBM-bound) runs beside the latency-bound generators instead of competing
-    with the LDS-bound jumps."""
+    The draws are generated on two high-priority side streams
+    (gc_mt19937_generate_split_j): phase 1 (jump stream) = the state's
+    sequence, the LDS-bound jumps and one more jump straight to the END state;
+    phase 2 (generator stream) = the latency-bound generators.  The host waits
+    only for the end state (phase 1 and a 2.5 KB copy), never for the draws or
+    the caller's queued work; the caller's stream waits for the draws.  With
+    MT_SPECULATE the next call's run (same count, from this call's end state)
+    is enqueued right behind, so its jumps run beside this call's generators
+    and its generators beside this call's consumer; a speculative run is used
+    only if torch's generator is exactly where the previous call left it and
+    the count matches, else it is dropped and the state is sent to the device
+    again."""
     from .rng import set_torch_mt_state, torch_mt_state
 
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -957,7 +1006,7 @@ def mt19937_draws(count: int, device) -> torch.Tensor:
     words, idx = torch_mt_state()
     hin, hout, dst = _mt_bufs(device)
     cur = torch.cuda.current_stream(device)
-    side = _mt_side(device)
+    js, _ = _mt_side(device)
     last = _MT_LAST.get(device.index)
     untouched = last is not None and last[1] == idx and np.array_equal(last[0], words)
     spec = _MT_SPEC.pop(device.index, None)
@@ -965,22 +1014,24 @@ def mt19937_draws(count: int, device) -> torch.Tensor:
         if spec is not None:  # a dropped run still moves dst on: send the state next time
             _MT_LAST.pop(device.index, None)
         return torch.empty(0, dtype=torch.int32, device=device)
-    with torch.cuda.stream(side):
-        if spec is not None and untouched and spec.count == count:
-            run = spec
-        else:
-            if spec is not None or not untouched:  # dst is not torch's state: send it
+    if spec is not None and untouched and spec.count == count:
+        run = spec
+    else:
+        if spec is not None or not untouched:  # dst is not torch's state: send it
+            with torch.cuda.stream(js):
                 h = hin.numpy().view(np.uint32)  # free: earlier copies from it were waited for
                 h[:624] = words
                 h[624] = idx
                 dst.copy_(hin, non_blocking=True)
-            run = _mt_enqueue(device, dst, count, hout, spec.slot ^ 1 if spec is not None else 0)
-        nxt = _mt_enqueue(device, dst, count, hout, run.slot ^ 1) if MT_SPECULATE else None
-    cur.wait_event(nxt.jumped if nxt is not None and MT_WAIT_NEXT_JUMPS else run.done)
+        run = _mt_enqueue(device, dst, count, int(idx), hout, spec.slot ^ 1 if spec is not None else 0)
+    nxt = _mt_enqueue(device, dst, count, run.idx_end, hout, run.slot ^ 1) if MT_SPECULATE else None
+    cur.wait_event(run.done)
+    if nxt is not None and MT_WAIT_NEXT_JUMPS:
+        cur.wait_event(nxt.p1)
     run.out.record_stream(cur)
     if nxt is not None:
         _MT_SPEC[device.index] = nxt
-    run.done.synchronize()
+    run.state_ready.synchronize()
     new = hout[run.slot].numpy().view(np.uint32)
     w2, i2 = new[:624].copy(), int(new[624])
     set_torch_mt_state(w2, i2)

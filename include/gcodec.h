@@ -348,6 +348,20 @@ int gc_mt19937_generate_jumped_j(uint32_t *state_dev, const uint32_t *table_dev,
  * arguments; an event between them marks the end of the jumps. */
 int gc_mt19937_generate_phase_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
                                 uint32_t *out, uint64_t count, void *workspace, int phase, gc_stream_t stream);
+/* the run split so that the END STATE is known before any draw exists (for
+ * pipelining back-to-back calls): phase 1 = the sequence + the jumps + one more
+ * jump to the state after `count` draws, written over state_dev (625 words);
+ * phase 2 = the generators (out only; they read the workspace, not state_dev,
+ * so the next run's phase 1 may start on another stream once this phase 1 is
+ * done, with its own workspace).  end_block = floor((idx + count - 1) / 624)
+ * for the state's read index idx (the host knows it: torch's generator state);
+ * end_coef = gc_mt19937_jump_table_j(624 * end_block, 1, 1) on the device
+ * (NULL when end_block = 0).  The new read index is idx + count - 624 end_block;
+ * an end_block that does not match idx yields an index above 624.  Workspace as
+ * gc_mt19937_workspace_size_j(count, J). */
+int gc_mt19937_generate_split_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                const uint32_t *end_coef, uint64_t end_block, uint32_t *out, uint64_t count,
+                                void *workspace, int phase, gc_stream_t stream);
 /* torch-mode QSGD quantize with the MT19937 draws consumed in-kernel (never
  * stored): q[i] = sign(x_i)*xi_i exactly as compressors.py:299-316 computes it
  * under torch.bernoulli (one draw per element, in order), as GC_I8 (bits <= 7)

@@ -1001,6 +1001,36 @@ def test_ms_encode_w1_matches_two_pass_and_oracle(levels, n):
         assert bits_eq(u32(words), O.lane_pack(q_ref, ql.offset, ql.bits, ql.per_word, ql.plane_words))
 
 
+@pytest.mark.parametrize("levels", [(2, 4), (4, 8), (2, 4, 6)])
+def test_ms_encode_w1_non_finite_given_norm(levels):
+    """the one-pass encode with a caller's finite norm below max |x| and NaN,
+    +-inf, |x| > norm, subnormal, tiny and -0 inputs scattered over the bucket
+    (a NaN may take the fast branch: RangeM ignores it) == the
+    two-pass kernels == the oracle."""
+    n = 7 * 4 * 4096 + 9
+    L = len(levels)
+    x = O.gen_input(n, seed=21)
+    x[::997] = np.nan
+    x[5::1001] = np.inf
+    x[7::1003] = -np.inf
+    x[11::889] = np.float32(3e-41)
+    x[13::883] = np.float32(-1e-35)
+    x[19::773] = 0.25
+    x[23::71] = -0.0
+    norm = np.float32(np.nanmax(np.abs(x[np.isfinite(x)])) / 4)
+    r = gcodec.rng.Reservation(0, 5 + L, 3, None, n, L)
+    xd = dev(x)
+    mw, words = codec.ms_encode_w1(xd, float(norm), levels, r)
+    mw2 = codec.ms_mask_encode(xd, float(norm), levels, r, 1)
+    assert torch.equal(mw, mw2)
+    assert torch.equal(words, codec.ms_select_encode(xd, float(norm), levels, r, mw2, 1))
+    m_ref = O.ms_mask(x, norm, levels, O.philox_rng(5 + L, 3))
+    assert bits_eq(codec.ms_mask_unpack(mw, n, levels, 1).cpu().numpy().astype(np.uint8), m_ref)
+    q_ref = O.ms_select(x, norm, levels, O.philox_rng(5 + L, 3), m_ref)
+    ql, _ = codec.ms_layouts(n, levels, 1)
+    assert bits_eq(u32(words), O.lane_pack(q_ref, ql.offset, ql.bits, ql.per_word, ql.plane_words))
+
+
 @pytest.mark.parametrize("name", ["ms_2_4_1e6", "ms_4_8_1e6"])
 def test_ms_encode_w1_torch_mode_digests(name):
     """the one-pass W = 1 encode with torch-mode draws (caller stream, KIND 1)

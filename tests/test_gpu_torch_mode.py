@@ -79,3 +79,43 @@ def test_torch_mode_compressor_back_to_back_vs_oracle():
             assert np.array_equal(q.cpu().numpy().astype(np.int32), np.asarray(exp, dtype=np.int32)), i
     finally:
         gcodec.set_rng_mode("philox")
+
+
+@pytest.mark.parametrize("idx,count", [(0, 1), (623, 1), (624, 1), (5, 619), (5, 620), (0, 624), (624, 624),
+                                       (3, 1248), (100, 2 * 262_080 + 17), (624, 3_000_001), (17, 10_000_000)])
+def test_split_end_state_vs_serial_stream(idx, count):
+    """gc_mt19937_generate_split_j: the end state jumped to directly in phase 1
+    (written over the device state before any draw exists) equals the serial
+    generator's state after `count` draws, including the read index, for read
+    indices 0 / mid / 624 and counts inside block 0, ending exactly on a block
+    boundary, and spanning many generators; the draws of phase 2 equal the
+    serial stream's."""
+    import ctypes as C
+    from gcodec import _lib
+
+    st = O.MT19937(1234)
+    st.draws(1000)
+    st._st.idx = idx
+    w0, i0 = st.state()
+    ref = st.draws(count)
+    w1, i1 = st.state()
+    state = torch.from_numpy(np.append(np.asarray(w0, np.uint32), np.uint32(i0)).view(np.int32)).to(DEV)
+    J = codec.mt_generator_draws(count)
+    gens = -(-count // J)
+    table, tgens = codec._mt_jump_table(DEV, gens - 1, J) if gens > 1 else (None, 0)
+    block = (idx + count - 1) // 624
+    end = codec._mt_end_coef(DEV, block)
+    ws = torch.empty(int(_lib.load().gc_mt19937_workspace_size_j(count, J)), dtype=torch.uint8, device=DEV)
+    out = torch.empty(count, dtype=torch.int32, device=DEV)
+    lib = _lib.load()
+    p = lambda t: None if t is None else C.c_void_p(t.data_ptr())  # noqa: E731
+    s = codec._stream(DEV)
+    assert lib.gc_mt19937_generate_split_j(p(state), p(table), tgens, J, p(end), block, None, count, p(ws), 1, s) == 0
+    torch.cuda.synchronize()
+    got = state.cpu().numpy().view(np.uint32)
+    assert int(got[624]) == i1 and np.array_equal(got[:624], np.asarray(w1, np.uint32))
+    assert lib.gc_mt19937_generate_split_j(p(state), p(table), tgens, J, p(end), block, p(out), count, p(ws), 2, s) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), np.asarray(ref, np.uint32))
+    # the state is left alone by phase 2
+    assert np.array_equal(state.cpu().numpy().view(np.uint32), got)

@@ -13,7 +13,7 @@ import torch  # noqa: E402
 import gcodec  # noqa: E402
 from gcodec import codec  # noqa: E402
 
-REPS = 10
+REPS = 20
 dev = torch.device("cuda", 0)
 n = 100_000_000
 x = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(1)).mul_(0.01)
@@ -75,4 +75,4 @@ for spec, wj in ((True, True), (True, False), (False, False)):
         call()
     torch.cuda.synchronize()
     print(f"buffer path, speculate={spec}, wait next jumps={wj}: {(time.perf_counter() - t0) / REPS * 1e3:.3f} ms per call")
-codec.MT_SPECULATE, codec.MT_WAIT_NEXT_JUMPS = True, True
+codec.MT_SPECULATE, codec.MT_WAIT_NEXT_JUMPS = True, False
