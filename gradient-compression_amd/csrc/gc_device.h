@@ -73,6 +73,69 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
     return c;
 }
 
+// Philox4x32-10 of the counter (g, y, z, w) when only g varies across the
+// wave and y, z, w and the key are uniform (the draws4 counter: quad index,
+// level, call offset): the same outputs as philox4x32_10, with the uniform
+// halves of rounds 1-3 kept on the scalar unit and every XOR of two uniform
+// terms folded before it meets a per-lane one (round 1: one product and one
+// XOR per lane; round 2: one product, two XORs; round 3: the full round with
+// one 2-input XOR).  About 3 VALU instructions fewer per block than the
+// generic rounds, which leave the compiler 3-input XORs of two SGPRs (a
+// v_mov each, the constant-bus limit) and no pre-folding.
+__device__ __forceinline__ uint4 philox4x32_10_g(uint32_t g, uint32_t y, uint32_t z, uint32_t w, uint32_t k0,
+                                                 uint32_t k1)
+{
+    constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, C0 = 0x9E3779B9u, C1 = 0xBB67AE85u;
+    // the folded uniform terms pass through an empty asm on an SGPR, so the
+    // compiler cannot re-associate them back into two per-lane XORs
+    auto fold = [](uint32_t v) {
+        asm("" : "+s"(v));
+        return v;
+    };
+    // round 1: p1 = M1 z is uniform
+    const uint64_t a0 = (uint64_t)M0 * g;
+    const uint64_t a1 = (uint64_t)M1 * z;
+    const uint32_t ux = (uint32_t)(a1 >> 32) ^ y ^ k0;  // uniform
+    const uint32_t uy = (uint32_t)a1;                   // uniform
+    const uint32_t vz = (uint32_t)(a0 >> 32) ^ fold(w ^ k1);
+    const uint32_t vw = (uint32_t)a0;
+    // round 2: p0 = M0 ux is uniform
+    const uint64_t b0 = (uint64_t)M0 * ux;
+    const uint64_t b1 = (uint64_t)M1 * vz;
+    uint4 c;
+    c.x = (uint32_t)(b1 >> 32) ^ fold(uy ^ (k0 + C0));
+    c.y = (uint32_t)b1;
+    c.z = vw ^ fold((uint32_t)(b0 >> 32) ^ (k1 + C1));
+    const uint32_t uw = (uint32_t)b0;  // uniform
+    // round 3: c.w uniform
+    {
+        const uint64_t p0 = (uint64_t)M0 * c.x;
+        const uint64_t p1 = (uint64_t)M1 * c.z;
+        uint4 o;
+        o.x = xor3((uint32_t)(p1 >> 32), c.y, k0 + 2u * C0);
+        o.z = (uint32_t)(p0 >> 32) ^ fold(uw ^ (k1 + 2u * C1));
+        o.y = (uint32_t)p1;
+        o.w = (uint32_t)p0;
+        c = o;
+    }
+    k0 += 3u * C0;
+    k1 += 3u * C1;
+#pragma unroll
+    for (int r = 3; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)M0 * c.x;
+        const uint64_t p1 = (uint64_t)M1 * c.z;
+        uint4 o;
+        o.x = xor3((uint32_t)(p1 >> 32), c.y, k0);
+        o.z = xor3((uint32_t)(p0 >> 32), c.w, k1);
+        o.y = (uint32_t)p1;
+        o.w = (uint32_t)p0;
+        c = o;
+        k0 += C0;
+        k1 += C1;
+    }
+    return c;
+}
+
 // Four draws for elements i0..i0+3 (i0 % 4 == 0) at scale `level`.
 template <int KIND, int IMPL = GC_PHILOX_IMPL>
 __device__ __forceinline__ uint4 draws4(const RngArgs &r, uint32_t level, uint64_t i0)
@@ -84,6 +147,10 @@ __device__ __forceinline__ uint4 draws4(const RngArgs &r, uint32_t level, uint64
         c.y = ((uint32_t)(g >> 32) & 0xffffu) | (level << 16);
         c.z = (uint32_t)r.offset;
         c.w = (uint32_t)(r.offset >> 32);
+        if constexpr (IMPL == 1) {
+            if (i0 < (1ull << 34))  // g < 2^32: c.y is the uniform level word
+                return philox4x32_10_g(c.x, level << 16, c.z, c.w, (uint32_t)r.seed, (uint32_t)(r.seed >> 32));
+        }
         return philox4x32_10<IMPL>(c, (uint32_t)r.seed, (uint32_t)(r.seed >> 32));
     } else {
         const uint32_t *p = r.stream + (uint64_t)level * r.n + i0;

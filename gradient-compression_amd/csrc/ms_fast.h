@@ -211,10 +211,16 @@ __device__ __forceinline__ void cache_store(void *__restrict__ cache, uint32_t i
     typedef typename CacheCell<CBY>::T T;
     T *p = reinterpret_cast<T *>(cache) + i0;
     if (i0 + 4 <= n) {  // i0 % 4 == 0: 4- / 8-byte aligned
-        if constexpr (CBY == 1)
-            *reinterpret_cast<uint32_t *>(p) = c.x | (c.y << 8) | (c.z << 16) | (c.w << 24);
-        else
-            *reinterpret_cast<uint2 *>(p) = make_uint2(c.x | (c.y << 16), c.z | (c.w << 16));
+        // v_perm_b32 byte selects: each cell truncated to its CBY bytes (the top
+        // field may carry garbage above the cell, mask_plane)
+        if constexpr (CBY == 1) {
+            const uint32_t lo = __builtin_amdgcn_perm(c.y, c.x, 0x0c0c0400u);  // [x0 y0 0 0]
+            const uint32_t hi = __builtin_amdgcn_perm(c.w, c.z, 0x0c0c0400u);  // [z0 w0 0 0]
+            *reinterpret_cast<uint32_t *>(p) = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+        } else {
+            *reinterpret_cast<uint2 *>(p) = make_uint2(__builtin_amdgcn_perm(c.y, c.x, 0x05040100u),
+                                                       __builtin_amdgcn_perm(c.w, c.z, 0x05040100u));
+        }
         return;
     }
     p[0] = (T)c.x;
@@ -255,6 +261,27 @@ __device__ __forceinline__ uint4 cache_cells(const uint2 &u)
         return make_uint4(u.x & 0xffffu, u.x >> 16, u.y & 0xffffu, u.y >> 16);
 }
 
+// the fast path's range check with fewer instructions than RangeI: the low
+// bound on 2 bits(x) - 2 (one v_lshl_add per element; +-0 wrap high), the high
+// bound on max |x| as a float (v_max3_f32 with |.| modifiers, no shift).  A NaN
+// x is ignored by the float max, so it may take the fast path; both paths give
+// it the same bits (T = cvt_flr(NaN) + r = r >= 0 qualifies the top level with
+// xi = 0, as the generic rounding's med3(NaN) = 0 does).
+struct RangeM {
+    uint32_t mn = 0xffffffffu;
+    float mx = 0.0f;
+    __device__ __forceinline__ void add4(const float4 &v)
+    {
+        const uint32_t a = 2u * __float_as_uint(v.x) - 2u, b = 2u * __float_as_uint(v.y) - 2u;
+        const uint32_t c = 2u * __float_as_uint(v.z) - 2u, e = 2u * __float_as_uint(v.w) - 2u;
+        mn = min(mn, min(min(a, b), min(c, e)));
+        float m;
+        asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(m) : "v"(v.x), "v"(v.y), "v"(v.z));
+        asm("v_max3_f32 %0, |%1|, %2, %3" : "=v"(mx) : "v"(v.w), "v"(m), "v"(mx));
+    }
+    __device__ __forceinline__ bool slow(uint32_t lo2, float norm) const { return (mn < lo2) | (mx > norm); }
+};
+
 // ---------------------------------------------------------------------------
 // per-plane work (4 elements i0..i0+3 of one plane)
 // ---------------------------------------------------------------------------
@@ -272,10 +299,10 @@ __device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t
                                            uint32_t cb = 0, uint4 *cv = nullptr)
 {
     const float4 v = load4_nt_tail<0>(x, i0, n);
-    RangeI rg;
+    RangeM rg;
     rg.add4(v);
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, dv.norm)))) {
         const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
         // cache lanes: -q = (T >> 24) * sign (0 for +-0, whose T is >= 0)
         int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
@@ -300,22 +327,28 @@ __device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t
                 mb[l - 1] = make_uint4(k0 ? bit : 0u, k1 ? bit : 0u, k2 ? bit : 0u, k3 ? bit : 0u);
             }
             if constexpr (CACHE) {
-                // level 0 has |q| <= s_0 <= cq (no clamp); the levels above are
-                // clamped (an unchosen level's field is never read, but must not
-                // spill into the next field)
+                // c accumulates sum_l -q_l << (l cb); the cell is then
+                // sum_l cq << (l cb) - c (ms_cells).  Level 0 has |q| <= s_0 <=
+                // cq (no clamp); the middle levels are clamped (an unchosen
+                // level's field is never read, but must not borrow from the
+                // next field); the top field may hold garbage above its cb
+                // bits: nothing reads them and the cell store truncates
                 const uint32_t sh = (uint32_t)l * cb;
-                const int32_t n0 = __mul24(t0 >> 24, s0), n1 = __mul24(t1 >> 24, s1);
-                const int32_t n2 = __mul24(t2 >> 24, s2), n3 = __mul24(t3 >> 24, s3);
-                if (l == 0) {
-                    c.x |= (uint32_t)(cq - n0);
-                    c.y |= (uint32_t)(cq - n1);
-                    c.z |= (uint32_t)(cq - n2);
-                    c.w |= (uint32_t)(cq - n3);
+                int32_t n0 = __mul24(t0 >> 24, s0), n1 = __mul24(t1 >> 24, s1);
+                int32_t n2 = __mul24(t2 >> 24, s2), n3 = __mul24(t3 >> 24, s3);
+                if (l > 0 && l < NL - 1) {
+                    n0 = med3_i32(n0, -cq, cq);
+                    n1 = med3_i32(n1, -cq, cq);
+                    n2 = med3_i32(n2, -cq, cq);
+                    n3 = med3_i32(n3, -cq, cq);
+                }
+                if (l == NL - 1) {
+                    c = make_uint4((uint32_t)n0 << sh, (uint32_t)n1 << sh, (uint32_t)n2 << sh, (uint32_t)n3 << sh);
                 } else {
-                    c.x |= (uint32_t)(cq - med3_i32(n0, -cq, cq)) << sh;
-                    c.y |= (uint32_t)(cq - med3_i32(n1, -cq, cq)) << sh;
-                    c.z |= (uint32_t)(cq - med3_i32(n2, -cq, cq)) << sh;
-                    c.w |= (uint32_t)(cq - med3_i32(n3, -cq, cq)) << sh;
+                    c.x += (uint32_t)n0 << sh;
+                    c.y += (uint32_t)n1 << sh;
+                    c.z += (uint32_t)n2 << sh;
+                    c.w += (uint32_t)n3 << sh;
                 }
             }
         }
@@ -334,12 +367,12 @@ __device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t
                 m.z = x2 <= lv.maxv ? (uint32_t)l : m.z;
                 m.w = x3 <= lv.maxv ? (uint32_t)l : m.w;
             }
-            if constexpr (CACHE) {
+            if constexpr (CACHE) {  // the same sum of -q (every level clamped here: exact for the fields)
                 const uint32_t sh = (uint32_t)l * cb;
-                c.x |= lane_of_q(sgn_of(v.x) * x0, cq) << sh;
-                c.y |= lane_of_q(sgn_of(v.y) * x1, cq) << sh;
-                c.z |= lane_of_q(sgn_of(v.z) * x2, cq) << sh;
-                c.w |= lane_of_q(sgn_of(v.w) * x3, cq) << sh;
+                c.x += (uint32_t)(cq - (int32_t)lane_of_q(sgn_of(v.x) * x0, cq)) << sh;
+                c.y += (uint32_t)(cq - (int32_t)lane_of_q(sgn_of(v.y) * x1, cq)) << sh;
+                c.z += (uint32_t)(cq - (int32_t)lane_of_q(sgn_of(v.z) * x2, cq)) << sh;
+                c.w += (uint32_t)(cq - (int32_t)lane_of_q(sgn_of(v.w) * x3, cq)) << sh;
             }
         }
 #pragma unroll
@@ -356,7 +389,7 @@ __device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t
         }
     }
     if constexpr (CACHE)
-        *cv = c;
+        *cv = c;  // sum_l -q_l << (l cb): the caller's ms_cells turns it into the cells
 }
 
 // OR the per-element bits of mask_plane into the field accumulators
@@ -427,11 +460,11 @@ __device__ __forceinline__ uint4 select_plane(const float *__restrict__ x, uint3
 {
     const float4 v = load4_nt_tail<0>(x, i0, n);
     const uint4 m = mask_levels4_fast<NL>(mk, fd, i0);
-    RangeI rg;
+    RangeM rg;
     rg.add4(v);
     const uint4 r = draws_at<KIND, NL, VAR>(rng, i0, m);  // the selected level's draw, either path
     uint4 ln;
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, dv.norm)))) {
         const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
         const gc_f2 S01 = {pick_level<NL>(fa.S24, m.x), pick_level<NL>(fa.S24, m.y)};
         const gc_f2 S23 = {pick_level<NL>(fa.S24, m.z), pick_level<NL>(fa.S24, m.w)};
@@ -537,6 +570,10 @@ __global__ __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict
     constexpr int PW = (LM + 3) / 4;  // planes per wave
     __shared__ uint4 part[3][kMsQuadsPerBlock];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    uint32_t Cf = 0;  // the cells' offsets: sum_l cq << (l cb)
+    if constexpr (CBY != 0)
+        for (int l = 0; l < NL; ++l)
+            Cf += (uint32_t)cq << ((uint32_t)l * cb);
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
         const uint32_t t = tb + lane;
         uint4 acc[NL - 1] = {};
@@ -552,7 +589,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict
                 if constexpr (CBY != 0) {
                     uint4 cv, mb[NL - 1];
                     mask_plane<KIND, NL, VAR, true>(x, n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (p * w), mb, cq, cb, &cv);
-                    cache_store<CBY>(cache, i0, n, cv);
+                    cache_store<CBY>(cache, i0, n, make_uint4(Cf - cv.x, Cf - cv.y, Cf - cv.z, Cf - cv.w));
                     mask_or<NL>(acc, mb);
                 } else {
                     uint4 mb[NL - 1];
@@ -852,27 +889,6 @@ __device__ __forceinline__ void fused_accumulate(uint32_t n, uint32_t i0, uint32
     acc.z += (uint32_t)nq.z << sh;
     acc.w += (uint32_t)nq.w << sh;
 }
-
-// the fast path's range check with fewer instructions than RangeI: the low
-// bound on 2 bits(x) - 2 (one v_lshl_add per element; +-0 wrap high), the high
-// bound on max |x| as a float (v_max3_f32 with |.| modifiers, no shift).  A NaN
-// x is ignored by the float max, so it may take the fast path; both paths give
-// it the same bits (T = cvt_flr(NaN) + r = r >= 0 qualifies the top level with
-// xi = 0, as the generic rounding's med3(NaN) = 0 does).
-struct RangeM {
-    uint32_t mn = 0xffffffffu;
-    float mx = 0.0f;
-    __device__ __forceinline__ void add4(const float4 &v)
-    {
-        const uint32_t a = 2u * __float_as_uint(v.x) - 2u, b = 2u * __float_as_uint(v.y) - 2u;
-        const uint32_t c = 2u * __float_as_uint(v.z) - 2u, e = 2u * __float_as_uint(v.w) - 2u;
-        mn = min(mn, min(min(a, b), min(c, e)));
-        float m;
-        asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(m) : "v"(v.x), "v"(v.y), "v"(v.z));
-        asm("v_max3_f32 %0, |%1|, %2, %3" : "=v"(mx) : "v"(v.w), "v"(m), "v"(mx));
-    }
-    __device__ __forceinline__ bool slow(uint32_t lo2, float norm) const { return (mn < lo2) | (mx > norm); }
-};
 
 template <int KIND, int NL, int VAR>
 __device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
