@@ -261,26 +261,6 @@ __device__ __forceinline__ uint4 cache_cells(const uint2 &u)
         return make_uint4(u.x & 0xffffu, u.x >> 16, u.y & 0xffffu, u.y >> 16);
 }
 
-// the fast path's range check with fewer instructions than RangeI: the low
-// bound on 2 bits(x) - 2 (one v_lshl_add per element; +-0 wrap high), the high
-// bound on max |x| as a float (v_max3_f32 with |.| modifiers, no shift).  A NaN
-// x is ignored by the float max, so it may take the fast path; both paths give
-// it the same bits (T = cvt_flr(NaN) + r = r >= 0 qualifies the top level with
-// xi = 0, as the generic rounding's med3(NaN) = 0 does).
-struct RangeM {
-    uint32_t mn = 0xffffffffu;
-    float mx = 0.0f;
-    __device__ __forceinline__ void add4(const float4 &v)
-    {
-        const uint32_t a = 2u * __float_as_uint(v.x) - 2u, b = 2u * __float_as_uint(v.y) - 2u;
-        const uint32_t c = 2u * __float_as_uint(v.z) - 2u, e = 2u * __float_as_uint(v.w) - 2u;
-        mn = min(mn, min(min(a, b), min(c, e)));
-        float m;
-        asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(m) : "v"(v.x), "v"(v.y), "v"(v.z));
-        asm("v_max3_f32 %0, |%1|, %2, %3" : "=v"(mx) : "v"(v.w), "v"(m), "v"(mx));
-    }
-    __device__ __forceinline__ bool slow(uint32_t lo2, float norm) const { return (mn < lo2) | (mx > norm); }
-};
 
 // ---------------------------------------------------------------------------
 // per-plane work (4 elements i0..i0+3 of one plane)
@@ -299,10 +279,10 @@ __device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t
                                            uint32_t cb = 0, uint4 *cv = nullptr)
 {
     const float4 v = load4_nt_tail<0>(x, i0, n);
-    RangeM rg;
+    RangeI rg;
     rg.add4(v);
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, dv.norm)))) {
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
         const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
         // cache lanes: -q = (T >> 24) * sign (0 for +-0, whose T is >= 0)
         int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
@@ -460,11 +440,11 @@ __device__ __forceinline__ uint4 select_plane(const float *__restrict__ x, uint3
 {
     const float4 v = load4_nt_tail<0>(x, i0, n);
     const uint4 m = mask_levels4_fast<NL>(mk, fd, i0);
-    RangeM rg;
+    RangeI rg;
     rg.add4(v);
     const uint4 r = draws_at<KIND, NL, VAR>(rng, i0, m);  // the selected level's draw, either path
     uint4 ln;
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, dv.norm)))) {
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
         const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
         const gc_f2 S01 = {pick_level<NL>(fa.S24, m.x), pick_level<NL>(fa.S24, m.y)};
         const gc_f2 S23 = {pick_level<NL>(fa.S24, m.z), pick_level<NL>(fa.S24, m.w)};
@@ -828,7 +808,8 @@ __device__ __forceinline__ void fused_quad_fast(const float4 &v, uint32_t i0, co
 // Markstein range, MSV_WIDE): the same bits and -q from the per-element rounding
 template <int KIND, int NL, int VAR = 0>
 __device__ __forceinline__ void fused_quad_slow(const float4 &v, uint32_t i0, const DivNorm &dv, const LevelsArg &lv,
-                                                const RngArgs &rng, uint32_t bitP, uint4 (&mb)[NL - 1], int4 &nq)
+                                                const RngArgs &rng, uint32_t bitP, uint4 (&mb)[NL - 1], int4 &nq,
+                                                int32_t qmax)
 {
     const float4 ql = quot4_exact(v, dv);
     uint4 m = make_uint4(0u, 0u, 0u, 0u);
@@ -856,7 +837,11 @@ __device__ __forceinline__ void fused_quad_slow(const float4 &v, uint32_t i0, co
     for (int f = 0; f < NL - 1; ++f)
         mb[f] = make_uint4(m.x > (uint32_t)f ? bitP : 0u, m.y > (uint32_t)f ? bitP : 0u,
                            m.z > (uint32_t)f ? bitP : 0u, m.w > (uint32_t)f ? bitP : 0u);
-    nq = make_int4(-q.x, -q.y, -q.z, -q.w);
+    // |x| > norm (a caller's norm below max |x|, or inf) saturates at +-qmax
+    // like the two-pass select's lane_of_q; an unclamped q would carry into
+    // the word's other lanes
+    nq = make_int4(-med3_i32(q.x, -qmax, qmax), -med3_i32(q.y, -qmax, qmax), -med3_i32(q.z, -qmax, qmax),
+                   -med3_i32(q.w, -qmax, qmax));
 }
 
 constexpr uint32_t kMsFusedMaxR = 8;  // q words per mask word at W = 1: 32 / (q lanes per word) <= 8
@@ -894,16 +879,16 @@ template <int KIND, int NL, int VAR>
 __device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
                                               uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
                                               const RngArgs &rng, uint32_t bitP, uint32_t sh,
-                                              uint4 (&macc)[NL - 1], uint4 &acc)
+                                              uint4 (&macc)[NL - 1], uint4 &acc, int32_t qmax)
 {
-    RangeM rg;
+    RangeI rg;
     rg.add4(v);
     uint4 mb[NL - 1];
     int4 nq;
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, dv.norm))))
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2))))
         fused_quad_fast<KIND, NL, VAR>(v, i0, dv, fa, rng, bitP, mb, nq);
     else
-        fused_quad_slow<KIND, NL, VAR>(v, i0, dv, lv, rng, bitP, mb, nq);
+        fused_quad_slow<KIND, NL, VAR>(v, i0, dv, lv, rng, bitP, mb, nq, qmax);
     fused_accumulate<NL>(n, i0, sh, mb, nq, macc, acc);
 }
 
@@ -917,27 +902,24 @@ template <int KIND, int NL, int VAR = 0>
 __global__ __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *__restrict__ x, uint32_t n,
                                                                  const float *__restrict__ normp, LevelsArg lv,
                                                                  MsFastArg fa, RngArgs rng, uint32_t Mm, uint32_t r,
-                                                                 uint32_t Lq, uint32_t wq, int32_t qmax,
-                                                                 uint32_t *__restrict__ mask_words,
+                                                                 uint32_t Lq, uint32_t wq, int32_t qmax, uint32_t Cw,
+                                                                 uint32_t pend, uint32_t *__restrict__ mask_words,
                                                                  uint32_t *__restrict__ words)
 {
+    // host-computed: Cw = sum_k qmax << (k wq) (the lane offsets of a full
+    // word), pend = ceil(n / Mm) (mask planes holding any element).  A block
+    // walks several tiles (grid-stride), so this prologue is paid per block
     const float norm = *normp;
     const DivNorm dv = make_div(norm);
     const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
     const uint32_t quads = Mm >> 2;
     const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    uint32_t Cw = 0;
-    for (uint32_t k = 0; k < Lq; ++k)
-        Cw += (uint32_t)qmax << (k * wq);
-    // the last plane of this wave holding any element (uniform): P = h + r k < ceil(n / Mm)
-    const uint32_t pend = (uint32_t)(((uint64_t)n + Mm - 1) / Mm);
-    const uint32_t kend = pend > h ? min(Lq, (pend - h + r - 1) / r) : 0u;
     __shared__ uint4 part[kMsFusedMaxR - 1][NL - 1][kMsQuadsPerBlock];
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
         const uint32_t t = tb + lane;
         uint4 macc[NL - 1] = {};
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
-        if (t < quads && kend > 0) {
+        if (t < quads) {
             uint32_t i0 = h * Mm + 4u * t;
             const uint32_t step = r * Mm;
             // planes below pend - 1 are full for every lane (their end (P + 1) Mm
@@ -948,9 +930,9 @@ __global__ __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *
             // one plane at a time (a next-plane register prefetch measured the
             // same: the waves of the CU hide the load latency)
 #pragma unroll 1
-            for (uint32_t k = 0; k < kend; ++k) {
+            for (uint32_t k = 0; k < Lq && h + r * k < pend; ++k) {  // planes past pend hold no element
                 fused_plane_r<KIND, NL, VAR>(load(k, i0), n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (h + r * k), k * wq,
-                                             macc, acc);
+                                             macc, acc, qmax);
                 i0 += step;
             }
         }

@@ -13,6 +13,9 @@
 // kernel wrote as one 1-2 byte cell per element (every level's lane value):
 // 43 + 15 us instead of 24 + 36 us at 23.5M floats, the same total: both
 // kernels are bound by the Philox draws (profiles/r01s_lab_ms.log); opt-in.
+#include <algorithm>
+#include <cstdlib>
+
 #include "gc_device.h"
 #include "gc_host.h"
 #include "segments.h"
@@ -332,6 +335,20 @@ static unsigned ms_grid(uint64_t quads)
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, 65535));
 }
 
+// tiles (64 word quads) per block of the Philox-bound wave-split kernels (the
+// one-pass encode, the mask encode with or without the q cache, the select):
+// their prologue (the norm's reciprocal and range bounds, 60-75 VALU per wave)
+// is paid once per block.  GC_MS_FUSED_TILES overrides it (measurement only)
+static uint64_t ms_tiles()
+{
+    static const uint64_t t = [] {
+        const char *e = getenv("GC_MS_FUSED_TILES");
+        const long v = e ? atol(e) : 0;
+        return (uint64_t)(v >= 1 && v <= 64 ? v : 2);
+    }();
+    return t;
+}
+
 // q cache geometry (ms_fast.h): cell bytes per element (0 = not supported:
 // outside the dense wave-split kernels, or the count fields of cb bits exceed
 // 16 bits).  Levels of 8-24 bits (MSV_WIDE) cache too: the cell holds the
@@ -404,12 +421,16 @@ int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_leve
     const RngArgs ra = rng_args_ms(rng, n);
     const MsFastArg fa = ms_fast_arg(levels);
     const uint32_t Mm = (uint32_t)mask_lanes->plane_words;
-    const unsigned g = ms_grid(Mm >> 2);
+    const unsigned g = (unsigned)std::max<uint64_t>(1, (ms_grid(Mm >> 2) + ms_tiles() - 1) / ms_tiles());
     const bool wide = !ms_fast_ok(mode, n, levels);
     const int32_t qmax = (int32_t)q_lanes->offset;
+    uint32_t Cw = 0;
+    for (uint32_t k = 0; k < q_lanes->per_word; ++k)
+        Cw += (uint32_t)qmax << (k * q_lanes->bits);
+    const uint32_t pend = (uint32_t)((n + Mm - 1) / Mm);
 #define GC_FW(KIND_, NL_, VAR_)                                                                                   \
     hipLaunchKernelGGL((k_ms_fused_w1<KIND_, NL_, VAR_>), dim3(g), dim3(64 * r), 0, st, x, (uint32_t)n, norm, la, \
-                       fa, ra, Mm, r, q_lanes->per_word, q_lanes->bits, qmax, mask_words, words)
+                       fa, ra, Mm, r, q_lanes->per_word, q_lanes->bits, qmax, Cw, pend, mask_words, words)
     if (levels->count == 2) {
         if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 2, MSV_WIDE); } else { GC_FW(0, 2, 0); } }
         else { if (wide) { GC_FW(1, 2, MSV_WIDE); } else { GC_FW(1, 2, 0); } }
@@ -445,7 +466,7 @@ int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const floa
                                                             fields, mask_words))
     if (ms_fast_wide_ok(mode, n, levels)) {
         const MsFastArg fa = ms_fast_arg(levels);
-        const unsigned g = ms_grid(M >> 2);
+        const unsigned g = (unsigned)std::max<uint64_t>(1, (ms_grid(M >> 2) + ms_tiles() - 1) / ms_tiles());
         const bool wide = !ms_fast_ok(mode, n, levels);
 #define GC_MF(KIND_, NL_)                                                                                         \
     if (wide)                                                                                                     \
@@ -501,7 +522,7 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
     if (ms_fast_wide_ok(mode, n, levels) && mask_lanes->plane_words >= 2 && mask_lanes->plane_words < (1ull << 32)) {
         const MsFastArg fa = ms_fast_arg(levels);
         const FastDiv fd = make_fastdiv((uint32_t)mask_lanes->plane_words);
-        const unsigned g = ms_grid(Mq >> 2);
+        const unsigned g = (unsigned)std::max<uint64_t>(1, (ms_grid(Mq >> 2) + ms_tiles() - 1) / ms_tiles());
         const bool wide = !ms_fast_ok(mode, n, levels);
 #define GC_SF(KIND_, NL_)                                                                                             \
     if (wide)                                                                                                         \
@@ -558,7 +579,7 @@ int gc_ms_mask_encode_cached(const float *x, uint64_t n, const float *norm, cons
     const RngArgs ra = rng_args_ms(rng, n);
     const MsFastArg fa = ms_fast_arg(levels);
     const uint32_t M = (uint32_t)mask_lanes->plane_words, w = mask_lanes->bits, fields = levels->count - 1;
-    const unsigned g = ms_grid(M >> 2);
+    const unsigned g = (unsigned)std::max<uint64_t>(1, (ms_grid(M >> 2) + ms_tiles() - 1) / ms_tiles());
     const bool wide = !ms_fast_ok(0, n, levels);
 #define GC_MFC(KIND_, NL_, VAR_, CBY_)                                                                                \
     GC_DISPATCH_L2(mask_lanes->per_word,                                                                             \
@@ -599,7 +620,7 @@ int gc_ms_select_cached(const void *cache, uint64_t n, const gc_levels *levels, 
     const MaskArg mk = mask_arg(mask_words, mask_lanes, levels->count);
     const FastDiv fd = make_fastdiv((uint32_t)mask_lanes->plane_words);
     const uint32_t Mq = (uint32_t)q_lanes->plane_words;
-    const unsigned g = ms_grid(Mq >> 2);
+    const unsigned g = (unsigned)std::max<uint64_t>(1, (ms_grid(Mq >> 2) + ms_tiles() - 1) / ms_tiles());
 #define GC_SC(NL_, CBY_)                                                                                            \
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_cache<LL, NL_, CBY_>), dim3(g), dim3(kBlock), 0, \
                                                          st, cache, (uint32_t)n, mk, fd, Mq, q_lanes->bits, cg.cb,    \

@@ -970,6 +970,12 @@ def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int) -> _MtRun:
         hout[slot].copy_(st_dev, non_blocking=True)
         run.state_ready = torch.cuda.Event()
         run.state_ready.record()
+    # the jump table and the end coefficients live on the caller's stream and
+    # may be replaced (table growth, cache eviction) while these runs are queued
+    for t in (table, end):
+        if t is not None:
+            t.record_stream(js)
+            t.record_stream(gs)
     with torch.cuda.stream(gs):
         gs.wait_event(run.p1)
         run.out = torch.empty(count, dtype=torch.int32, device=dev)

@@ -346,10 +346,14 @@ int main(int argc, char **argv)
     CK(hipMalloc(&mw3, (size_t)Mm * 4 + 64));
     CK(hipMalloc(&wq3, (size_t)Mq * 4 + 64));
     auto p_w1 = [&] { GK(gc_ms_encode_w1(x, n, norm, &lv, &rng, &ml, &ql, mw2, wq2, nullptr)); };
+    uint32_t Cw3 = 0;
+    for (uint32_t k = 0; k < ql.per_word; ++k)
+        Cw3 += (uint32_t)qmax << (k * ql.bits);
+    const uint32_t pend3 = (uint32_t)((n + Mm - 1) / Mm);
     auto v_w1 = [&](auto kern) {
         return [=] {
-            hipLaunchKernelGGL(kern, dim3((Mm / 4 + 63) / 64), dim3(64 * rr), 0, 0, x, n32, norm, la, fa, ra, Mm, rr,
-                               ql.per_word, ql.bits, qmax, mw3, wq3);
+            hipLaunchKernelGGL(kern, dim3((Mm / 4 + 127) / 128), dim3(64 * rr), 0, 0, x, n32, norm, la, fa, ra, Mm, rr,
+                               ql.per_word, ql.bits, qmax, Cw3, pend3, mw3, wq3);
         };
     };
     p_w1();
