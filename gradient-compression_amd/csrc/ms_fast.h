@@ -517,8 +517,16 @@ constexpr uint32_t kMsQuadsPerBlock = 64;  // word quads per block (one per lane
 // mask encode: thermometer fields of the resolution level (compressors.py:799-807)
 // ---------------------------------------------------------------------------
 // CBY = 0: mask only; 1 / 2: also the q cache cells (CBY bytes per element)
+// GC_MS_WPE (measurement builds only, tools/Makefile lab_ms_w8): pin the
+// Philox-bound kernels' occupancy with amdgpu_waves_per_eu
+#ifdef GC_MS_WPE
+#define GC_MS_OCC __attribute__((amdgpu_waves_per_eu(GC_MS_WPE, GC_MS_WPE)))
+#else
+#define GC_MS_OCC
+#endif
+
 template <int LM, int KIND, int NL, int VAR = 0, int CBY = 0>
-__global__ __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict__ x, uint32_t n,
+__global__ GC_MS_OCC __launch_bounds__(kBlock) void k_ms_mask_fast(const float *__restrict__ x, uint32_t n,
                                                          const float *__restrict__ normp, LevelsArg lv, MsFastArg fa,
                                                          RngArgs rng, uint32_t M, uint32_t w, uint32_t fields,
                                                          uint32_t *__restrict__ mask_words, void *__restrict__ cache = nullptr,
@@ -899,7 +907,7 @@ __device__ __forceinline__ float4 load4_guard(const float *__restrict__ x, uint3
 
 // blockDim = 64 r (r <= kMsFusedMaxR waves); wave h walks planes h + r k, k < Lq.
 template <int KIND, int NL, int VAR = 0>
-__global__ __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *__restrict__ x, uint32_t n,
+__global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *__restrict__ x, uint32_t n,
                                                                  const float *__restrict__ normp, LevelsArg lv,
                                                                  MsFastArg fa, RngArgs rng, uint32_t Mm, uint32_t r,
                                                                  uint32_t Lq, uint32_t wq, int32_t qmax, uint32_t Cw,

@@ -335,16 +335,19 @@ static unsigned ms_grid(uint64_t quads)
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, 65535));
 }
 
-// tiles (64 word quads) per block of the Philox-bound wave-split kernels (the
-// one-pass encode, the mask encode with or without the q cache, the select):
-// their prologue (the norm's reciprocal and range bounds, 60-75 VALU per wave)
-// is paid once per block.  GC_MS_FUSED_TILES overrides it (measurement only)
+// tiles (64 word quads) per block of the wave-split kernels.  One: two or more
+// amortise the prologue (the norm's reciprocal and range bounds, 60-75 VALU
+// per wave; 43.2 -> 40.5 VALU per element for the one-pass encode at two) but
+// halve the waves in flight, and the kernels are slower (one-pass 35.1 /
+// 38.7 / 42.6 / 54.6 us at 1 / 2 / 3 / 4 tiles, mask + cache 35.7 / 38.5 /
+// 41.5 / 46.4 us; profiles/r03k_lab_ms_t*.log).  GC_MS_FUSED_TILES overrides
+// it (measurement only)
 static uint64_t ms_tiles()
 {
     static const uint64_t t = [] {
         const char *e = getenv("GC_MS_FUSED_TILES");
         const long v = e ? atol(e) : 0;
-        return (uint64_t)(v >= 1 && v <= 64 ? v : 2);
+        return (uint64_t)(v >= 1 && v <= 64 ? v : 1);
     }();
     return t;
 }

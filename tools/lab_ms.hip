@@ -332,6 +332,7 @@ int main(int argc, char **argv)
         };
     };
     vs.push_back({"product mask encode + cache", p_maskc, xb + mb + cbytes, {}});
+    vs.push_back({"lab mask + cache (product math)", v_maskc(k_ms_mask_fast<32, 0, 2, 0, 1>), xb + mb + cbytes, {}});
     vs.push_back({"lab mask + cache NORNG", v_maskc(k_ms_mask_fast<32, 0, 2, MSV_NORNG, 1>), xb + mb + cbytes, {}});
     vs.push_back({"lab mask + cache NORNG|NOSLOW", v_maskc(k_ms_mask_fast<32, 0, 2, MSV_NORNG | MSV_NOSLOW, 1>),
                   xb + mb + cbytes, {}});
@@ -352,7 +353,7 @@ int main(int argc, char **argv)
     const uint32_t pend3 = (uint32_t)((n + Mm - 1) / Mm);
     auto v_w1 = [&](auto kern) {
         return [=] {
-            hipLaunchKernelGGL(kern, dim3((Mm / 4 + 127) / 128), dim3(64 * rr), 0, 0, x, n32, norm, la, fa, ra, Mm, rr,
+            hipLaunchKernelGGL(kern, dim3((Mm / 4 + 63) / 64), dim3(64 * rr), 0, 0, x, n32, norm, la, fa, ra, Mm, rr,
                                ql.per_word, ql.bits, qmax, Cw3, pend3, mw3, wq3);
         };
     };
@@ -360,7 +361,11 @@ int main(int argc, char **argv)
     cmp("one-pass mask == two-pass", mw, mw2, (size_t)Mm * 4);
     cmp("one-pass words == two-pass", wq, wq2, (size_t)Mq * 4);
     v_w1(k_ms_fused_w1<0, 2, MSV_NORNG>)();  // (lab variant: a different stream, run for the timing only)
+    v_w1(k_ms_fused_w1<0, 2, 0>)();  // the product's math compiled into the lab (GC_MS_WPE builds)
+    cmp("lab one-pass (product math) mask", mw3, mw2, (size_t)Mm * 4);
+    cmp("lab one-pass (product math) words", wq3, wq2, (size_t)Mq * 4);
     vs.push_back({"product one-pass W=1 (mask + select)", p_w1, xb + mb + qb, {}});
+    vs.push_back({"lab one-pass (product math)", v_w1(k_ms_fused_w1<0, 2, 0>), xb + mb + qb, {}});
     vs.push_back({"lab one-pass NORNG", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG>), xb + mb + qb, {}});
     vs.push_back({"lab one-pass NORNG|NOSLOW", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG | MSV_NOSLOW>), xb + mb + qb, {}});
     vs.push_back({"product decode order 0", p_dec(0), xb + mb + qb, {}});
