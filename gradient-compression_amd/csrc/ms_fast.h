@@ -56,8 +56,11 @@ inline FastDiv make_fastdiv(uint32_t d)
     return f;
 }
 
-// kernel variants: the product uses VAR = 0 (levels <= 7 bits) or MSV_WIDE;
-// the others are lab variants (tools/lab_ms.hip)
+// kernel variants: the product uses VAR = 0 (levels <= 7 bits) or MSV_WIDE,
+// and MSV_EAGER0 for the one-pass encode with Philox draws (33.5 against
+// 34.9 us on the ResNet50 bucket, profiles/r03l_lab_ms.log: the two Philox
+// chains interleave, and the level-0 block is needed by nearly every wave
+// anyway); the others are lab variants (tools/lab_ms.hip)
 enum : int {
     MSV_PERTHREAD = 1,  // one thread walks all planes of its word quad (no wave split)
     MSV_NORNG = 2,      // measurement only: draws = a hash of the element index (no Philox)
@@ -65,6 +68,8 @@ enum : int {
     MSV_WIDE = 8,       // a lowest level of 8-24 bits: the wave-split kernels with the generic
                         // per-element rounding (quot4_exact + xi_from_q) on every quad
     MSV_DEFER = 16,     // lab: the one-pass kernel with the generic path deferred to after the plane loop
+    MSV_EAGER0 = 32,    // the one-pass fast path computes level 0's draws for every quad, interleaved
+                        // with the upper levels' (no wave-level branch; same draws and outputs)
 };
 
 template <int KIND, int VAR>
@@ -772,6 +777,9 @@ __device__ __forceinline__ void fused_quad_fast(const float4 &v, uint32_t i0, co
                                                 const RngArgs &rng, uint32_t bitP, uint4 (&mb)[NL - 1], int4 &nq)
 {
     const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+    uint4 r0e;
+    if constexpr ((VAR & MSV_EAGER0) != 0)
+        r0e = ms_draws4<KIND, VAR>(rng, 0, i0);  // independent of the upper levels': the chains interleave
     int4 T;
     bool k0 = false, k1 = false, k2 = false, k3 = false;  // some level >= 1 qualifies
 #pragma unroll
@@ -796,8 +804,12 @@ __device__ __forceinline__ void fused_quad_fast(const float4 &v, uint32_t i0, co
         // field f = l - 1: [m >= l] = some level >= l qualifies
         mb[l - 1] = make_uint4(k0 ? bitP : 0u, k1 ? bitP : 0u, k2 ? bitP : 0u, k3 ? bitP : 0u);
     }
-    if (!(k0 && k1 && k2 && k3)) {  // level 0's draws only when an element stays there
-        const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
+    if ((VAR & MSV_EAGER0) != 0 || !(k0 && k1 && k2 && k3)) {  // level 0's draws only when an element stays there
+        uint4 r;
+        if constexpr ((VAR & MSV_EAGER0) != 0)
+            r = r0e;
+        else
+            r = ms_draws4<KIND, VAR>(rng, 0, i0);
         const gc_f2 S = {fa.S24[0], fa.S24[0]};
         const gc_f2 a = q01 * S, b = q23 * S;
         const int32_t w0 = ms_t_v(a.x, r.x), w1 = ms_t_v(a.y, r.y), w2 = ms_t_v(b.x, r.z), w3 = ms_t_v(b.y, r.w);

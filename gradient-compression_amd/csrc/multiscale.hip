@@ -435,10 +435,10 @@ int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_leve
     hipLaunchKernelGGL((k_ms_fused_w1<KIND_, NL_, VAR_>), dim3(g), dim3(64 * r), 0, st, x, (uint32_t)n, norm, la, \
                        fa, ra, Mm, r, q_lanes->per_word, q_lanes->bits, qmax, Cw, pend, mask_words, words)
     if (levels->count == 2) {
-        if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 2, MSV_WIDE); } else { GC_FW(0, 2, 0); } }
+        if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 2, MSV_WIDE); } else { GC_FW(0, 2, MSV_EAGER0); } }
         else { if (wide) { GC_FW(1, 2, MSV_WIDE); } else { GC_FW(1, 2, 0); } }
     } else {
-        if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 3, MSV_WIDE); } else { GC_FW(0, 3, 0); } }
+        if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 3, MSV_WIDE); } else { GC_FW(0, 3, MSV_EAGER0); } }
         else { if (wide) { GC_FW(1, 3, MSV_WIDE); } else { GC_FW(1, 3, 0); } }
     }
 #undef GC_FW

@@ -151,9 +151,9 @@ __global__ __launch_bounds__(kBlock) void k_decode_scatter1(const uint32_t *__re
     const uint32_t mask = (1u << w) - 1u;
     const int32_t Q = (int32_t)((wd >> (plane * w)) & mask) - sub;
     const float d = c * (float)Q;
-    if constexpr (SEG) {
+    if constexpr (SEG) {  // the setgrad's 0 + RN(alpha * d) (reducer.py:757-761): -0 becomes +0
         const SegPos p = seg_find(sg, (uint64_t)id);
-        p.r.ptr[(uint64_t)id - p.r.start] = d * alpha;
+        p.r.ptr[(uint64_t)id - p.r.start] = d * alpha + 0.0f;
     } else {
         out[id] = d * alpha;
     }

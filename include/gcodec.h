@@ -192,7 +192,8 @@ int gc_randk_encode_w1(const float *x, const int64_t *idx, uint64_t k, float *xk
 /* the same two with x given as the per-parameter tensors (a gc_segments table,
  * below): the reducer's gather reads every index from its tensor, so no
  * flattened bucket is built for GlobalRandK (reducer.py:713-723 flattens the
- * whole gradient, then gathers K of its elements) */
+ * whole gradient, then gathers K of its elements).  Indices are not
+ * range-checked on the device: every idx[i] must be in [0, segs->n) */
 typedef struct gc_segments gc_segments;
 int gc_randk_gather_absmax_segments(const gc_segments *segs, const int64_t *idx, uint64_t k, float *xk, float *norm,
                                     void *workspace, gc_stream_t stream);
@@ -256,7 +257,9 @@ int gc_segments_scatter(const float *flat, float alpha, const gc_segments *segs,
  * (the GlobalRandK setgrad of every coordinate, reducer.py:759-761, tensor to tensor) */
 int gc_segments_copy(const gc_segments *src, const gc_segments *dst, float alpha, gc_stream_t stream);
 /* the GlobalRandK decode-scatter (gc_qsgd_decode with idx) into the tensors of segs:
- * element idx[i] = RN(decode_i * alpha) (reducer.py:754 + 759-761) */
+ * element idx[i] = RN(decode_i * alpha) (reducer.py:754 + 759-761).  Like the
+ * flat form, the indices are not range-checked on the device: every idx[i]
+ * must be in [0, segs->n) */
 int gc_qsgd_decode_scatter_segments(const uint32_t *words, const int64_t *idx, uint64_t k, const float *norm,
                                     uint32_t bits, const gc_lanes *lanes, float alpha, const gc_segments *segs,
                                     gc_stream_t stream);

@@ -366,6 +366,10 @@ int main(int argc, char **argv)
     cmp("lab one-pass (product math) words", wq3, wq2, (size_t)Mq * 4);
     vs.push_back({"product one-pass W=1 (mask + select)", p_w1, xb + mb + qb, {}});
     vs.push_back({"lab one-pass (product math)", v_w1(k_ms_fused_w1<0, 2, 0>), xb + mb + qb, {}});
+    v_w1(k_ms_fused_w1<0, 2, MSV_EAGER0>)();
+    cmp("lab one-pass EAGER0 mask", mw3, mw2, (size_t)Mm * 4);
+    cmp("lab one-pass EAGER0 words", wq3, wq2, (size_t)Mq * 4);
+    vs.push_back({"lab one-pass EAGER0", v_w1(k_ms_fused_w1<0, 2, MSV_EAGER0>), xb + mb + qb, {}});
     vs.push_back({"lab one-pass NORNG", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG>), xb + mb + qb, {}});
     vs.push_back({"lab one-pass NORNG|NOSLOW", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG | MSV_NOSLOW>), xb + mb + qb, {}});
     vs.push_back({"product decode order 0", p_dec(0), xb + mb + qb, {}});
