@@ -134,6 +134,28 @@ __device__ __forceinline__ gc_f2 quot2_signed(float a, float b, const DivNorm &d
     return __builtin_elementwise_fma(e, y, q0);
 }
 
+// the fast path's range check, split: the low bound (tiny |x|, where the
+// Markstein quotient may be inexact) on the bits, 2 bits(x) - 2 (one
+// v_lshl_add per element; +-0 wrap high and pass); the high bound on the
+// quotient itself: |q| <= 1 for all four (false for NaN, +-inf and |x| > norm
+// alike; where |x| <= norm the quotient is exact, so |q| <= 1 exactly then).
+// 11 instructions per quad against RangeI's 14.
+struct RangeLo {
+    uint32_t mn = 0xffffffffu;
+    __device__ __forceinline__ void add4(const float4 &v)
+    {
+        const uint32_t a = 2u * __float_as_uint(v.x) - 2u, b = 2u * __float_as_uint(v.y) - 2u;
+        const uint32_t c = 2u * __float_as_uint(v.z) - 2u, e = 2u * __float_as_uint(v.w) - 2u;
+        mn = min(mn, min(min(a, b), min(c, e)));
+    }
+    __device__ __forceinline__ bool tiny(uint32_t lo2) const { return mn < lo2; }
+};
+
+__device__ __forceinline__ bool q_in_unit(const gc_f2 &a, const gc_f2 &b)
+{
+    return (fabsf(a.x) <= 1.0f) & (fabsf(a.y) <= 1.0f) & (fabsf(b.x) <= 1.0f) & (fabsf(b.y) <= 1.0f);
+}
+
 // mask levels of 4 fast-path elements: last level l whose xi_l <= maxv
 template <int KIND, int NL, int VAR = 0>
 __device__ __forceinline__ uint4 ms_levels4_int(const float4 &v, const DivNorm &dv, const LevelsArg &lv,
@@ -284,11 +306,11 @@ __device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t
                                            uint32_t cb = 0, uint4 *cv = nullptr)
 {
     const float4 v = load4_nt_tail<0>(x, i0, n);
-    RangeI rg;
+    RangeLo rg;
     rg.add4(v);
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
-        const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+    const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.tiny(lo2) && q_in_unit(q01, q23)))) {
         // cache lanes: -q = (T >> 24) * sign (0 for +-0, whose T is >= 0)
         int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
         if constexpr (CACHE) {
@@ -445,12 +467,12 @@ __device__ __forceinline__ uint4 select_plane(const float *__restrict__ x, uint3
 {
     const float4 v = load4_nt_tail<0>(x, i0, n);
     const uint4 m = mask_levels4_fast<NL>(mk, fd, i0);
-    RangeI rg;
+    RangeLo rg;
     rg.add4(v);
     const uint4 r = draws_at<KIND, NL, VAR>(rng, i0, m);  // the selected level's draw, either path
     uint4 ln;
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2)))) {
-        const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+    const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.tiny(lo2) && q_in_unit(q01, q23)))) {
         const gc_f2 S01 = {pick_level<NL>(fa.S24, m.x), pick_level<NL>(fa.S24, m.y)};
         const gc_f2 S23 = {pick_level<NL>(fa.S24, m.z), pick_level<NL>(fa.S24, m.w)};
         const gc_f2 a = q01 * S01, b = q23 * S23;
@@ -773,10 +795,10 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
 // T >> 24 is a sign-extended byte.  -q = (T >> 24) * sign(x) (0 for +-0,
 // whose T is >= 0 anyway).
 template <int KIND, int NL, int VAR = 0>
-__device__ __forceinline__ void fused_quad_fast(const float4 &v, uint32_t i0, const DivNorm &dv, const MsFastArg &fa,
-                                                const RngArgs &rng, uint32_t bitP, uint4 (&mb)[NL - 1], int4 &nq)
+__device__ __forceinline__ void fused_quad_fast(const float4 &v, const gc_f2 &q01, const gc_f2 &q23, uint32_t i0,
+                                                const MsFastArg &fa, const RngArgs &rng, uint32_t bitP,
+                                                uint4 (&mb)[NL - 1], int4 &nq)
 {
-    const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
     uint4 r0e;
     if constexpr ((VAR & MSV_EAGER0) != 0)
         r0e = ms_draws4<KIND, VAR>(rng, 0, i0);  // independent of the upper levels': the chains interleave
@@ -901,12 +923,13 @@ __device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint3
                                               const RngArgs &rng, uint32_t bitP, uint32_t sh,
                                               uint4 (&macc)[NL - 1], uint4 &acc, int32_t qmax)
 {
-    RangeI rg;
+    RangeLo rg;
     rg.add4(v);
     uint4 mb[NL - 1];
     int4 nq;
-    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.slow(lo2, hi2))))
-        fused_quad_fast<KIND, NL, VAR>(v, i0, dv, fa, rng, bitP, mb, nq);
+    const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
+    if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.tiny(lo2) && q_in_unit(q01, q23))))
+        fused_quad_fast<KIND, NL, VAR>(v, q01, q23, i0, fa, rng, bitP, mb, nq);
     else
         fused_quad_slow<KIND, NL, VAR>(v, i0, dv, lv, rng, bitP, mb, nq, qmax);
     fused_accumulate<NL>(n, i0, sh, mb, nq, macc, acc);

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode(const uint32_t *__restrict
 #pragma unroll
         for (int k0 = 0; k0 < LQ; k0 += C) {
           int64_t id[C][4];
-          if constexpr (MODE == 2)  // GRandK scatter: the chunk's index loads together
+          if constexpr (MODE == 2 || MODE == 4)  // GRandK scatter: the chunk's index loads together
               gather_idx<C>(idx, n, Mq, 4 * t, k0, id);
 #pragma unroll
           for (int c = 0; c < C; ++c) {
@@ -146,6 +146,13 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode(const uint32_t *__restrict
                 o.w = ms_dq((int32_t)((wd.w >> sh) & msk) - sub, norm, sel_level(lv, m.w), order, alpha);
                 if (MODE == 3) {
                     seg_store4(sg, i0, n, o);
+                } else if (MODE == 4) {  // GRandK scatter into the tensors: the setgrad's 0 + RN(alpha d)
+                    for (int e = 0; e < 4; ++e)
+                        if (i0 + e < n) {
+                            const uint64_t id_e = (uint64_t)id[c][e];
+                            const SegPos p = seg_find(sg, id_e);
+                            p.r.ptr[id_e - p.r.start] = pickf(o, e) + 0.0f;
+                        }
                 } else if (MODE == 0 && i0 + 4 <= n) {
                     *reinterpret_cast<float4 *>(out + i0) = o;
                 } else {
@@ -651,14 +658,14 @@ static int ms_decode(const char *what, const uint32_t *words, const uint32_t *ma
     GC_REQUIRE(order == 0 || order == 1, "%s: order must be 0 (multi-scale) or 1 (two-scale)", what);
     GC_REQUIRE(aligned16(words) && aligned16(mask_words), "%s: words must be 16-byte aligned", what);
     SegArg sg{};
-    if (segs && (rc = seg_arg(segs, n, &sg, what)))
+    if (segs && (rc = seg_arg(segs, idx ? segs->n : n, &sg, what)))  // with idx: n = K of the table's elements
         return rc;
     if (q_lanes->plane_words == 0)
         return GC_OK;
     hipStream_t st = as_stream(stream);
     const LevelsArg la = levels_arg(levels);
     const MaskArg mk = mask_arg(mask_words, mask_lanes, levels->count);
-    const int mode = segs ? 3 : idx ? 2 : (aligned16(out) ? 0 : 1);
+    const int mode = segs ? (idx ? 4 : 3) : idx ? 2 : (aligned16(out) ? 0 : 1);
     const unsigned grid = grid_for(q_lanes->plane_words >> 2);
     const int32_t sub = (int32_t)(q_lanes->world * q_lanes->offset);
 #define GC_MD(MODE_)                                                                                               \
@@ -679,7 +686,8 @@ static int ms_decode(const char *what, const uint32_t *words, const uint32_t *ma
             if (order == 0) { GC_DF(0, 3); } else { GC_DF(1, 3); }
         }
 #undef GC_DF
-    } else if (mode == 0) { GC_MD(0); } else if (mode == 1) { GC_MD(1); } else if (mode == 2) { GC_MD(2); } else { GC_MD(3); }
+    } else if (mode == 0) { GC_MD(0); } else if (mode == 1) { GC_MD(1); } else if (mode == 2) { GC_MD(2); }
+    else if (mode == 3) { GC_MD(3); } else { GC_MD(4); }
 #undef GC_MD
     return launch_status(what);
 }
@@ -699,6 +707,16 @@ int gc_ms_decode_segments(const uint32_t *words, const uint32_t *mask_words, uin
     GC_REQUIRE(segs, "gc_ms_decode_segments: null segments");
     return ms_decode("gc_ms_decode_segments", words, mask_words, nullptr, n, norm, levels, mask_lanes, q_lanes, order,
                      alpha, nullptr, segs, stream);
+}
+
+int gc_ms_decode_scatter_segments(const uint32_t *words, const uint32_t *mask_words, const int64_t *idx, uint64_t k,
+                                  const float *norm, const gc_levels *levels, const gc_lanes *mask_lanes,
+                                  const gc_lanes *q_lanes, int order, float alpha, const gc_segments *segs,
+                                  gc_stream_t stream)
+{
+    GC_REQUIRE(segs && (k == 0 || idx), "gc_ms_decode_scatter_segments: null segments / idx");
+    return ms_decode("gc_ms_decode_scatter_segments", words, mask_words, idx, k, norm, levels, mask_lanes, q_lanes,
+                     order, alpha, nullptr, segs, stream);
 }
 
 int gc_ms_mask_unpack(const uint32_t *mask_words, const gc_lanes *mask_lanes, uint32_t levels_count, int8_t *mask,

@@ -117,6 +117,7 @@ SIGNATURES = {
     "gc_ms_select_cached": (C.c_int, [P, u64, LEVP, P, LANESP, LANESP, P, P]),
     "gc_ms_decode": (C.c_int, [P, P, P, u64, P, LEVP, LANESP, LANESP, C.c_int, f32, P, P]),
     "gc_ms_decode_segments": (C.c_int, [P, P, u64, P, LEVP, LANESP, LANESP, C.c_int, f32, SEGSP, P]),
+    "gc_ms_decode_scatter_segments": (C.c_int, [P, P, P, u64, P, LEVP, LANESP, LANESP, C.c_int, f32, SEGSP, P]),
     "gc_ms_mask_unpack": (C.c_int, [P, LANESP, u32, P, P]),
     "gc_ms_quantize_mask": (C.c_int, [P, u64, P, LEVP, RNGP, P, P]),
     "gc_ms_select_quantize": (C.c_int, [P, u64, P, LEVP, RNGP, P, P, u32, P]),

@@ -485,6 +485,21 @@ def qsgd_decode_segments(words, norm, bits, segs: Segments, world=1, alpha=1.0, 
                                               C.byref(segs.struct), _stream(dev)), "gc_qsgd_decode_segments")
 
 
+def ms_decode_scatter_segments(words, mask_words, idx, norm, levels, segs: Segments, world=1, order=0, alpha=1.0):
+    """ms_decode(..., idx=idx) writing element idx[i] straight into its tensor,
+    RN(decode_i * alpha) + 0 (the GlobalRandK two-scale setgrad)."""
+    dev = _dev(words)
+    idx = _idx(idx, dev)
+    k = idx.numel()
+    ql, ml = ms_layouts(k, levels, world)
+    lv = levels_struct(levels)
+    nt = norm_tensor(norm, dev)
+    check(_lib.load().gc_ms_decode_scatter_segments(_p(words), _p(mask_words), _p(idx), k, _p(nt), C.byref(lv),
+                                                    C.byref(ml), C.byref(ql), int(order), float(alpha),
+                                                    C.byref(segs.struct), _stream(dev)),
+          "gc_ms_decode_scatter_segments")
+
+
 def ms_decode_segments(words, mask_words, norm, levels, segs: Segments, world=1, order=0, alpha=1.0):
     dev = _dev(words)
     ql, ml = ms_layouts(segs.n, levels, world)

@@ -256,6 +256,11 @@ class QSGDMaxNormTwoScaleCompressor(_MultiScalePacked):
 class GlobalRandKMaxNormTwoScaleCompressor(QSGDMaxNormTwoScaleCompressor):
     """compressors.py:683-751 — identical arithmetic on the K-subset."""
 
+    def decode_scatter_segments(self, norm, words, mask_words, idx, segs, world=1, alpha=1.0):
+        """decode(..., idx=idx) writing element idx[i] straight into its tensor."""
+        return self.backend.ms_decode_scatter_segments(words, mask_words, idx, norm, self.levels, segs, world, 1,
+                                                       alpha)
+
 
 class QSGDMaxNormMultiScaleCompressor(_MultiScalePacked):
     """compressors.py:754-826.  Unpacked forms: no L x n float cache, the

@@ -400,10 +400,42 @@ class GlobalRandKMaxNormTwoScaleReducer(QSGDMaxNormTwoScaleReducer):
         self._indices_queue = []
 
     _next_indices = GlobalRandKMaxNormReducer._next_indices
+    _segment_pair = GlobalRandKMaxNormReducer._segment_pair
+
+    def _reduce_segments(self, comp, in_segs, out_segs):
+        """The step without a flat bucket (as GlobalRandKMaxNormReducer's):
+        the subset gathered from the tensors, the two-scale passes on it, the
+        setgrad tensor to tensor and the decode-scatter into grad_out
+        (reducer.py:1568-1628)."""
+        W = self.n_workers
+        codec = self._codec
+        idx = self._next_indices(in_segs.n, in_segs.device)
+        with self._timer("reduce.norm", verbosity=2):
+            xk, local = codec.randk_gather_absmax_segments(in_segs, idx)
+            norm = self._all_reduce(local, dist.ReduceOp.MAX)
+        with self._timer("reduce.compress", verbosity=2):
+            both = comp.encode_w1(norm, xk) if W == 1 else None
+            if both is not None:
+                mask, words = both
+            else:
+                mask = comp.encode_mask(norm, xk, world=W)
+                self._all_reduce(mask)
+                words = comp.encode(norm, xk, mask, world=W)
+        with self._timer("reduce.reduce.vector", verbosity=2):
+            self._all_reduce(words)
+        bits = self.n_bits(norm) + self.n_bits(mask) + self.n_bits(words)
+        with self._timer("reduce.setgrad", verbosity=2):
+            codec.segments_copy(in_segs, out_segs, 1.0 / W)
+        with self._timer("reduce.decompress", verbosity=2):
+            comp.decode_scatter_segments(norm, words, mask, idx, out_segs, world=W, alpha=1.0 / W)
+        return bits
 
     def reduce(self, grad_in, grad_out):
         W = self.n_workers
         comp = self._make()
+        pair = self._segment_pair(grad_in, grad_out)
+        if pair is not None and hasattr(comp, "decode_scatter_segments"):
+            return self._reduce_segments(comp, *pair)
         flat, _ = self._flat_pack(grad_in)
         n = flat.buffer.numel()
         idx = self._next_indices(n, flat.buffer.device)

@@ -305,6 +305,14 @@ int gc_ms_decode(const uint32_t *words, const uint32_t *mask_words, const int64_
 int gc_ms_decode_segments(const uint32_t *words, const uint32_t *mask_words, uint64_t n, const float *norm,
                           const gc_levels *levels, const gc_lanes *mask_lanes, const gc_lanes *q_lanes, int order,
                           float alpha, const gc_segments *segs, gc_stream_t stream);
+/* the GlobalRandK two-scale decode-scatter (gc_ms_decode with idx) into the
+ * tensors of segs: element idx[i] = RN(decode_i * alpha) + 0 (reducer.py:1617-1628:
+ * decompress, scatter into the flat buffer, setgrad x 1/W).  Every idx[i] must
+ * be in [0, segs->n) (not range-checked on the device) */
+int gc_ms_decode_scatter_segments(const uint32_t *words, const uint32_t *mask_words, const int64_t *idx, uint64_t k,
+                                  const float *norm, const gc_levels *levels, const gc_lanes *mask_lanes,
+                                  const gc_lanes *q_lanes, int order, float alpha, const gc_segments *segs,
+                                  gc_stream_t stream);
 /* unpacked selected level per element (int8), from a thermometer stream */
 int gc_ms_mask_unpack(const uint32_t *mask_words, const gc_lanes *mask_lanes, uint32_t levels_count,
                       int8_t *mask, gc_stream_t stream);

@@ -170,6 +170,30 @@ def test_randk_segments_equal_flat(k):
         codec.segments_copy(segs, codec.Segments(outs[:-1]))
 
 
+@pytest.mark.parametrize("levels,world", [([2, 4], 1), ([2, 4], 2), ([4, 8], 3)])
+def test_ms_decode_scatter_segments_equal_flat(levels, world):
+    """gc_ms_decode_scatter_segments (the GlobalRandK two-scale decode-scatter
+    into the tensors, x 1/W, + 0) == ms_decode with idx into a flat bucket
+    followed by the setgrad 0 + RN(g / W)."""
+    ts, ref = carve(RAGGED, seed=71)
+    segs = codec.Segments(ts, chunk_shift=6)
+    k = 20_000
+    idx = torch.randperm(segs.n, generator=torch.Generator().manual_seed(k))[:k].to(DEV)
+    xk = torch.from_numpy(ref).to(DEV)[idx]
+    norm = codec.absmax(xk)
+    r = gcodec.Generator(9, "philox").reserve(k, len(levels))
+    m = codec.ms_mask_encode(xk, norm, levels, r, world)
+    w = codec.ms_select_encode(xk, norm, levels, r, m, world)
+    flat = torch.from_numpy(ref).to(DEV)
+    codec.ms_decode(w, m, k, norm, levels, world, 1, 1.0, idx=idx, out=flat)
+    want = flat * np.float32(1.0 / world) + 0.0
+    outs = [torch.full_like(t, 5.0) for t in ts]
+    osegs = codec.Segments(outs, chunk_shift=9)
+    codec.segments_copy(segs, osegs, 1.0 / world)
+    codec.ms_decode_scatter_segments(w, m, idx, norm, levels, osegs, world, 1, 1.0 / world)
+    assert u32(torch.cat(outs)).tobytes() == u32(want).tobytes()
+
+
 REDUCERS = [
     ("QSGDMaxNormReducer", dict(quantization_level=4)),
     ("QSGDMaxNormTwoScaleReducer", dict(lower_quantization_level=2, higher_quantization_level=4)),
@@ -178,6 +202,7 @@ REDUCERS = [
     ("GlobalRandKMaxNormReducer", dict(K=20_000, quantization_level=4)),  # gather + encode (K > fused max)
     ("GlobalRandKMaxNormReducer", dict(K=1000, quantization_level=16)),   # b above the fused lanes
     ("GlobalRandKMaxNormTwoScaleReducer", dict(K=1000, lower_quantization_level=2, higher_quantization_level=4)),
+    ("GlobalRandKMaxNormTwoScaleReducer", dict(K=30_000, lower_quantization_level=4, higher_quantization_level=8)),
 ]
 
 
