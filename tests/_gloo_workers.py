@@ -304,3 +304,41 @@ def hook_vs_reference(rank, world, init_file, fixture, out_dir, use_gpu):
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def rccl_path_world(rank, world, init_file, out_dir):
+    """The QSGD-MN and multi-scale DP paths with every collective on RCCL
+    ("nccl"): absmax -> all_reduce(MAX) -> encode -> all_reduce(SUM words)
+    -> decode; mask lanes -> all_reduce(SUM) -> select -> all_reduce(SUM) ->
+    decode (reducer.py:516-554, 1636-1715).  Saves what the test checks."""
+    import gcodec
+    from gcodec import codec
+    from oracle import oracle as O
+
+    dev = torch.device("cuda", rank)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"file://{init_file}", rank=rank, world_size=world, device_id=dev)
+    n, bits, levels = 1_000_003, 4, [2, 4]
+    x = torch.from_numpy(O.gen_input(n, seed=11, kind=1)).to(dev)
+    gen = gcodec.Generator(9, "philox", per_rank=False)
+    norm = codec.absmax(x)
+    dist.all_reduce(norm, op=dist.ReduceOp.MAX)
+    off_q = gen.offset
+    words = codec.qsgd_encode(x, norm, bits, gen.reserve(n), world)
+    dist.all_reduce(words)
+    dec = codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world)
+    off_ms = gen.offset
+    r = gen.reserve(n, len(levels))
+    mw = codec.ms_mask_encode(x, norm, levels, r, world)
+    dist.all_reduce(mw)
+    mwords = codec.ms_select_encode(x, norm, levels, r, mw, world)
+    dist.all_reduce(mwords)
+    mdec = codec.ms_decode(mwords, mw, n, norm, levels, world, 0, 1.0 / world)
+    mask = codec.ms_mask_unpack(mw, n, levels, world)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, f"rccl{rank}.npz"), n=n, bits=bits, levels=np.array(levels), key=gen.seed,
+             off_q=off_q, off_ms=off_ms, backend=np.array(dist.get_backend()), world=dist.get_world_size(),
+             norm=norm.cpu().numpy(), words=words.cpu().numpy(), dec=dec.cpu().numpy(),
+             ms_mask=mask.cpu().numpy().astype(np.uint8), ms_dec=mdec.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
