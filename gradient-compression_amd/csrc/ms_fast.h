@@ -300,12 +300,11 @@ __device__ __forceinline__ uint4 cache_cells(const uint2 &u)
 // whole branches (each with its own draws), so the common fast path carries
 // no per-level divergence.
 template <int KIND, int NL, int VAR = 0, bool CACHE = false>
-__device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t n, uint32_t i0, const DivNorm &dv,
-                                           uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
-                                           const RngArgs &rng, uint32_t bit, uint4 (&mb)[NL - 1], int32_t cq = 0,
-                                           uint32_t cb = 0, uint4 *cv = nullptr)
+__device__ __forceinline__ void mask_plane_v(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                             uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                             const RngArgs &rng, uint32_t bit, uint4 (&mb)[NL - 1], int32_t cq = 0,
+                                             uint32_t cb = 0, uint4 *cv = nullptr)
 {
-    const float4 v = load4_nt_tail<0>(x, i0, n);
     RangeLo rg;
     rg.add4(v);
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
@@ -397,6 +396,16 @@ __device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t
     }
     if constexpr (CACHE)
         *cv = c;  // sum_l -q_l << (l cb): the caller's ms_cells turns it into the cells
+}
+
+template <int KIND, int NL, int VAR = 0, bool CACHE = false>
+__device__ __forceinline__ void mask_plane(const float *__restrict__ x, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                           uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                           const RngArgs &rng, uint32_t bit, uint4 (&mb)[NL - 1], int32_t cq = 0,
+                                           uint32_t cb = 0, uint4 *cv = nullptr)
+{
+    mask_plane_v<KIND, NL, VAR, CACHE>(load4_nt_tail<0>(x, i0, n), n, i0, dv, lo2, hi2, lv, fa, rng, bit, mb, cq, cb,
+                                       cv);
 }
 
 // OR the per-element bits of mask_plane into the field accumulators
@@ -941,7 +950,11 @@ __device__ __forceinline__ float4 load4_guard(const float *__restrict__ x, uint3
 }
 
 // blockDim = 64 r (r <= kMsFusedMaxR waves); wave h walks planes h + r k, k < Lq.
-template <int KIND, int NL, int VAR = 0>
+// U planes' loads are issued together before their math (U = 1: one plane at
+// a time): a wave's chain of dependent plane loads is what bounds the kernel
+// (at 7 waves per SIMD and one 1 KB load in flight per wave, Little's law
+// gives about the 3.2 TB/s it reaches), so U > 1 keeps U KB in flight per wave.
+template <int KIND, int NL, int VAR = 0, int U = 1>
 __global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(const float *__restrict__ x, uint32_t n,
                                                                  const float *__restrict__ normp, LevelsArg lv,
                                                                  MsFastArg fa, RngArgs rng, uint32_t Mm, uint32_t r,
@@ -957,6 +970,11 @@ __global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(con
     const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
     const uint32_t quads = Mm >> 2;
     const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    // planes k < kfull are full for every lane (their end (P + 1) Mm <=
+    // (pend - 1) Mm < n: plain 16-byte loads, no per-lane guard); planes
+    // k < kend hold elements (P < pend)
+    const uint32_t kend = h < pend ? min(Lq, (pend - h + r - 1) / r) : 0u;
+    const uint32_t kfull = h + 1 < pend ? min(kend, (pend - 1 - h + r - 1) / r) : 0u;
     __shared__ uint4 part[kMsFusedMaxR - 1][NL - 1][kMsQuadsPerBlock];
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < quads; tb += gridDim.x * kMsQuadsPerBlock) {
         const uint32_t t = tb + lane;
@@ -965,17 +983,26 @@ __global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(con
         if (t < quads) {
             uint32_t i0 = h * Mm + 4u * t;
             const uint32_t step = r * Mm;
-            // planes below pend - 1 are full for every lane (their end (P + 1) Mm
-            // <= (pend - 1) Mm < n): plain 16-byte loads, no per-lane guard
-            auto load = [&](uint32_t k, uint32_t i) {
-                return h + r * k + 1 < pend ? ld_nt(reinterpret_cast<const float4 *>(x + i)) : load4_guard(x, i, n);
-            };
-            // one plane at a time (a next-plane register prefetch measured the
-            // same: the waves of the CU hide the load latency)
+            uint32_t k = 0;
+            if constexpr (U > 1) {
 #pragma unroll 1
-            for (uint32_t k = 0; k < Lq && h + r * k < pend; ++k) {  // planes past pend hold no element
-                fused_plane_r<KIND, NL, VAR>(load(k, i0), n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (h + r * k), k * wq,
-                                             macc, acc, qmax);
+                for (; k + U <= kfull; k += U) {
+                    float4 xv[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        xv[u] = ld_nt(reinterpret_cast<const float4 *>(x + i0 + u * step));
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        fused_plane_r<KIND, NL, VAR>(xv[u], n, i0 + u * step, dv, lo2, hi2, lv, fa, rng,
+                                                     1u << (h + r * (k + u)), (k + u) * wq, macc, acc, qmax);
+                    i0 += U * step;
+                }
+            }
+#pragma unroll 1
+            for (; k < kend; ++k) {
+                const float4 v = k < kfull ? ld_nt(reinterpret_cast<const float4 *>(x + i0)) : load4_guard(x, i0, n);
+                fused_plane_r<KIND, NL, VAR>(v, n, i0, dv, lo2, hi2, lv, fa, rng, 1u << (h + r * k), k * wq, macc, acc,
+                                             qmax);
                 i0 += step;
             }
         }

@@ -359,6 +359,20 @@ static uint64_t ms_tiles()
     return t;
 }
 
+// planes per load batch of the one-pass W = 1 encode (k_ms_fused_w1's U) for
+// two levels with Philox draws: 2 (33.7-33.9 against 34.9-35.0 us at U = 1 on
+// the ResNet50 bucket, 73 against 57 VGPRs; U = 3 the same as 2:
+// profiles/r03s_ms_sweep_u*.log).  GC_MS_FUSED_U=1 selects the one-plane loop
+// (measurement only)
+static int ms_fused_u()
+{
+    static const int u = [] {
+        const char *e = getenv("GC_MS_FUSED_U");
+        return e && atol(e) == 1 ? 1 : 2;
+    }();
+    return u;
+}
+
 // q cache geometry (ms_fast.h): cell bytes per element (0 = not supported:
 // outside the dense wave-split kernels, or the count fields of cb bits exceed
 // 16 bits).  Levels of 8-24 bits (MSV_WIDE) cache too: the cell holds the
@@ -438,11 +452,15 @@ int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_leve
     for (uint32_t k = 0; k < q_lanes->per_word; ++k)
         Cw += (uint32_t)qmax << (k * q_lanes->bits);
     const uint32_t pend = (uint32_t)((n + Mm - 1) / Mm);
-#define GC_FW(KIND_, NL_, VAR_)                                                                                   \
-    hipLaunchKernelGGL((k_ms_fused_w1<KIND_, NL_, VAR_>), dim3(g), dim3(64 * r), 0, st, x, (uint32_t)n, norm, la, \
+#define GC_FW(KIND_, NL_, ...)                                                                                     \
+    hipLaunchKernelGGL((k_ms_fused_w1<KIND_, NL_, __VA_ARGS__>), dim3(g), dim3(64 * r), 0, st, x, (uint32_t)n, norm, la, \
                        fa, ra, Mm, r, q_lanes->per_word, q_lanes->bits, qmax, Cw, pend, mask_words, words)
     if (levels->count == 2) {
-        if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 2, MSV_WIDE); } else { GC_FW(0, 2, MSV_EAGER0); } }
+        if (rng->kind == GC_RNG_PHILOX) {
+            if (wide) { GC_FW(0, 2, MSV_WIDE); }
+            else if (ms_fused_u() == 2) { GC_FW(0, 2, MSV_EAGER0, 2); }
+            else { GC_FW(0, 2, MSV_EAGER0); }
+        }
         else { if (wide) { GC_FW(1, 2, MSV_WIDE); } else { GC_FW(1, 2, 0); } }
     } else {
         if (rng->kind == GC_RNG_PHILOX) { if (wide) { GC_FW(0, 3, MSV_WIDE); } else { GC_FW(0, 3, MSV_EAGER0); } }
