@@ -49,6 +49,7 @@ for js_p, gs_p, cs_p in ((HIGH, HIGH, None), (HIGH, NORM, None), (NORM, HIGH, No
     torch.cuda.synchronize()
     codec._MT_SIDE[dev.index] = (torch.cuda.Stream(dev, priority=js_p), torch.cuda.Stream(dev, priority=gs_p))
     codec._MT_SPEC.pop(dev.index, None)
+    codec._MT_LAST.pop(dev.index, None)  # the dropped run moved the device state: send torch's again
     caller = torch.cuda.Stream(dev, priority=cs_p) if cs_p is not None else None
     name = lambda p: "high" if p == HIGH else "normal"  # noqa: E731
     print(f"jumps {name(js_p)}, generators {name(gs_p)}, caller {name(cs_p) if cs_p is not None else 'default'}: "
