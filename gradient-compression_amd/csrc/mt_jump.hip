@@ -86,47 +86,33 @@ __device__ __forceinline__ void twist_column(const uint32_t *o, uint32_t *nw, ui
         nw[k] = mtj_mix(c0, mtj_mix(o[0], o[1], o[kMtM]), B);
 }
 
-// x_0 .. x_{kMtSeqWs-1} of the caller's state frame; window 0 and the read index
+// x_0 .. x_{kMtSeqWs-1} of the caller's state frame; window 0 and the read index.
+// One workgroup: the block after b is twisted column by column (twist_column,
+// one column per lane of the first 227 threads) from one LDS buffer into the
+// other, and all 256 threads store it.  One barrier per block, waiting on LDS
+// traffic only: __syncthreads would also drain the global stores in flight
+// (seven of those per block took this chain-critical kernel to 20 us, 38 us
+// beside the pipeline's other kernels).
 __global__ __launch_bounds__(256) void k_mt_seq(const uint32_t *__restrict__ state, uint32_t *__restrict__ ws)
 {
-    __shared__ uint32_t s[kMtN];
+    __shared__ uint32_t buf[2][kMtN];
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < kMtN; i += 256) {
-        s[i] = state[i];
-        ws[kWsSeq + i] = state[i];
-        ws[kWsWin + i] = state[i];  // generator 0 starts from the state itself
+        const uint32_t v = state[i];
+        buf[0][i] = v;
+        ws[kWsSeq + i] = v;
+        ws[kWsWin + i] = v;  // generator 0 starts from the state itself
     }
     if (tid == 0)
         ws[0] = state[kMtN];
     __syncthreads();
     for (uint32_t b = 1; b < kMtSeqWs / kMtN; ++b) {
-        // block-wide twist: the three phases with barriers
-        uint32_t v = 0;
-        constexpr uint32_t H = kMtN - kMtM;
-        if (tid < H)
-            v = mtj_mix(s[tid], s[tid + 1], s[tid + kMtM]);
-        __syncthreads();
-        if (tid < H)
-            s[tid] = v;
-        __syncthreads();
-        if (tid < H)
-            v = mtj_mix(s[H + tid], s[H + tid + 1], s[tid]);
-        __syncthreads();
-        if (tid < H)
-            s[H + tid] = v;
-        __syncthreads();
-        const uint32_t k = 2 * H + tid;
-        if (k < kMtN - 1)
-            v = mtj_mix(s[k], s[k + 1], s[k - H]);
-        else if (k == kMtN - 1)
-            v = mtj_mix(s[k], s[0], s[k - H]);
-        __syncthreads();
-        if (k < kMtN)
-            s[k] = v;
-        __syncthreads();
+        // block b from block b-1 (the other buffer); the stores of block b-1
+        // read this buffer before the previous barrier (lgkmcnt(0) there)
+        twist_column(buf[(b - 1) & 1u], buf[b & 1u], tid);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         for (uint32_t i = tid; i < kMtN; i += 256)
-            ws[kWsSeq + (uint64_t)b * kMtN + i] = s[i];
-        __syncthreads();
+            ws[kWsSeq + (uint64_t)b * kMtN + i] = buf[b & 1u][i];
     }
 }
 
