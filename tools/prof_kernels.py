@@ -38,12 +38,13 @@ while time.perf_counter() - t0 < SETTLE:  # clocks ramp over ~0.1-0.3 s of susta
         codec.absmax(x3, out=nrm)
         ms.encode_w1(nrm, x3)
     torch.cuda.synchronize()
+dout = torch.empty(n3, device=dev)  # the decode writes one preallocated buffer, as in bench.py
 for _ in range(REPS):
     codec.absmax(x3, out=nrm)
     m, w = ms.encode_w1(nrm, x3)
     m2 = ms.encode_mask(nrm, x3, 1)
     w2 = ms.encode(nrm, x3, m2, 1)
-    ms.decode(nrm, w2, m2, n3, 1, 1.0)
+    ms.decode(nrm, w2, m2, n3, 1, 1.0, out=dout)
 # the W > 1 default (q_cache): mask pass + q cache cells, then the select from
 # the cache, at W = 2 lane sizing (one rank's mask: timing only)
 msc = gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen, q_cache=True)
