@@ -1,6 +1,8 @@
-"""The headline step (absmax -> QSGD-MN 4-bit encode, 100M fp32) per encode
-grid cap (GC_ENC_GRID, read once per process: run once per value).
-    GC_ENC_GRID=16384 python tools/enc_grid_sweep.py"""
+"""The headline step (absmax -> QSGD-MN 4-bit encode, 100M fp32), timed as
+queued loops.  For the r03zk sweep (profiles/r03zk_enc_grid_sweep.log) the
+library temporarily read a GC_ENC_GRID grid cap; the product keeps its fixed
+12288-block grid, so this now times the product step.
+    python tools/enc_grid_sweep.py"""
 import os
 import sys
 
