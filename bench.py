@@ -49,8 +49,22 @@ def _args():
                     help="bucket elements per rank (--numel under torchrun, whose parser takes --n as ambiguous)")
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-oracle sample budget (0 = skip)")
-    ap.add_argument("--no-extras", action="store_true", help="skip decode / reduce-path / parity-mode legs")
-    return ap.parse_args()
+    ap.add_argument("--no-extras", action="store_true", help="skip every leg after the headline (= --legs none)")
+    ap.add_argument("--legs", default="all",
+                    help="comma list of the legs after the headline: " + ",".join(LEGS) + " (or all / none)")
+    ap.add_argument("--n5", type=int, default=1_000_000_000, help="config 5 bucket elements per rank")
+    a = ap.parse_args()
+    want = "none" if a.no_extras else a.legs
+    a.legs = (set(LEGS) if want == "all" else set() if want == "none" else
+              {s.strip() for s in want.split(",") if s.strip()})
+    bad = a.legs - set(LEGS)
+    if bad:
+        ap.error(f"unknown legs {sorted(bad)}; known: {','.join(LEGS)}")
+    return a
+
+
+# the legs after the headline, in the order they run (none of them is `value`)
+LEGS = ("decode", "reduce", "torch", "pcie", "config3", "epilogue", "config4", "config5", "packers")
 
 
 _HOLD_MS_PER_MCYCLE = []
@@ -96,7 +110,7 @@ def _events(torch, fn, reps):
 def _traffic(kernel: str, n: int, bits: int):
     """HBM bytes per launch of `kernel` from the committed PMC profile
     (profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
-    over this same workload, collected by tools/profile.sh on an earlier run)
+    over this same workload, collected by tools/gpu.sh pmc on an earlier run)
     -> (bytes, source) or (None, None).  Not measured by this run: PMC
     counters need their own rocprofv3 pass."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -274,9 +288,9 @@ def pcie_inclusive(torch, codec, gen, x, n, bits, world, lanes, K):
     return res
 
 
-def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
-    """BASELINE.json configs 3-5 (parity cases; not the headline `value`)."""
-    from gcodec import shapes
+def other_configs(torch, dist, gcodec, codec, dev, world, rank, K, legs, n5):
+    """BASELINE.json configs 3-5 and the fused epilogue (parity cases; not the
+    headline `value`), the ones named in `legs`."""
     res = {}
     reps = max(20, K)
 
@@ -299,11 +313,26 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
             el = t.item()
         return el / reps * 1e3
 
+    if legs & {"config3", "epilogue"}:
+        res.update(_config3_epilogue(torch, dist, gcodec, codec, dev, world, rank, sync_ms, reps, legs))
+    if "config4" in legs:
+        res.update(_config4(torch, dist, gcodec, codec, dev, world, rank, sync_ms, reps))
+    if "config5" in legs:
+        res.update(_config5(torch, dist, gcodec, codec, dev, world, sync_ms, n5))
+    torch.cuda.empty_cache()
+    return res
+
+
+def _config3_epilogue(torch, dist, gcodec, codec, dev, world, rank, sync_ms, reps, legs):
+    from gcodec import shapes
+    res = {}
+    g = torch.Generator(device=dev).manual_seed(11 + rank)
+    gen = gcodec.Generator(5 + rank, "philox")
+    if "config3" not in legs:
+        return _epilogue(torch, gcodec, codec, dev, world, g, gen, sync_ms, res)
     # config 3: two-scale "4+2" on a ResNet50-sized bucket (MultiScale levels [2, 4])
     n3 = 23_520_842
-    g = torch.Generator(device=dev).manual_seed(11 + rank)
     x3 = torch.randn(n3, device=dev, generator=g).mul_(0.01)
-    gen = gcodec.Generator(5 + rank, "philox")
     for tag, ms in (("twoscale_2_4", gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen)),
                     ("multiscale_2_4", gcodec.QSGDMaxNormMultiScaleCompressor(dev, [2, 4], generator=gen)),
                     ("twoscale_2_4_q_cache",
@@ -376,8 +405,14 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
             "kernels": kernels}
         del m_, w_, d_
     del x3
+    if "epilogue" in legs:
+        _epilogue(torch, gcodec, codec, dev, world, g, gen, sync_ms, res)
+    return res
 
-    # fused TensorBuffer / setgrad on the ResNet50 list (161 tensors)
+
+def _epilogue(torch, gcodec, codec, dev, world, g, gen, sync_ms, res):
+    """fused TensorBuffer / setgrad on the ResNet50 list (161 tensors)."""
+    from gcodec import shapes
     sizes = shapes.resnet50_sizes()
     base = torch.randn(sum(sizes) + 4 * len(sizes), device=dev, generator=g).mul_(0.01)
     grads, pos = [], 0
@@ -406,7 +441,13 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
         ep[f"reducer_step_ms_{'fused' if fused else 'unfused'}"] = sync_ms(lambda: red.reduce(grads, grads))
     res["epilogue_resnet50_qsgd4"] = ep
     del base, grads, segs, flat
+    return res
 
+
+def _config4(torch, dist, gcodec, codec, dev, world, rank, sync_ms, reps):
+    from gcodec import shapes
+    res = {}
+    gen = gcodec.Generator(5 + rank, "philox")
     # config 4: GRandK K=10000, 4-bit, VGG16-sized bucket: gather -> encode -> RCCL -> decode/scatter.
     # codec.RandKStep: pointers and structs resolved once, one ctypes call per launch.  W = 1: gather +
     # max-norm + encode in one launch (gc_randk_encode_w1), then the decode-scatter; W > 1: gather + local
@@ -502,19 +543,28 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
         except Exception as e:  # capture unsupported on this runtime: report, do not fail the bench
             res["config4_grandk_k10000"]["hipgraph_us_per_step"] = f"capture failed: {type(e).__name__}: {e}"
     del x4
+    return res
 
-    # config 5: 1B fp32, 8-bit, chunked encode | RCCL SUM | decode on separate streams
-    n5 = 1_000_000_000
+
+def _config5(torch, dist, gcodec, codec, dev, world, sync_ms, n5):
+    """config 5: 1B fp32, 8-bit, chunked encode | RCCL SUM | decode on separate
+    streams.  N > 1: one extra traced call records, from HIP events, whether
+    chunk c's decode started (and finished) before chunk c+1's SUM ended."""
+    res = {}
+    gen = gcodec.Generator(17, "philox")
     try:
         x5 = torch.empty(n5, device=dev).normal_(0, 0.01)
         out5 = torch.empty_like(x5)
         pipe = gcodec.ChunkedQSGDAllReduce(n5, 8, dev, chunks=8, generator=gen)
         t = sync_ms(lambda: pipe(x5, out5), reps=3)
         ln = codec.qsgd_layout(n5, 8, world)
-        res["config5_1b_8bit_chunked"] = {
-            "n": n5, "chunks": 8, "ms_per_step": t, "grad_floats_per_s": world * n5 / (t * 1e-3),
-            "lane_bits": ln.bits, "packed_bytes_per_rank": 4 * ln.plane_words,
-            "reference_wire_bytes_per_rank": 4 * n5}
+        r = {"n": n5, "chunks": 8, "ms_per_step": t, "grad_floats_per_s": world * n5 / (t * 1e-3),
+             "lane_bits": ln.bits, "packed_bytes_per_rank": 4 * ln.plane_words,
+             "reference_wire_bytes_per_rank": 4 * n5}
+        if world > 1:
+            tr = pipe.trace(x5, out5)
+            r["overlap"] = tr
+        res["config5_1b_8bit_chunked"] = r
         del x5, out5, pipe
     except torch.cuda.OutOfMemoryError:
         res["config5_1b_8bit_chunked"] = {"skipped": "out of device memory"}
@@ -522,8 +572,263 @@ def other_configs(torch, dist, gcodec, codec, dev, world, rank, K):
     return res
 
 
+def _timed_steps(torch, dist, fn, k, world, dev) -> float:
+    """Seconds for k calls of fn, barrier + synchronize on both sides, MAX over ranks."""
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    return el
+
+
+def reduce_legs(torch, dist, codec, step, words, dec, norm, n, bits, world, lanes, K, dev) -> dict:
+    """The full DP path: absmax -> MAX -> encode -> all_reduce(SUM packed words)
+    -> decode + 1/W; at N >= 4 (even) also through gcodec.NodeTopology as two
+    'nodes' of N/2 ranks, with the flat and hierarchical sums compared."""
+    res = {}
+
+    def path():
+        step()
+        if world > 1:
+            dist.all_reduce(words)
+        codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
+
+    pel = _timed_steps(torch, dist, path, K, world, dev)
+    res["reduce_path"] = {"grad_floats_per_s": world * n * K / pel, "ms_per_step": pel / K * 1e3,
+                          "packed_bytes_per_rank": 4 * lanes.plane_words,
+                          "steps": "absmax, all_reduce MAX, encode, all_reduce SUM (RCCL), decode + 1/W"}
+    if world >= 4 and world % 2 == 0:
+        # intra reduce-scatter, "inter-node" all-reduce of 1/L of the words, intra
+        # all-gather: the multi-node code path on one node
+        try:
+            from gcodec.topology import NodeTopology
+            topo = NodeTopology(world // 2)
+
+            def hpath():
+                step()
+                topo.all_reduce(words)
+                codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
+
+            hel = _timed_steps(torch, dist, hpath, K, world, dev)
+            step()  # flat vs hierarchical sum of the same encoded words
+            a = words.clone()
+            dist.all_reduce(a)
+            b = words.clone()
+            topo.all_reduce(b)
+            ok = torch.tensor([int(torch.equal(a, b))], device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank's sums agree
+            res["reduce_path_2x_nodes"] = {"ms_per_step": hel / K * 1e3, "local_size": world // 2,
+                                           "bit_identical_to_flat": bool(ok.item())}
+        except Exception as e:  # noqa: BLE001 — report, never fail the headline bench
+            res["reduce_path_2x_nodes"] = f"failed: {type(e).__name__}: {e}"
+    return res
+
+
+def torch_mode_leg(torch, np, gcodec, codec, x, n, bits, words, lanes, dev, pgen_philox) -> dict:
+    """Reference-parity mode (compressors.py:310 under torch.manual_seed): the
+    torch CPU generator's MT19937 stream made on the GPU (jumped parallel
+    generators on two side streams), then the encode from those draws; torch's
+    generator state advances exactly as the reference's would.  Timed three
+    ways against the Philox path in the same harness (W = 1 lanes):
+    encode only (norm fixed), absmax + encode per call (what a reducer does),
+    and a training cadence (each call behind a few ms of unrelated GPU work,
+    the backward, so the speculation has time to run ahead)."""
+    pgen = gcodec.Generator(0, "torch")
+    torch.manual_seed(42)
+    nm = codec.absmax(x)
+    pgen.reserve(n)  # warm: builds the jump table once per process
+    codec.qsgd_encode_torch(x, nm, bits, 1, out=words, lanes=lanes)
+
+    def enc_torch():
+        codec.qsgd_encode(x, nm, bits, pgen.reserve(n), 1, out=words, lanes=lanes)
+
+    def step_torch():
+        codec.absmax(x, out=nm)
+        enc_torch()
+
+    def enc_philox():
+        codec.qsgd_encode(x, nm, bits, pgen_philox.reserve(n), 1, out=words, lanes=lanes)
+
+    def step_philox():
+        codec.absmax(x, out=nm)
+        enc_philox()
+
+    def per_call_ms(fn, reps=20, runs=3):
+        for _ in range(8):  # warm: both end-state jump polynomials of this count, the speculation started
+            fn()
+        torch.cuda.synchronize()
+        best = []
+        for _ in range(runs):  # the fastest of `runs` timed loops
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            best.append((time.perf_counter() - t0) / reps * 1e3)
+        return min(best), best
+
+    enc_ms, enc_runs = per_call_ms(enc_torch)
+    stp_ms, stp_runs = per_call_ms(step_torch)
+    enc_px, _ = per_call_ms(enc_philox)
+    stp_px, _ = per_call_ms(step_philox)
+    t0 = time.perf_counter()
+    for _ in range(20):  # fused: the generator kernel quantizes with its own draws, then the lane pack
+        codec.qsgd_encode_torch(x, nm, bits, 1, out=words, lanes=lanes)
+    torch.cuda.synchronize()
+    t_fused = (time.perf_counter() - t0) / 20 * 1e3
+
+    # training cadence: a stand-in backward (bf16 GEMMs, ~3 ms) between calls
+    a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    c = torch.empty_like(a)
+
+    def backward():
+        for _ in range(3):
+            torch.mm(a, a, out=c)
+
+    bw_ms, _ = per_call_ms(backward, reps=10)
+    cad_torch, _ = per_call_ms(lambda: (backward(), step_torch()), reps=10)
+    cad_px, _ = per_call_ms(lambda: (backward(), step_philox()), reps=10)
+    del a, c
+
+    st = codec.mt19937_seed_state(42)
+    sd = torch.from_numpy(st.view(np.int32)).to(dev)
+    draws = torch.empty(n, dtype=torch.int32, device=dev)
+    ms_gen = _events(torch, lambda: codec.mt19937_generate(sd, n, out=draws), 3)
+    ms_ser = _events(torch, lambda: codec.mt19937_generate(sd, 10_000_000, out=draws, parallel=False), 1)
+    del draws
+    return {
+        "n": n,
+        "encode_only": {"ms_per_call": enc_ms, "grad_floats_per_s": n / (enc_ms * 1e-3), "runs_ms": enc_runs,
+                        "philox_ms_per_call": enc_px, "frac_of_philox_rate": enc_px / enc_ms},
+        "absmax_plus_encode": {"ms_per_call": stp_ms, "grad_floats_per_s": n / (stp_ms * 1e-3), "runs_ms": stp_runs,
+                               "philox_ms_per_call": stp_px, "frac_of_philox_rate": stp_px / stp_ms},
+        "training_cadence": {"backward_standin_ms": bw_ms, "torch_added_ms_per_call": cad_torch - bw_ms,
+                             "philox_added_ms_per_call": cad_px - bw_ms,
+                             "note": "each step = 3 bf16 8192^3 GEMMs (the stand-in backward) then absmax + "
+                                     "encode; added = step - GEMMs alone (the side-stream draws run during "
+                                     "the GEMMs and share the chip with them)"},
+        "fused_generator_quantize_ms_per_call": t_fused,
+        "mt19937_parallel_ms": ms_gen, "mt19937_parallel_draws_per_s": n / (ms_gen * 1e-3),
+        "mt19937_serial_draws_per_s": 10_000_000 / (ms_ser * 1e-3),
+        "note": "torch-CPU-generator (MT19937) draws, bit-exact with compressors.py: jump-ahead parallel "
+                "generators on two high-priority side streams (phase 1 = sequence + jumps + a jump straight to "
+                "the end state, phase 2 = the generators) -> encode from the draws on the caller's stream; "
+                "torch's state is written back every call (host sync) as soon as phase 1 is done; back to back, "
+                "the next same-size call's run is enqueued behind this one and used only if torch's generator "
+                "is untouched.  The headline (Philox) step is absmax + encode: compare absmax_plus_encode."}
+
+
+def packers_leg(torch, gcodec, codec, dev, gen, rank) -> dict:
+    """The literal drop-in packers on the ResNet50 bucket (23,520,842 elements,
+    4-bit sign + xi of the QSGDBP call site, compressors.py:338-378): device
+    greedy 4-mode pack / unpack (Extension CPU/bitpacking.cpp:16-55) and byte
+    pack / unpack (Extension CPU BP/bytepacking.cpp:6-64), each timed as queued
+    launches with HIP events; algorithmic bytes = what the call must read +
+    write.  Plus the QSGDBPCompressor.compress / decompress calls end to end
+    (they synchronise: word counts go to the host)."""
+    n = 23_520_842
+    g = torch.Generator(device=dev).manual_seed(21 + rank)
+    x = torch.randn(n, device=dev, generator=g).mul_(0.01)
+    nm = codec.absmax(x)
+    xi, sg = codec.qsgd_quantize_split(x, nm, 4, gen.reserve(n))
+    res = {"n": n, "bits": 4}
+
+    def row(us, nbytes, **kw):
+        gbs = nbytes / (us * 1e-6) / 1e9
+        return {"us": us, "algorithmic_bytes": nbytes, "gbs": gbs, "frac_hbm_peak": gbs / HBM_PEAK_GBS, **kw}
+
+    pk = gcodec.codec.Greedy4Device(n, dev)
+    for name, src in (("xi", xi), ("sign", sg)):
+        pk.pack(src)
+        nw = pk.result()
+        w = pk.words[:nw].clone()
+        us_p = _events(torch, lambda: pk.pack(src), 20) * 1e3
+        pk.unpack(w)
+        cnt = pk.result()
+        ok = bool(torch.equal(pk.values[:n], src))
+        us_u = _events(torch, lambda: pk.unpack(w), 20) * 1e3
+        res[f"greedy4_pack_{name}"] = row(us_p, 4 * n + 4 * nw, words=nw)
+        res[f"greedy4_unpack_{name}"] = row(us_u, 4 * nw + 4 * cnt, values=cnt, round_trip_exact=ok)
+    q8 = codec.qsgd_quantize(x, nm, 4, gen.reserve(n))
+    bw = codec.bytepack8(q8)
+    us_bp = _events(torch, lambda: codec.bytepack8(q8), 20) * 1e3
+    us_bu = _events(torch, lambda: codec.byteunpack8(bw), 20) * 1e3
+    res["bytepack8_int8"] = row(us_bp, n + 8 * bw.numel())
+    res["byteunpack8"] = row(us_bu, 8 * bw.numel() + 8 * bw.numel())
+    comp = gcodec.QSGDBPCompressor(dev, 4, generator=gen)
+    c = comp.compress(x)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        c = comp.compress(x)
+    torch.cuda.synchronize()
+    t_c = (time.perf_counter() - t0) / 10 * 1e3
+    t0 = time.perf_counter()
+    for _ in range(10):
+        comp.decompress(c[0], c[1], c[2], n)
+    torch.cuda.synchronize()
+    t_d = (time.perf_counter() - t0) / 10 * 1e3
+    res["qsgdbp_compress_ms"] = t_c
+    res["qsgdbp_decompress_ms"] = t_d
+    res["qsgdbp_note"] = ("compress = absmax + quantize_split + 2 device greedy4 packs + 3 host syncs (norm, word "
+                          "counts); the reference packs on the host at 0.56 M elem/s (BASELINE.md)")
+    del x, xi, sg, q8, bw, pk
+    return res
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` (N > 1) without a launcher: start N ranks
+    as ONE child `python -m torch.distributed.run` (one process per GPU,
+    rendezvous on 127.0.0.1), before this process has touched the GPU, and
+    return the child's exit code.  Never an exec: the child is a separate
+    process, this one only forwards its output (rank 0's JSON line included)."""
+    import subprocess
+
+    # torchrun's own parser would take a bare "--n" as an abbreviation of its options
+    fwd = ["--numel" if a == "--n" else ("--numel=" + a[4:] if a.startswith("--n=") else a) for a in sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *fwd]
+    print(f"bench.py: --gpus {n} without WORLD_SIZE: launching {n} ranks ({' '.join(cmd[1:5])} ...)",
+          file=sys.stderr, flush=True)
+    env = dict(os.environ, GC_BENCH_LAUNCHED="1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = _args()
+    if args.gpus < 1:
+        print(f"bench.py: --gpus {args.gpus} must be >= 1", file=sys.stderr)
+        return 2
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if os.environ.get("GC_BENCH_LAUNCHED"):  # the child launcher did not set it: never recurse
+            print("bench.py: launched ranks have no WORLD_SIZE", file=sys.stderr)
+            return 2
+        return launch_ranks(args.gpus)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree",
+              file=sys.stderr)
+        return 2
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -531,7 +836,6 @@ def main():
     import gcodec
     from gcodec import codec
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # GC_BENCH_BACKEND=gloo: rehearsal of the N>1 control flow on a 1-GPU box
@@ -539,6 +843,10 @@ def main():
     backend = os.environ.get("GC_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local %= max(torch.cuda.device_count(), 1)
+    elif world > 1 and torch.cuda.device_count() < world:  # device_count does not initialise the GPU
+        print(f"bench.py: {world} ranks over RCCL need {world} GPUs, {torch.cuda.device_count()} visible",
+              file=sys.stderr)
+        return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -728,9 +1036,10 @@ def main():
     if world > 1:
         out["process_group"] = _pg_evidence(torch, dist, dev, local, 4 * M)
 
-    if not args.no_extras:
+    legs = args.legs
+    dec = torch.empty(n, dtype=torch.float32, device=dev) if legs & {"decode", "reduce"} else None
+    if "decode" in legs:
         # decode of the (W-summed) words, 1/W folded in
-        dec = torch.empty(n, dtype=torch.float32, device=dev)
         ms_dec = _events(torch, lambda: codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec,
                                                            lanes=lanes), reps)
         out["kernels_ms"]["k_qsgd_decode"] = ms_dec
@@ -742,123 +1051,19 @@ def main():
         copy_gbs = 8 * n / (ms_copy * 1e-3) / 1e9
         out["roofline"]["achievable_copy_gbs"] = copy_gbs
         out["roofline"]["frac_of_copy"] = out["roofline"]["achieved"] / copy_gbs
-
-        # full DP path: norm -> encode -> all_reduce(SUM words) -> decode
-        def path():
-            step()
-            if world > 1:
-                dist.all_reduce(words)
-            codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
-
-        for _ in range(2):
-            path()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(K):
-            path()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        pel = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([pel], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            pel = t.item()
-        out["reduce_path"] = {"grad_floats_per_s": world * n * K / pel, "ms_per_step": pel / K * 1e3,
-                              "packed_bytes_per_rank": 4 * M,
-                              "steps": "absmax, all_reduce MAX, encode, all_reduce SUM (RCCL), decode + 1/W"}
-
-        if world >= 4 and world % 2 == 0:
-            # the same path through gcodec.NodeTopology as if the node were 2 nodes of
-            # world/2 GPUs (intra reduce-scatter, "inter-node" all-reduce of 1/L of the
-            # words, intra all-gather): the multi-node code path on one node
-            try:
-                from gcodec.topology import NodeTopology
-                topo = NodeTopology(world // 2)
-
-                def hpath():
-                    step()
-                    topo.all_reduce(words)
-                    codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
-
-                for _ in range(2):
-                    hpath()
-                torch.cuda.synchronize()
-                dist.barrier()
-                t0 = time.perf_counter()
-                for _ in range(K):
-                    hpath()
-                torch.cuda.synchronize()
-                dist.barrier()
-                hel = time.perf_counter() - t0
-                t = torch.tensor([hel], dtype=torch.float64, device=dev)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                # flat vs hierarchical sum of the same encoded words
-                step()
-                a = words.clone()
-                dist.all_reduce(a)
-                step_b = words.clone()
-                topo.all_reduce(step_b)
-                hier_ok = bool(torch.equal(a, step_b))
-                out["reduce_path_2x_nodes"] = {"ms_per_step": t.item() / K * 1e3, "local_size": world // 2,
-                                               "bit_identical_to_flat": hier_ok}
-            except Exception as e:  # noqa: BLE001 — report, never fail the headline bench
-                out["reduce_path_2x_nodes"] = f"failed: {type(e).__name__}: {e}"
-
-        del dec
-        # reference-parity mode: torch CPU-generator (MT19937) stream, generated on the
-        # GPU by the jumped parallel generators, then the encode from those draws;
-        # per call: torch state read -> H2D, draws, encode, state D2H (synchronises)
-        pgen = gcodec.Generator(0, "torch")
-        torch.manual_seed(42)
-        nm = codec.absmax(x)
-        pgen.reserve(n)  # warm: builds the jump table once per process
-        codec.qsgd_encode_torch(x, nm, bits, 1, out=words, lanes=lanes)
-        for _ in range(8):  # warm: both end-state jump polynomials of this count, the speculation started
-            codec.qsgd_encode(x, nm, bits, pgen.reserve(n), 1, out=words, lanes=lanes)
-        torch.cuda.synchronize()
-        reps_mt = 20
-        runs_mt = []
-        for _ in range(3):  # timed loops (the first still fills the side streams' pipeline): the fastest is reported
-            t0 = time.perf_counter()
-            for _ in range(reps_mt):  # draw buffer: 4n bytes of draws, then the full-chip encode reads them
-                codec.qsgd_encode(x, nm, bits, pgen.reserve(n), 1, out=words, lanes=lanes)
-            torch.cuda.synchronize()
-            runs_mt.append((time.perf_counter() - t0) / reps_mt)
-        t_mt = min(runs_mt)
-        t0 = time.perf_counter()
-        for _ in range(reps_mt):  # fused: the generator kernel quantizes with its own draws, then the lane pack
-            codec.qsgd_encode_torch(x, nm, bits, 1, out=words, lanes=lanes)
-        torch.cuda.synchronize()
-        t_mt_fused = (time.perf_counter() - t0) / reps_mt
-        st = codec.mt19937_seed_state(42)
-        sd = torch.from_numpy(st.view(np.int32)).to(dev)
-        draws = torch.empty(n, dtype=torch.int32, device=dev)
-        ms_gen = _events(torch, lambda: codec.mt19937_generate(sd, n, out=draws), 3)
-        ms_ser = _events(torch, lambda: codec.mt19937_generate(sd, 10_000_000, out=draws, parallel=False), 1)
-        out["torch_parity_mode"] = {
-            "n": n, "grad_floats_per_s": n / t_mt, "ms_per_call": t_mt * 1e3,
-            "ms_per_call_runs": [r * 1e3 for r in runs_mt],
-            "fused_generator_quantize_ms_per_call": t_mt_fused * 1e3,
-            "mt19937_parallel_ms": ms_gen, "mt19937_parallel_draws_per_s": n / (ms_gen * 1e-3),
-            "mt19937_serial_draws_per_s": 10_000_000 / (ms_ser * 1e-3),
-            "note": "torch-CPU-generator (MT19937) draws, bit-exact with compressors.py: jump-ahead parallel "
-                    "generators on two high-priority side streams (gc_mt19937_generate_split_j: phase 1 = "
-                    "sequence + jumps + a jump straight to the end state, phase 2 = the generators) -> encode "
-                    "from the draws on the caller's stream; torch's state is written back every call as soon as "
-                    "phase 1 is done; back-to-back calls: the next same-size call's run is enqueued behind this "
-                    "one (its jumps beside these generators, its generators beside this encode) and used only if "
-                    "torch's generator is untouched.  fused_*: the generator kernel quantizes with its own draws "
-                    "(gc_qsgd_quantize_mt19937, no draw buffer) + lane pack"}
-        del draws
+    if "reduce" in legs:
+        out.update(reduce_legs(torch, dist, codec, step, words, dec, norm, n, bits, world, lanes, K, dev))
+    del dec
+    if "torch" in legs:
+        out["torch_parity_mode"] = torch_mode_leg(torch, np, gcodec, codec, x, n, bits, words, lanes, dev, gen)
+    if "pcie" in legs:
         # PCIe-inclusive: the reference's path starts and ends in host memory
         out["pcie_inclusive"] = pcie_inclusive(torch, codec, gen, x, n, bits, world, lanes, K)
-
-
-    if not args.no_extras:
-        out["configs"] = other_configs(torch, dist, gcodec, codec, dev, world, rank, K)
+    cfg = other_configs(torch, dist, gcodec, codec, dev, world, rank, K, legs, args.n5)
+    if cfg:
+        out["configs"] = cfg
+    if "packers" in legs:
+        out["packers"] = packers_leg(torch, gcodec, codec, dev, gen, rank)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(n, bits, args.cpu_seconds)
@@ -871,4 +1076,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

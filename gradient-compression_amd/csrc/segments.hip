@@ -181,6 +181,21 @@ static_assert(sizeof(gc_seg) == sizeof(SegRec), "gc_seg / SegRec layout");
 
 extern "C" {
 
+uint32_t gc_segments_sizes_hash(const uint64_t *sizes, uint64_t count)
+{
+    uint32_t h = 2166136261u;
+    auto mix = [&h](uint64_t v) {
+        for (int i = 0; i < 8; ++i, v >>= 8) {
+            h ^= (uint32_t)(v & 0xffu);
+            h *= 16777619u;
+        }
+    };
+    mix(count);
+    for (uint64_t i = 0; sizes && i < count; ++i)
+        mix(sizes[i]);
+    return h ? h : 1u;
+}
+
 uint64_t gc_segments_chunks(uint64_t n, uint32_t chunk_shift)
 {
     if (chunk_shift < 4 || chunk_shift > 30)
@@ -261,6 +276,9 @@ int gc_segments_copy(const gc_segments *src, const gc_segments *dst, float alpha
         return rc;
     GC_REQUIRE(src->count == dst->count, "gc_segments_copy: %llu vs %llu tensors", (unsigned long long)src->count,
                (unsigned long long)dst->count);
+    GC_REQUIRE(src->sizes_hash == 0 || dst->sizes_hash == 0 || src->sizes_hash == dst->sizes_hash,
+               "gc_segments_copy: the two tensor lists have different sizes (hash %08x vs %08x)", src->sizes_hash,
+               dst->sizes_hash);
     const uint64_t n = src->n;
     if (n == 0)
         return GC_OK;

@@ -73,7 +73,7 @@ class gc_segments(C.Structure):
         ("seg", C.c_void_p),
         ("chunk_seg", C.c_void_p),
         ("chunk_shift", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("sizes_hash", C.c_uint32),
     ]
 
 
@@ -103,6 +103,7 @@ SIGNATURES = {
     "gc_lane_pack": (C.c_int, [P, u32, LANESP, P, P]),
     "gc_lane_unpack": (C.c_int, [P, LANESP, P, P]),
     "gc_segments_chunks": (u64, [u64, u32]),
+    "gc_segments_sizes_hash": (u32, [P, u64]),
     "gc_segments_plan": (C.c_int, [P, P, u64, u32, P, P, u64, P]),
     "gc_segments_flatten_absmax": (C.c_int, [SEGSP, P, P, P, P]),
     "gc_segments_scatter": (C.c_int, [P, f32, SEGSP, P]),

@@ -434,7 +434,9 @@ class Segments:
         self.key = Segments.key_of(tensors)
         self._seg = torch.from_numpy(seg_host.view(np.int64)).to(dev)
         self._chunk = torch.from_numpy(chunk_host.view(np.int32)).to(dev)
-        self.struct = _lib.gc_segments(count, n, self._seg.data_ptr(), self._chunk.data_ptr(), chunk_shift, 0)
+        self.sizes_hash = int(lib.gc_segments_sizes_hash(sizes.ctypes.data_as(C.c_void_p), count))
+        self.struct = _lib.gc_segments(count, n, self._seg.data_ptr(), self._chunk.data_ptr(), chunk_shift,
+                                       self.sizes_hash)
 
     @staticmethod
     def key_of(tensors):
@@ -743,7 +745,7 @@ def mt19937_seed_state(seed: int) -> np.ndarray:
     return st
 
 
-_MT_TABLE = {}  # (device index, J) -> (int32 tensor [gens * 624], gens): jump coefficients of generators 1..gens
+_MT_TABLE = {}  # (device index, J) -> (int32 tensor [gens * 624], gens, ready event): jump coefficients of generators 1..gens
 _MT_WS = {}     # (device index, stream) -> workspace tensor
 MT_MAX_GENERATORS = 1024
 
@@ -758,23 +760,30 @@ def mt_generator_draws(count: int) -> int:
     return 624 * max(1, -(-count // (624 * g)))
 
 
-def _mt_jump_table(dev, gens: int, J: int = _lib.GC_MT_JUMP_DRAWS):
+def _mt_jump_table(dev, gens: int, J: int = _lib.GC_MT_JUMP_DRAWS, stream=None):
     """Device jump table covering generators 1..gens for generators of J draws
     (host-computed once per process and J, grown geometrically; it depends
-    only on J and the generator index, not on the seed)."""
+    only on J and the generator index, not on the seed) -> (table, gens).
+
+    The table is (re)built on the caller's current stream (the upload is
+    synchronous, the growth's torch.cat is a kernel); `stream` (default: the
+    current stream) is made to wait for that build, so a table grown on one
+    stream is never read unwritten by kernels on another."""
     key = (dev.index, J)
     cur = _MT_TABLE.get(key)
     have = cur[1] if cur is not None else 0
-    if have >= gens:
-        return cur
-    total = max(gens, 2 * have, 16)
-    host = np.empty((total - have) * 624, dtype=np.uint32)
-    check(_lib.load().gc_mt19937_jump_table_j(J, have + 1, total - have, host.ctypes.data_as(C.c_void_p)),
-          "gc_mt19937_jump_table")
-    part = torch.from_numpy(host.view(np.int32)).to(dev)
-    table = part if cur is None else torch.cat([cur[0], part])
-    _MT_TABLE[key] = (table, total)
-    return _MT_TABLE[key]
+    if have < gens:
+        total = max(gens, 2 * have, 16)
+        host = np.empty((total - have) * 624, dtype=np.uint32)
+        check(_lib.load().gc_mt19937_jump_table_j(J, have + 1, total - have, host.ctypes.data_as(C.c_void_p)),
+              "gc_mt19937_jump_table")
+        part = torch.from_numpy(host.view(np.int32)).to(dev)
+        table = part if cur is None else torch.cat([cur[0], part])
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(dev))
+        cur = _MT_TABLE[key] = (table, total, ready)
+    (stream or torch.cuda.current_stream(dev)).wait_event(cur[2])
+    return cur[0], cur[1]
 
 
 def mt19937_generate(state_dev: torch.Tensor, count: int, out=None, parallel: bool = True,
@@ -814,16 +823,20 @@ def _mt_ws(dev, st, count: int, J: int) -> torch.Tensor:
 _MT_PIN = {}  # device index -> {path: (pinned state in, pinned states out, device state)}: 625 int32 each
 
 
-def _mt_bufs(device, path: str = "draws"):
+def _mt_bufs(device, path: str = "draws", stream=None):
     """Per device and path ("draws": mt19937_draws, two out slots for its
     speculative runs; "fused": the generator-quantize path): separate buffers,
-    so a run still queued on one path never writes what the other reads."""
+    so a run still queued on one path never writes what the other reads.  The
+    device state is allocated on `stream`, the stream that writes it (the
+    caching allocator then never hands it a block whose last user is still
+    queued on another stream)."""
     d = _MT_PIN.setdefault(device.index, {})
     b = d.get(path)
     if b is None:
-        b = d[path] = (torch.empty(625, dtype=torch.int32).pin_memory(),
-                       [torch.empty(625, dtype=torch.int32).pin_memory() for _ in range(2)],
-                       torch.empty(625, dtype=torch.int32, device=device))
+        with torch.cuda.stream(stream or torch.cuda.current_stream(device)):
+            b = d[path] = (torch.empty(625, dtype=torch.int32).pin_memory(),
+                           [torch.empty(625, dtype=torch.int32).pin_memory() for _ in range(2)],
+                           torch.empty(625, dtype=torch.int32, device=device))
     return b
 
 
@@ -905,7 +918,11 @@ _MT_SPEC = {}  # device index -> the speculative run of the next same-size call
 _MT_END = {}   # (device index, end block B) -> device coefficients of x^(624 B - 1) mod P
 _MT_WSS = {}   # (device index, slot) -> workspace of the runs in that slot
 _MT_BUSY = {}  # (device index, slot) -> event after the last generators that read the slot's workspace
+_MT_PREV = {}  # device index -> the count of the last mt19937_draws call
 MT_SPECULATE = True  # generate the draws of the next same-size torch-mode call ahead (mt19937_draws)
+# a speculative run holds 4 * count bytes of draws + one generator workspace on the device until the
+# next call; it is started only after two calls in a row of the same count, and never above this count
+MT_SPECULATE_MAX_DRAWS = 1 << 30
 MT_WAIT_NEXT_JUMPS = False  # consumers also wait for the speculative run's jumps (mt19937_draws)
 
 
@@ -940,7 +957,10 @@ def _mt_end_coef(dev, block: int):
     return t
 
 
-def _mt_ws_slot(dev, slot: int, count: int, J: int) -> torch.Tensor:
+def _mt_ws_slot(dev, slot: int, count: int, J: int, js) -> torch.Tensor:
+    """The workspace of a slot's runs, allocated on the jump stream js that
+    writes it (its generators on the other side stream read it after js's
+    phase-1 event, and record_stream keeps it alive for them)."""
     need = int(_lib.load().gc_mt19937_workspace_size_j(count, J))
     key = (dev.index, slot)
     ws = _MT_WSS.get(key)
@@ -948,7 +968,10 @@ def _mt_ws_slot(dev, slot: int, count: int, J: int) -> torch.Tensor:
         busy = _MT_BUSY.get(key)
         if busy is not None:
             busy.synchronize()  # the old buffer may still be read by queued generators
-        ws = _MT_WSS[key] = torch.empty(need, dtype=torch.uint8, device=dev)
+        _MT_WSS.pop(key, None)
+        with torch.cuda.stream(js):
+            ws = _MT_WSS[key] = torch.empty(need, dtype=torch.uint8, device=dev)
+        ws.record_stream(_mt_side(dev)[1])
     return ws
 
 
@@ -966,11 +989,11 @@ def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int) -> _MtRun:
     phase 2 on the generator stream, after phase 1: the draws."""
     J = mt_generator_draws(count)
     gens = -(-count // J)
-    table, tgens = _mt_jump_table(dev, gens - 1, J) if gens > 1 else (None, 0)
+    js, gs = _mt_side(dev)
+    table, tgens = _mt_jump_table(dev, gens - 1, J, stream=js) if gens > 1 else (None, 0)
     block = (idx + count - 1) // 624
     end = _mt_end_coef(dev, block)
-    js, gs = _mt_side(dev)
-    ws = _mt_ws_slot(dev, slot, count, J)
+    ws = _mt_ws_slot(dev, slot, count, J, js)
     busy = _MT_BUSY.get((dev.index, slot))
     lib = _lib.load()
     run = _MtRun()
@@ -1025,9 +1048,11 @@ def mt19937_draws(count: int, device) -> torch.Tensor:
     if device.index is None:
         device = torch.device("cuda", torch.cuda.current_device())
     words, idx = torch_mt_state()
-    hin, hout, dst = _mt_bufs(device)
-    cur = torch.cuda.current_stream(device)
     js, _ = _mt_side(device)
+    hin, hout, dst = _mt_bufs(device, "draws", stream=js)
+    cur = torch.cuda.current_stream(device)
+    repeat = _MT_PREV.get(device.index) == count
+    _MT_PREV[device.index] = count
     last = _MT_LAST.get(device.index)
     untouched = last is not None and last[1] == idx and np.array_equal(last[0], words)
     spec = _MT_SPEC.pop(device.index, None)
@@ -1045,7 +1070,8 @@ def mt19937_draws(count: int, device) -> torch.Tensor:
                 h[624] = idx
                 dst.copy_(hin, non_blocking=True)
         run = _mt_enqueue(device, dst, count, int(idx), hout, spec.slot ^ 1 if spec is not None else 0)
-    nxt = _mt_enqueue(device, dst, count, run.idx_end, hout, run.slot ^ 1) if MT_SPECULATE else None
+    spec_ok = MT_SPECULATE and repeat and count <= MT_SPECULATE_MAX_DRAWS
+    nxt = _mt_enqueue(device, dst, count, run.idx_end, hout, run.slot ^ 1) if spec_ok else None
     cur.wait_event(run.done)
     if nxt is not None and MT_WAIT_NEXT_JUMPS:
         cur.wait_event(nxt.p1)
@@ -1058,6 +1084,26 @@ def mt19937_draws(count: int, device) -> torch.Tensor:
     set_torch_mt_state(w2, i2)
     _MT_LAST[device.index] = (w2, i2)
     return run.out
+
+
+def mt_release(device=None):
+    """Drop the torch-mode state kept between calls on `device` (all devices
+    if None): the speculative run (4 * count bytes of draws), the generator
+    workspaces and the device state buffers.  Called when a generator leaves
+    torch mode; the next torch-mode call starts from torch's state again."""
+    keys = [device.index] if device is not None else sorted({k for k in _MT_SPEC} | {k[0] for k in _MT_WSS}
+                                                               | set(_MT_PIN) | set(_MT_LAST))
+    for d in keys:
+        for k in [k for k in _MT_BUSY if k[0] == d]:
+            _MT_BUSY.pop(k).synchronize()  # queued generators may still read the workspaces
+        spec = _MT_SPEC.pop(d, None)
+        if spec is not None:
+            spec.done.synchronize()
+        for k in [k for k in _MT_WSS if k[0] == d]:
+            del _MT_WSS[k]
+        _MT_PIN.pop(d, None)
+        _MT_LAST.pop(d, None)
+        _MT_PREV.pop(d, None)
 
 
 # ---------------------------------------------------------------------------
@@ -1092,24 +1138,54 @@ def _g4_result(res: torch.Tensor, what: str) -> int:
     return count
 
 
+class Greedy4Device:
+    """Device greedy-4 packing of buckets of one size with the buffers
+    allocated once: pack() / unpack() only enqueue (no allocation, no host
+    sync); result() reads the (count, status) pair back (one 16-byte D2H)."""
+
+    def __init__(self, n: int, device, unpack_words: int | None = None):
+        lib = _lib.load()
+        self.device = torch.device(device)
+        self.n = int(n)
+        self.cap = self.n // 3 + 2
+        self.words = torch.empty(self.cap, dtype=torch.int32, device=self.device)
+        nw = self.cap if unpack_words is None else int(unpack_words)
+        self.ucap = max(15 * nw, 1)
+        self.values = torch.empty(self.ucap, dtype=torch.int32, device=self.device)
+        ws = max(int(lib.gc_greedy4_workspace_size(self.n)), int(lib.gc_greedy4_unpack_workspace_size(nw)))
+        self.ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
+        self.res = torch.zeros(2, dtype=torch.int64, device=self.device)
+
+    def pack(self, a: torch.Tensor):
+        """a: int32 [n] on the device -> self.words (count via result())."""
+        assert a.dtype == torch.int32 and a.numel() == self.n and a.is_contiguous()
+        check(_lib.load().gc_greedy4_pack_device(_p(a), self.n, _p(self.words), self.cap, _p(self.res),
+                                                 C.c_void_p(self.res.data_ptr() + 8), _p(self.ws),
+                                                 _stream(self.device)), "gc_greedy4_pack_device")
+
+    def unpack(self, w: torch.Tensor):
+        """w: int32 words on the device -> self.values (count via result())."""
+        assert w.dtype == torch.int32 and w.is_contiguous() and 15 * w.numel() <= self.ucap
+        check(_lib.load().gc_greedy4_unpack_device(_p(w), w.numel(), _p(self.values), self.ucap, _p(self.res),
+                                                   C.c_void_p(self.res.data_ptr() + 8), _p(self.ws),
+                                                   _stream(self.device)), "gc_greedy4_unpack_device")
+
+    def result(self, what: str = "greedy4") -> int:
+        return _g4_result(self.res, what)
+
+
 def greedy4_pack(src: torch.Tensor) -> torch.Tensor:
     """The reference's greedy 4-mode format (extensions/Extension CPU/bitpacking.cpp:5-124).
     Device tensors: HIP list-ranking packer (gc_greedy4_pack_device); host
     tensors: the host packer, like the reference's CPU extension."""
     lib = _lib.load()
     if src.is_cuda:
-        dev = _dev(src)
         a = src.detach().contiguous().view(-1)
         if a.dtype != torch.int32:
             a = a.to(torch.int32)
-        n = a.numel()
-        cap = n // 3 + 2
-        out = torch.empty(cap, dtype=torch.int32, device=dev)
-        ws = torch.empty(int(lib.gc_greedy4_workspace_size(n)), dtype=torch.uint8, device=dev)
-        res = torch.zeros(2, dtype=torch.int64, device=dev)
-        check(lib.gc_greedy4_pack_device(_p(a), n, _p(out), cap, _p(res), C.c_void_p(res.data_ptr() + 8), _p(ws),
-                                         _stream(dev)), "gc_greedy4_pack_device")
-        return out[:_g4_result(res, "greedy4_pack")]
+        pk = Greedy4Device(a.numel(), _dev(a), unpack_words=0)
+        pk.pack(a)
+        return pk.words[:pk.result("greedy4_pack")]
     a = np.ascontiguousarray(src.detach().numpy().astype(np.int32, copy=False)).reshape(-1)
     out = np.empty(a.size + 1, dtype=np.int32)
     nw = check(lib.gc_greedy4_pack(a.ctypes.data_as(C.c_void_p), a.size, out.ctypes.data_as(C.c_void_p),

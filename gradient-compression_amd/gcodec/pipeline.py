@@ -69,11 +69,19 @@ class ChunkedQSGDAllReduce:
             return dist.all_reduce(words, group=self.group, async_op=True)
         return None
 
-    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None, _trace: dict | None = None) -> torch.Tensor:
         if out is None:
             out = torch.empty_like(x)
         W = self.world
         compute = torch.cuda.current_stream(self.device)
+
+        def mark(key, stream):  # timing events of trace(); nothing when not tracing
+            if _trace is not None:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(stream)
+                _trace.setdefault(key, []).append(e)
+
+        mark("start", compute)
         self.codec.absmax(x, out=self.norm)
         self._max(self.norm)
         norm_ready = torch.cuda.Event()
@@ -82,17 +90,47 @@ class ChunkedQSGDAllReduce:
         for (s, e), ln, wd in zip(self.bounds, self.lanes, self.words):
             rng = self.gen.reserve(e - s, 1, device=self.device, backend=self.codec)
             self.codec.qsgd_encode(x[s:e], self.norm, self.bits, rng, W, out=wd, lanes=ln)
+            mark("encode_end", compute)
             work = self._reduce(wd)
             if work is None:
                 encoded = torch.cuda.Event()
                 encoded.record(compute)
+            if _trace is not None:  # a probe stream that waits for this chunk's SUM only
+                with torch.cuda.stream(_trace["probe"]):
+                    if work is not None:
+                        work.wait()
+                    else:
+                        _trace["probe"].wait_event(encoded)
+                    mark("sum_end", _trace["probe"])
             with torch.cuda.stream(self.dec_stream):
                 if work is not None:
                     work.wait()  # the decode stream waits for this chunk's RCCL SUM; the host does not block
                 else:
                     self.dec_stream.wait_event(encoded)
+                mark("decode_start", self.dec_stream)
                 self.codec.qsgd_decode(wd, e - s, self.norm, self.bits, W, 1.0 / W, out=out[s:e], lanes=ln)
+                mark("decode_end", self.dec_stream)
         compute.wait_stream(self.dec_stream)
         for t in [x, out, self.norm, *self.words]:
             t.record_stream(self.dec_stream)
         return out
+
+    def trace(self, x: torch.Tensor, out: torch.Tensor | None = None) -> dict:
+        """One call with HIP timing events on every stream it uses: per chunk
+        the end of its encode, of its SUM (seen from a probe stream that waits
+        for that chunk's collective only), and the start / end of its decode,
+        in ms from the call's start.  `decode_overlaps_next_sum` is the
+        evidence that the pipeline overlaps: decode(c) started before SUM(c+1)
+        ended, for every c."""
+        torch.cuda.synchronize(self.device)
+        tr = {"probe": torch.cuda.Stream(self.device)}
+        self(x, out, _trace=tr)
+        torch.cuda.synchronize(self.device)
+        t0 = tr["start"][0]
+        ms = {k: [t0.elapsed_time(e) for e in tr[k]]
+              for k in ("encode_end", "sum_end", "decode_start", "decode_end")}
+        C = len(self.bounds)
+        started = [ms["decode_start"][c] < ms["sum_end"][c + 1] for c in range(C - 1)]
+        ended = [ms["decode_end"][c] < ms["sum_end"][c + 1] for c in range(C - 1)]
+        return {"chunks": C, "ms": ms, "decode_overlaps_next_sum": bool(started) and all(started),
+                "decode_c_started_before_sum_c1_ended": started, "decode_c_ended_before_sum_c1_ended": ended}

@@ -97,6 +97,10 @@ class Generator:
     def set_mode(self, mode: str):
         if mode not in ("philox", "torch"):
             raise ValueError("rng mode must be 'philox' or 'torch'")
+        if getattr(self, "mode", None) == "torch" and mode != "torch":
+            from . import codec
+
+            codec.mt_release()  # the speculative draws and workspaces torch mode kept on the device
         self.mode = mode
 
     def manual_seed(self, seed: int):

@@ -239,9 +239,12 @@ struct gc_segments {
     const gc_seg *seg;         /* device, count records; a sentinel is not needed */
     const uint32_t *chunk_seg; /* device, gc_segments_chunks(n, chunk_shift) entries */
     uint32_t chunk_shift;      /* 4..30 */
-    uint32_t reserved;         /* 0 */
+    uint32_t sizes_hash;       /* gc_segments_sizes_hash of the tensor sizes, or 0 (unknown) */
 };
 uint64_t gc_segments_chunks(uint64_t n, uint32_t chunk_shift);
+/* a nonzero 32-bit hash of the per-tensor sizes (FNV-1a over the count and each size):
+ * calls that pair two tables (gc_segments_copy) refuse two nonzero hashes that differ */
+uint32_t gc_segments_sizes_hash(const uint64_t *sizes, uint64_t count);
 /* host: (sizes[count], device ptrs[count]) -> seg[count], chunk_seg[chunk_capacity >=
  * gc_segments_chunks(n, chunk_shift)] (host buffers to upload); *n_out = total elements */
 int gc_segments_plan(const uint64_t *sizes, float *const *ptrs, uint64_t count, uint32_t chunk_shift,
@@ -254,7 +257,10 @@ int gc_segments_flatten_absmax(const gc_segments *segs, float *flat, float *norm
  * (reducer.py:543-549, 755-761); the + 0 maps -0 to +0 exactly as the reference does */
 int gc_segments_scatter(const float *flat, float alpha, const gc_segments *segs, gc_stream_t stream);
 /* dst tensor element e = RN(src tensor element e * alpha) + 0.0f for two lists of the same tensor sizes
- * (the GlobalRandK setgrad of every coordinate, reducer.py:759-761, tensor to tensor) */
+ * (the GlobalRandK setgrad of every coordinate, reducer.py:759-761, tensor to tensor).  The host
+ * checks the tensor count, the total n and, when both tables carry one, sizes_hash; per-tensor
+ * sizes that differ under equal count and n with a zero hash are undefined behaviour (the records
+ * live on the device and are not read back) */
 int gc_segments_copy(const gc_segments *src, const gc_segments *dst, float alpha, gc_stream_t stream);
 /* the GlobalRandK decode-scatter (gc_qsgd_decode with idx) into the tensors of segs:
  * element idx[i] = RN(decode_i * alpha) (reducer.py:754 + 759-761).  Like the

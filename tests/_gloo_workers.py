@@ -342,3 +342,36 @@ def rccl_path_world(rank, world, init_file, out_dir):
              ms_mask=mask.cpu().numpy().astype(np.uint8), ms_dec=mdec.cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()
+
+
+def hip_randk_vgg16_world(rank, world, init_file, out_dir, K, bits, steps):
+    """GlobalRandKMaxNormReducer (HIP codec, torch-mode RNG) on the VGG16 tensor
+    list, rank r's gradient = gen_input(seed 42 + r), gloo over CUDA tensors on
+    cuda:0: the SHA-256 of every step's grad_out (tests/golden/make_golden_big.py
+    ran the REFERENCE reducer the same way)."""
+    import hashlib
+    import json
+
+    import gcodec
+    from gcodec import shapes
+    from oracle import oracle as O
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    sizes = shapes.vgg16_sizes()
+    x = torch.from_numpy(O.gen_input(sum(sizes), seed=SEED + rank, kind=0)).to(dev)
+    gin = list(torch.split(x, sizes))
+    red = gcodec.GlobalRandKMaxNormReducer(dev, seed=SEED, K=K, quantization_level=bits,
+                                           generator=gcodec.Generator(0, "torch"))
+    res = []
+    for _ in range(steps):
+        gout = [torch.empty_like(g) for g in gin]
+        nbits = red.reduce(gin, gout)
+        torch.cuda.synchronize()
+        out = torch.cat(gout).cpu().numpy()
+        res.append({"out": hashlib.sha256(out.tobytes()).hexdigest(), "bits": int(nbits)})
+    with open(os.path.join(out_dir, f"v{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -2,6 +2,9 @@
 
 Run in the build container only (needs /root/reference, which does not exist
 on the GPU box):  python tests/golden/make_golden.py
+                  python tests/golden/make_golden.py --reducer-worlds 4,8
+(the second form writes only reducers_w4.npz / reducers_w8.npz: the six
+hot-path reducers under gloo at W = 4 and 8)
 
 It imports the reference's compressors.py / reducer.py on CPU (torch 2.10 CPU,
 the reference pins 1.7.1) and records inputs and outputs.  The fixtures are
@@ -253,6 +256,12 @@ def packer_fixtures():
 
 
 def main():
+    if "--reducer-worlds" in sys.argv:  # round 4: only the reducer fixtures at these world sizes
+        for w in (int(v) for v in sys.argv[sys.argv.index("--reducer-worlds") + 1].split(",")):
+            torch.set_num_threads(max(1, 8 // w))
+            np.savez_compressed(os.path.join(HERE, f"reducers_w{w}.npz"), **reducer_fixtures(w))
+            print("written", f"reducers_w{w}.npz", flush=True)
+        return
     torch.set_num_threads(8)
     meta = {"torch": torch.__version__, "seed": SEED, "generator": "tests/golden/make_golden.py"}
 
@@ -287,7 +296,7 @@ def main():
             cases[f"n{n}_k{K}/{k}"] = v
     np.savez_compressed(os.path.join(HERE, "randk.npz"), **cases)
 
-    # 4) Reducers under gloo, W = 1 and 2
+    # 4) Reducers under gloo, W = 1 and 2 (4 and 8: --reducer-worlds 4,8)
     for w in (1, 2):
         np.savez_compressed(os.path.join(HERE, f"reducers_w{w}.npz"), **reducer_fixtures(w))
 

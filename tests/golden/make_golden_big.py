@@ -18,8 +18,13 @@ config sizes and records digests only (the arrays are 0.1-1 GB each):
             from the end -> gather -> norm -> compress -> decompress) for the
             first two pops (8,266 then 10,000 indices; the draws continue),
             and the reference GlobalRandKMaxNormReducer itself under a gloo
-            W = 1 group on the VGG16 tensor list for the same two steps
+            group on the VGG16 tensor list for the same two steps, at W = 1
+            and (round 4) W = 2, 4, 8 (rank r's gradient: gen_input seed
+            42 + r, so rank 0 holds the W = 1 input)
                                                      reducer.py:697-766
+
+    python tests/golden/make_golden_big.py --only randk_reducer_k10000_vgg16_w4,...
+regenerates the named digests only and keeps the others.
 
 Inputs are oracle.gen_input (libm-free integer formula): numpy, C and HIP
 regenerate the identical x, so only digests are committed.
@@ -138,7 +143,7 @@ def _randk_reducer_worker(rank, world, init_file, out_file, K, bits, steps):
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     sizes = vgg16_sizes()
     n = sum(sizes)
-    x = torch.from_numpy(oracle.gen_input(n, seed=SEED, kind=0))
+    x = torch.from_numpy(oracle.gen_input(n, seed=SEED + rank, kind=0))
     gin = list(torch.split(x, sizes))
     red = reducer_mod.GlobalRandKMaxNormReducer(CPU, _NoTimer(), SEED, K=K, quantization_level=bits)
     res = []
@@ -146,22 +151,31 @@ def _randk_reducer_worker(rank, world, init_file, out_file, K, bits, steps):
         gout = [torch.empty_like(g) for g in gin]
         bits_sent = red.reduce(gin, gout)
         res.append(dict(out=sha(torch.cat(gout)), bits=int(bits_sent)))
-    with open(out_file, "w") as f:
+    with open(f"{out_file}.{rank}", "w") as f:
         json.dump(res, f)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def randk_reducer_digest(K, bits, steps=2):
+def randk_reducer_digest(K, bits, steps=2, world=1):
     import torch.multiprocessing as mp
 
+    torch.set_num_threads(max(1, 8 // world))
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "r.json")
-        mp.spawn(_randk_reducer_worker, args=(1, os.path.join(td, "init"), out, K, bits, steps), nprocs=1, join=True)
-        with open(out) as f:
-            res = json.load(f)
+        mp.spawn(_randk_reducer_worker, args=(world, os.path.join(td, "init"), out, K, bits, steps), nprocs=world,
+                 join=True)
+        ranks = []
+        for r in range(world):
+            with open(f"{out}.{r}") as f:
+                ranks.append(json.load(f))
+    torch.set_num_threads(8)
     sizes = vgg16_sizes()
-    return dict(n=sum(sizes), tensors=len(sizes), kind=0, K=K, bits=bits, world=1, steps=res)
+    d = dict(n=sum(sizes), tensors=len(sizes), kind=0, K=K, bits=bits, world=world, steps=ranks[0])
+    if world > 1:
+        d["input_seeds"] = [SEED + r for r in range(world)]
+        d["ranks"] = ranks
+    return d
 
 
 def main():
@@ -176,8 +190,19 @@ def main():
         ("ms_2_4_resnet50", lambda: ms_digest(23_520_842, (2, 4))),
         ("randk_k10000_vgg16", lambda: randk_digest(14_728_266, 10_000, 4)),
         ("randk_reducer_k10000_vgg16", lambda: randk_reducer_digest(10_000, 4)),
+        ("randk_reducer_k10000_vgg16_w2", lambda: randk_reducer_digest(10_000, 4, world=2)),
+        ("randk_reducer_k10000_vgg16_w4", lambda: randk_reducer_digest(10_000, 4, world=4)),
+        ("randk_reducer_k10000_vgg16_w8", lambda: randk_reducer_digest(10_000, 4, world=8)),
     ]
+    only = None
+    if "--only" in sys.argv:
+        only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
+        with open(os.path.join(HERE, "golden_big.json")) as f:
+            old = json.load(f)
+        d.update(old["digests"])
     for name, fn in jobs:
+        if only is not None and name not in only:
+            continue
         t0 = time.time()
         d[name] = fn()
         print(f"{name}: {time.time() - t0:.1f} s", flush=True)

@@ -183,6 +183,25 @@ def test_segments_plan(shift):
     assert lib.gc_segments_chunks(10, 3) == 0
 
 
+def test_segments_copy_refuses_different_sizes():
+    """two tables with the same count and n but different
+    per-tensor sizes are refused on the host (sizes_hash), before any launch."""
+    from gcodec import _lib
+
+    lib = _lib.load()
+
+    def h(sizes):
+        a = np.array(sizes, dtype=np.uint64)
+        return int(lib.gc_segments_sizes_hash(a.ctypes.data_as(C.c_void_p), len(sizes)))
+
+    assert h([3, 5]) != h([5, 3]) and h([3, 5]) == h([3, 5]) and h([]) != 0
+    fake = C.c_void_p(0x1000)
+    a = _lib.gc_segments(2, 8, fake, fake, 12, h([3, 5]))
+    b = _lib.gc_segments(2, 8, fake, fake, 12, h([5, 3]))
+    assert lib.gc_segments_copy(C.byref(a), C.byref(b), 1.0, None) == _lib.GC_EINVAL
+    assert b"different sizes" in lib.gc_last_error()
+
+
 def test_ms_cache_bytes():
     """q cache cells (gc_ms_cache_bytes, host only): count * bit_length(2 qmax)
     bits in 1 or 2 bytes on the dense wave-split kernels (2-3 levels of <= 24 bits)."""

@@ -51,3 +51,33 @@ def test_bench_two_ranks_gloo_pipelined():
     d = _line(r.stdout)
     _check(d, 2)
     assert d["config"]["pipelining"] and d["collectives"] == "gloo"
+
+
+SCALE_ARGS = ["--numel", "2000000", "--steps", "3", "--warmup", "1", "--settle", "0", "--cpu-seconds", "0",
+              "--legs", "reduce,config5", "--n5", "2000000"]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_plain_bench_gpus_n_launches_ranks(world):
+    """The driver's SCALE form: plain `python bench.py --gpus N` (no torchrun,
+    no WORLD_SIZE) must start N ranks itself and report them, with the
+    process group's own evidence (ranks share cuda:0 over gloo here; on the
+    8-GPU node the same command runs one rank per GPU over RCCL)."""
+    env = dict(os.environ, GC_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), *SCALE_ARGS], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=115)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == world and d["config"]["parallelism"] == f"dp{world}"
+    assert d["pipelined_issue_bit_identical"] is True
+    pg = d["process_group"]
+    assert pg["world_size"] == world and len(pg["ranks"]) == world and pg["backend"] == "gloo"
+    assert sorted(x["rank"] for x in pg["ranks"]) == list(range(world))
+    assert d["reduce_path"]["ms_per_step"] > 0
+    if world >= 4:
+        assert d["reduce_path_2x_nodes"]["bit_identical_to_flat"] is True
+    ov = d["configs"]["config5_1b_8bit_chunked"]["overlap"]
+    assert ov["chunks"] == 8 and len(ov["ms"]["sum_end"]) == 8
+    assert all(a <= b for a, b in zip(ov["ms"]["decode_start"], ov["ms"]["decode_end"]))

@@ -1,6 +1,7 @@
-"""The HIP reducers at W = 1 and 2 on the GPU box (two processes on cuda:0,
-gloo over CUDA tensors), bit-compared with the REFERENCE reducers' outputs
-(tests/golden/reducers_w*.npz).  RCCL needs one GPU per rank, so the
+"""The HIP reducers at W = 1, 2, 4 and 8 on the GPU box (W processes on
+cuda:0, gloo over CUDA tensors), bit-compared with the REFERENCE reducers'
+outputs (tests/golden/reducers_w*.npz; golden_big.json for the VGG16
+GlobalRandK reducer at W = 2 / 4 / 8).  RCCL needs one GPU per rank, so the
 collective here is gloo; the codec calls, stream handling and lane sizing
 for W are the product path."""
 import os
@@ -36,7 +37,7 @@ def _check_vs_reference(world, td):
                 assert i > 0
 
 
-@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_hip_reducers_match_reference(world):
     fixture = os.path.join(GOLD, f"reducers_w{world}.npz")
     with tempfile.TemporaryDirectory() as td:
@@ -125,3 +126,24 @@ def test_single_bucket_hook_matches_reference_reducers_gpu(world):
         mp.spawn(W.hook_vs_reference, args=(world, os.path.join(td, "init"), fixture, td, True), nprocs=world,
                  join=True)
         check_hook_vs_reference(world, td)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_randk_reducer_vgg16_multirank_vs_reference(world):
+    """Config 4 at its world sizes: GlobalRandKMaxNormReducer, K = 10,000,
+    4-bit, the VGG16 tensor list, W ranks with different gradients, two steps:
+    every rank's grad_out equals the REFERENCE reducer's (SHA-256 from
+    make_golden_big.py, the reference run under gloo at the same W)."""
+    import json
+
+    big = json.load(open(os.path.join(GOLD, "golden_big.json")))["digests"]
+    meta = big[f"randk_reducer_k10000_vgg16_w{world}"]
+    assert meta["world"] == world
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(W.hip_randk_vgg16_world, args=(world, os.path.join(td, "init"), td, meta["K"], meta["bits"],
+                                                len(meta["steps"])), nprocs=world, join=True)
+        for r in range(world):
+            got = json.load(open(os.path.join(td, f"v{r}.json")))
+            for s, (g, ref) in enumerate(zip(got, meta["ranks"][r])):
+                assert g["out"] == ref["out"], f"rank {r} step {s}"
+                assert 0 < g["bits"] <= ref["bits"]

@@ -119,3 +119,36 @@ def test_split_end_state_vs_serial_stream(idx, count):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), np.asarray(ref, np.uint32))
     # the state is left alone by phase 2
     assert np.array_equal(state.cpu().numpy().view(np.uint32), got)
+
+
+def test_table_growth_while_caller_stream_busy():
+    """the jump table grows (torch.cat) on the caller's stream while
+    the draws run on the side streams.  With the caller's stream held busy by a
+    sleep kernel, the side streams must still wait for the grown table: the
+    draws equal the serial stream's."""
+    codec.mt_release()
+    codec._MT_TABLE.clear()
+    torch.manual_seed(7)
+    for cnt, hold in ((1_000_003, 0), (30_000_001, 50_000_000), (30_000_001, 0), (60_000_017, 50_000_000)):
+        ref, w2, i2 = _oracle_next(cnt)
+        if hold:
+            torch.cuda._sleep(hold)  # the caller's stream stays busy while the table grows
+        got = codec.mt19937_draws(cnt, DEV)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint32), ref), cnt
+        words, idx = torch_mt_state()
+        assert idx == i2 and np.array_equal(words, w2), cnt
+
+
+def test_release_drops_speculation_and_stays_exact():
+    """mt_release (called when a generator leaves torch mode) drops the
+    speculative run and workspaces; the next calls start from torch's state."""
+    torch.manual_seed(11)
+    for i in range(5):
+        if i == 3:
+            codec.mt_release(DEV)
+            assert DEV.index not in codec._MT_SPEC
+        ref, _, _ = _oracle_next(200_003)
+        got = codec.mt19937_draws(200_003, DEV)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint32), ref), i

@@ -1,4 +1,4 @@
-"""Summarise the SQ / LDS counter passes of tools/profile_r02.sh (prof_<tag>_k)
+"""Summarise the SQ / LDS counter passes of tools/gpu.sh kprof (prof_<tag>_k)
 into profiles/<tag>_k_sq.json: per kernel, the median per launch of every
 counter, and the wait / issue fractions of SQ_WAVE_CYCLES."""
 import csv

@@ -1,4 +1,4 @@
-"""Summarise a tools/profile.sh run into profiles/:
+"""Summarise a tools/gpu.sh driver / pmc run into profiles/:
   profiles/<tag>_kernel_stats.csv   (rocprofv3 --stats, copied)
   profiles/<tag>_pmc.json           (per-kernel HBM bytes per launch)
   profiles/pmc_traffic.json         (latest, read by bench.py for roofline.traffic)
@@ -61,7 +61,7 @@ def main(tag, n=100_000_000, bits=4):
         f, w = fetch.get(k), write.get(k)
         out["kernels"][k] = {"fetch_size_kib_raw": f, "write_size_kib": w,
                              "hbm_bytes_per_launch": None if f is None or w is None else (2 * f + w) * 1024}
-    # the per-kernel workload of tools/prof_kernels.py (tools/profile_r02.sh -> prof_<tag>_k)
+    # the per-kernel workload of tools/prof_kernels.py (tools/gpu.sh kprof -> prof_<tag>_k)
     if os.path.isdir(os.path.join(ROOT, "gpurun_out", f"prof_{tag}_k")):
         kf, kw = counter(f"{tag}_k", "fetch", "FETCH_SIZE"), counter(f"{tag}_k", "write", "WRITE_SIZE")
         kstats = glob.glob(os.path.join(ROOT, "gpurun_out", f"prof_{tag}_k", "trace", "**", "*kernel_stats.csv"),

@@ -8,7 +8,7 @@ Steady state: a clock settle first (SETTLE seconds of config-3 steps, as
 bench.py's --settle), and every kernel name is launched at ONE size only, so a
 kernel's rocprof average / spread describes one workload (k_absmax: the
 ResNet50 bucket; the 1e8 headline kernels are profiled over bench.py itself,
-tools/profile.sh)."""
+tools/gpu.sh pmc)."""
 import os
 import sys
 
