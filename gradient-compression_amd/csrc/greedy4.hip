@@ -8,22 +8,29 @@
 // otherwise); the next word starts at i + CNT[mode].  Values must lie in
 // [0, 255] (the reference corrupts negatives and loops forever on >= 256).
 //
-// The word starts form a chain next(i) = i + CNT[mode(i)] — list ranking, not
-// a scan.  Three phases:
-//   k_g4_chunk    per 2048-element chunk (LDS): modes, then pointer-doubling
-//                 tables nxt_k = next^(2^k); for each of the 15 possible entry
-//                 offsets (a word starting before the chunk ends at most 14
-//                 into it) binary-lift to the chunk's exit offset and count
-//                 the words -> a 15-state transition table per chunk.
-//   k_g4_group / k_g4_walk / k_g4_spread
-//                 compose the transitions of 256-chunk groups, walk the groups
-//                 from offset 0 (one thread; groups are few), then each group
-//                 walks its chunks: every chunk gets its entry offset and
-//                 output word base.
-//   k_g4_emit     per chunk: rebuild the tables, word j of the chunk starts at
-//                 next^j(entry) (binary decomposition of j over the tables),
-//                 pack it, store it at base + j.  Fully parallel.
-// Unpack: per-word element counts -> block sums -> one-block scan -> emit.
+// The word starts form a chain next(i) = i + CNT[mode(i)] from i = 0: a scan
+// whose elements are FUNCTIONS.  Cut the positions into segments of 16; a
+// word that starts in one segment ends at most 14 positions into the next, so
+// a segment maps the offset its first word starts at (0..14, or 15 = past n)
+// to the offset its chain leaves at and the words it emitted: a 16-entry
+// table, and tables compose associatively.
+//   k_g4p_tile     per 4096-element tile (256 threads x one segment): window
+//                  flags by SWAR byte tests, the segment table by a backward
+//                  recurrence held in registers (static indices only), then a
+//                  reduction tree of the 256 tables in LDS -> the tile's
+//                  table.  Also stores the values as bytes for the emit.
+//   k_g4p_group    per 256 tiles: reduction tree -> the group's table
+//   k_g4p_top      one block: walks the group tables from offset 0 (LDS) ->
+//                  each group's entry offset and word base; the total
+//   k_g4p_spread   per group: the tree again, then a down-sweep from the
+//                  group's entry -> every tile's entry offset and word base
+//   k_g4p_emit     per tile: the tile's tree again (from the bytes), a
+//                  down-sweep from its entry -> every segment's entry and
+//                  base; each thread packs its segment's words into LDS, the
+//                  block stores the tile's words coalesced.
+// HBM: src read once (4n), the bytes written and read (2n), the words written.
+// Unpack: per-word element counts -> block sums -> one-block scan -> decode
+// into LDS -> coalesced stores.
 #include "gc_device.h"
 #include "gc_host.h"
 
@@ -31,234 +38,327 @@
 
 namespace gc {
 
-constexpr int G4_CHUNK = 2048;                 // elements per chunk
-constexpr int G4_HALO = 16;                    // >= 14 values past the chunk
-constexpr int G4_LEVELS = 10;                  // 2^10 > max words per chunk (683)
-constexpr int G4_TAB = G4_CHUNK + G4_HALO;     // table entries per level
-constexpr int G4_GROUP = 256;                  // chunks per group
 constexpr unsigned G4_THREADS = 256;
+constexpr uint32_t G4_SEG = 16;                         // positions per segment (one thread)
+constexpr uint32_t G4_TILE = G4_SEG * G4_THREADS;       // 4096 positions per tile
+constexpr uint32_t G4_GROUP = 256;                      // tiles per group
+constexpr uint32_t G4_DEAD = 15;                        // table state: the chain has passed n
+constexpr uint32_t G4_TOP_CHUNK = 64;                   // group tables staged in LDS per top step
 constexpr uint32_t G4_STATUS_RANGE = 1u, G4_STATUS_NOSPC = 2u;
 
 __constant__ int c_g4_cnt[4] = {15, 7, 4, 3};
 __constant__ int c_g4_bits[4] = {2, 4, 7, 8};
 __constant__ int c_g4_top[4] = {28, 26, 23, 22};
 
-struct G4Smem {
-    uint8_t v[G4_CHUNK + 32];           // values (0-padded past n)
-    uint16_t nxt[G4_LEVELS][G4_TAB];    // next^(2^k), local indices; >= len: absorbing
+// 4 byte-threshold flags of one dword (bytes b0..b3): bit j set iff byte j has
+// a bit of `hi` set (hi = ~(lim - 1) for a power-of-two limit)
+__device__ __forceinline__ uint32_t byte_flags(uint32_t w, uint32_t hi)
+{
+    const uint32_t x = w & hi;
+    const uint32_t y = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;  // byte's top bit set iff byte != 0
+    return ((y & 0x80808080u) * 0x00204081u) >> 28;           // gather the 4 top bits
+}
+
+// table entries: exit offset (4 bits) | words << 4
+__device__ __forceinline__ uint32_t g4_compose(uint32_t a, const uint16_t *b)
+{
+    const uint32_t e = b[a & 15u];
+    return (e & 15u) | (((a >> 4) + (e >> 4)) << 4);
+}
+__device__ __forceinline__ uint32_t g4_compose32(uint32_t a, const uint32_t *b)
+{
+    const uint32_t e = b[a & 15u];
+    return (e & 15u) | (((a >> 4) + (e >> 4)) << 4);
+}
+
+struct G4Tile {
+    uint32_t v[(G4_TILE + 32) / 4];  // values as bytes (0 past n), 32-byte halo
+    uint16_t node[2 * G4_THREADS][16];  // reduction tree: leaves 256..511, root 1
 };
 
-// load chunk values + halo, compute next (level 0) and the doubling levels.
-// len = elements of the chunk that are < n.  Returns via smem.
-__device__ void g4_build(G4Smem &sm, const int32_t *__restrict__ src, uint64_t n, uint64_t start, uint32_t len,
-                         uint32_t *__restrict__ status)
+// modes of this thread's 16 positions (2 bits each) from the LDS bytes, and
+// its segment table (16 entries, exit | words << 4) by the backward recurrence
+// f[p] = 1 word + f[p + cnt(p)] (an exit past the segment: offset p + cnt - 16).
+// seg0 = global position of the segment, n = bucket size.
+__device__ __forceinline__ void g4_segment(const G4Tile &sm, uint64_t seg0, uint64_t n, uint32_t &modes,
+                                           uint32_t f[16])
 {
-    const unsigned tid = threadIdx.x;
-    bool bad = false;
-    for (uint32_t i = tid; i < G4_CHUNK + 32; i += G4_THREADS) {
-        const uint64_t g = start + i;
-        int32_t v = 0;
-        if (g < n && i < G4_CHUNK + G4_HALO) {
-            v = src[g];
-            bad |= (uint32_t)v > 255u;
-        }
-        sm.v[i] = (uint8_t)v;
+    const unsigned t = threadIdx.x;
+    const uint4 a = *reinterpret_cast<const uint4 *>(&sm.v[4 * t]);
+    const uint4 b = *reinterpret_cast<const uint4 *>(&sm.v[4 * t + 4]);
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t ge4 = 0, ge16 = 0, ge128 = 0;  // bit j: byte j of the 32 (positions seg .. seg+31)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        ge4 |= byte_flags(w[k], 0xfcfcfcfcu) << (4 * k);
+        ge16 |= byte_flags(w[k], 0xf0f0f0f0u) << (4 * k);
+        ge128 |= byte_flags(w[k], 0x80808080u) << (4 * k);
     }
-    if (bad)
+    modes = 0;
+    const uint32_t live = seg0 >= n ? 0u : (uint32_t)std::min<uint64_t>(16, n - seg0);  // positions < n
+#pragma unroll
+    for (int p = 15; p >= 0; --p) {
+        const uint32_t m = ((ge4 >> p) & 0x7fffu) == 0 ? 0u : ((ge16 >> p) & 0x7fu) == 0 ? 1u
+                                                             : ((ge128 >> p) & 0xfu) == 0 ? 2u : 3u;
+        modes |= m << (2 * p);
+        // the four possible successors (static indices): past the segment -> its offset there
+        const uint32_t s3 = p + 3 < 16 ? f[(p + 3) & 15] : (uint32_t)(p + 3 - 16);
+        const uint32_t s4 = p + 4 < 16 ? f[(p + 4) & 15] : (uint32_t)(p + 4 - 16);
+        const uint32_t s7 = p + 7 < 16 ? f[(p + 7) & 15] : (uint32_t)(p + 7 - 16);
+        const uint32_t s15v = p == 0 ? f[15] : (uint32_t)(p - 1);  // p + 15 >= 16 unless p == 0
+        const uint32_t nx = m == 0 ? s15v : m == 1 ? s7 : m == 2 ? s4 : s3;
+        f[p] = (uint32_t)p < live ? nx + 16u : G4_DEAD;
+    }
+}
+
+// reduction tree over the 256 leaves node[256 + t] -> node[1]
+__device__ __forceinline__ void g4_tree_up(G4Tile &sm)
+{
+    const unsigned t = threadIdx.x;
+#pragma unroll 1
+    for (uint32_t lvl = G4_THREADS / 2; lvl >= 1; lvl >>= 1) {
+        __syncthreads();
+        for (uint32_t k = t; k < lvl * 16; k += G4_THREADS) {
+            const uint32_t i = lvl + (k >> 4), e = k & 15u;
+            sm.node[i][e] = (uint16_t)g4_compose(sm.node[2 * i][e], sm.node[2 * i + 1]);
+        }
+    }
+    __syncthreads();
+}
+
+// load tile `tile` of the values into LDS as bytes (0 past n) + halo.
+// From int32 src (range-checked; the bytes also go to vb) or from vb.
+template <bool FROM_SRC, bool ALIGNED>
+__device__ __forceinline__ void g4_load(G4Tile &sm, const int32_t *__restrict__ src, uint8_t *__restrict__ vb,
+                                        uint64_t n, uint64_t start, uint32_t *__restrict__ status)
+{
+    const unsigned t = threadIdx.x;
+    bool bad = false;
+#pragma unroll
+    for (uint32_t j = 0; j < G4_TILE / (4 * G4_THREADS) + 1; ++j) {
+        const uint32_t q = j * G4_THREADS + t;  // dword (4 positions) of the tile
+        if (q >= (G4_TILE + 32) / 4)
+            break;
+        const uint64_t g = start + 4ull * q;
+        uint32_t packed = 0;
+        if (FROM_SRC) {
+            int4 v = make_int4(0, 0, 0, 0);
+            if (g + 4 <= n) {
+                if (ALIGNED)
+                    v = *reinterpret_cast<const int4 *>(src + g);
+                else
+                    v = make_int4(src[g], src[g + 1], src[g + 2], src[g + 3]);
+            } else if (g < n) {
+                v.x = src[g];
+                v.y = g + 1 < n ? src[g + 1] : 0;
+                v.z = g + 2 < n ? src[g + 2] : 0;
+            }
+            bad |= ((uint32_t)v.x | (uint32_t)v.y | (uint32_t)v.z | (uint32_t)v.w) > 255u;
+            packed = ((uint32_t)v.x & 0xffu) | (((uint32_t)v.y & 0xffu) << 8) | (((uint32_t)v.z & 0xffu) << 16) |
+                     ((uint32_t)v.w << 24);
+            if (q < G4_TILE / 4 && g < n)
+                *reinterpret_cast<uint32_t *>(vb + g) = packed;  // vb is padded to whole dwords
+        } else if (g < n) {
+            packed = *reinterpret_cast<const uint32_t *>(vb + g);  // zero past n (written so by k_g4p_tile)
+        }
+        sm.v[q] = packed;
+    }
+    if (FROM_SRC && bad)
         atomicOr(status, G4_STATUS_RANGE);
     __syncthreads();
-    // level 0: positions [0, G4_TAB); >= len absorbing
-    for (uint32_t i = tid; i < (uint32_t)G4_TAB; i += G4_THREADS) {
-        uint32_t nx = i;
-        if (i < len) {
-            uint32_t m15 = 0, m7 = 0, m4 = 0;
-#pragma unroll
-            for (int j = 0; j < 15; ++j) {
-                const uint32_t v = sm.v[i + j];  // i + 14 < G4_CHUNK + 32
-                m15 = max(m15, v);
-                if (j < 7)
-                    m7 = max(m7, v);
-                if (j < 4)
-                    m4 = max(m4, v);
-            }
-            const int mode = m15 < 4 ? 0 : (m7 < 16 ? 1 : (m4 < 128 ? 2 : 3));
-            nx = i + (uint32_t)c_g4_cnt[mode];
-        }
-        sm.nxt[0][i] = (uint16_t)nx;
-    }
-    __syncthreads();
-    for (int k = 1; k < G4_LEVELS; ++k) {
-        for (uint32_t i = tid; i < (uint32_t)G4_TAB; i += G4_THREADS) {
-            const uint32_t a = sm.nxt[k - 1][i];
-            sm.nxt[k][i] = a < (uint32_t)G4_TAB ? sm.nxt[k - 1][a] : (uint16_t)a;
-        }
-        __syncthreads();
-    }
 }
 
-// from local entry e (< 15): words until the chain leaves [0, len) and the
-// exit offset past len.  (exit, words) packed as words << 8 | exit.
-__device__ __forceinline__ uint32_t g4_lift(const G4Smem &sm, uint32_t e, uint32_t len)
+template <bool ALIGNED>
+__global__ __launch_bounds__(G4_THREADS) void k_g4p_tile(const int32_t *__restrict__ src, uint64_t n,
+                                                         uint8_t *__restrict__ vb, uint32_t *__restrict__ agg,
+                                                         uint32_t *__restrict__ status)
 {
-    if (e >= len)
-        return (e - len) & 0xffu;
-    uint32_t pos = e, cnt = 0;
+    __shared__ G4Tile sm;
+    const uint64_t start = (uint64_t)blockIdx.x * G4_TILE;
+    g4_load<true, ALIGNED>(sm, src, vb, n, start, status);
+    uint32_t modes, f[16];
+    g4_segment(sm, start + G4_SEG * threadIdx.x, n, modes, f);
+    (void)modes;
 #pragma unroll
-    for (int k = G4_LEVELS - 1; k >= 0; --k) {
-        const uint32_t p2 = sm.nxt[k][pos];
-        if (p2 < len) {
-            pos = p2;
-            cnt += 1u << k;
-        }
-    }
-    pos = sm.nxt[0][pos];  // the step that leaves the chunk
-    return ((cnt + 1) << 8) | ((pos - len) & 0xffu);
-}
-
-__global__ __launch_bounds__(G4_THREADS) void k_g4_chunk(const int32_t *__restrict__ src, uint64_t n,
-                                                         uint32_t *__restrict__ trans, uint32_t *__restrict__ status)
-{
-    __shared__ G4Smem sm;
-    const uint64_t c = blockIdx.x;
-    const uint64_t start = c * G4_CHUNK;
-    const uint32_t len = (uint32_t)std::min<uint64_t>(G4_CHUNK, n - start);
-    g4_build(sm, src, n, start, len, status);
+    for (int e = 0; e < 16; ++e)
+        sm.node[G4_THREADS + threadIdx.x][e] = (uint16_t)(e == 15 ? G4_DEAD : f[e]);
+    g4_tree_up(sm);
     if (threadIdx.x < 16)
-        trans[c * 16 + threadIdx.x] = threadIdx.x < 15 ? g4_lift(sm, threadIdx.x, len) : 0u;
+        agg[(uint64_t)blockIdx.x * 16 + threadIdx.x] = sm.node[1][threadIdx.x];
 }
 
-// compose the transitions of each group of G4_GROUP chunks (15 walkers)
-__global__ __launch_bounds__(G4_THREADS) void k_g4_group(const uint32_t *__restrict__ trans, uint64_t chunks,
-                                                         uint32_t *__restrict__ gtrans)
+// tables of up to 256 items (16 x u32 each) in LDS: up-sweep to node[1]
+struct G4Group {
+    uint32_t node[2 * G4_GROUP][16];
+    uint32_t st[2 * G4_GROUP];
+    uint64_t bs[2 * G4_GROUP];
+};
+
+__device__ __forceinline__ void g4_group_up(G4Group &sm, const uint32_t *__restrict__ items, uint64_t first,
+                                            uint32_t cnt)
 {
-    __shared__ uint32_t t[G4_GROUP * 16];
-    const uint64_t c0 = (uint64_t)blockIdx.x * G4_GROUP;
-    const uint32_t cnt = (uint32_t)std::min<uint64_t>(G4_GROUP, chunks - c0);
-    for (uint32_t i = threadIdx.x; i < cnt * 16; i += G4_THREADS)
-        t[i] = trans[c0 * 16 + i];
-    __syncthreads();
-    if (threadIdx.x < 16) {
-        uint32_t state = threadIdx.x, words = 0;
-        if (threadIdx.x < 15) {
-            for (uint32_t j = 0; j < cnt; ++j) {
-                const uint32_t x = t[j * 16 + state];
-                words += x >> 8;
-                state = x & 0xffu;
-            }
-        }
-        gtrans[(uint64_t)blockIdx.x * 16 + threadIdx.x] = (words << 8) | state;  // words <= 256*683 < 2^24
+    const unsigned t = threadIdx.x;
+    for (uint32_t k = t; k < G4_GROUP * 16; k += G4_THREADS) {  // leaves; past the end: identity (dead = 15)
+        const uint32_t i = k >> 4, e = k & 15u;
+        sm.node[G4_GROUP + i][e] = i < cnt ? items[(first + i) * 16 + e] : e;
     }
+#pragma unroll 1
+    for (uint32_t lvl = G4_GROUP / 2; lvl >= 1; lvl >>= 1) {
+        __syncthreads();
+        for (uint32_t k = t; k < lvl * 16; k += G4_THREADS) {
+            const uint32_t i = lvl + (k >> 4), e = k & 15u;
+            sm.node[i][e] = g4_compose32(sm.node[2 * i][e], sm.node[2 * i + 1]);
+        }
+    }
+    __syncthreads();
 }
 
-// one block: walk the groups from offset 0; group entry + word base; total
-__global__ __launch_bounds__(G4_THREADS) void k_g4_walk(const uint32_t *__restrict__ gtrans, uint64_t groups,
+__global__ __launch_bounds__(G4_THREADS) void k_g4p_group(const uint32_t *__restrict__ agg, uint64_t tiles,
+                                                          uint32_t *__restrict__ gagg)
+{
+    __shared__ G4Group sm;
+    const uint64_t first = (uint64_t)blockIdx.x * G4_GROUP;
+    g4_group_up(sm, agg, first, (uint32_t)std::min<uint64_t>(G4_GROUP, tiles - first));
+    if (threadIdx.x < 16)
+        gagg[(uint64_t)blockIdx.x * 16 + threadIdx.x] = sm.node[1][threadIdx.x];
+}
+
+// one block: the chain through the groups from offset 0 -> entries, bases, total
+__global__ __launch_bounds__(G4_THREADS) void k_g4p_top(const uint32_t *__restrict__ gagg, uint64_t groups,
                                                         uint32_t *__restrict__ gentry, uint64_t *__restrict__ gbase,
                                                         uint64_t *__restrict__ nwords, uint64_t cap,
                                                         uint32_t *__restrict__ status)
 {
-    constexpr uint32_t TILE = 1024;
-    __shared__ uint32_t t[TILE * 16];
-    __shared__ uint32_t st_state;
-    __shared__ uint64_t st_base;
-    if (threadIdx.x == 0) {
-        st_state = 0;
-        st_base = 0;
-    }
-    for (uint64_t g0 = 0; g0 < groups; g0 += TILE) {
-        const uint32_t cnt = (uint32_t)std::min<uint64_t>(TILE, groups - g0);
+    __shared__ uint32_t t16[G4_TOP_CHUNK * 16];
+    uint32_t state = 0;
+    uint64_t base = 0;
+    for (uint64_t g0 = 0; g0 < groups; g0 += G4_TOP_CHUNK) {
+        const uint32_t cnt = (uint32_t)std::min<uint64_t>(G4_TOP_CHUNK, groups - g0);
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < cnt * 16; i += G4_THREADS)
-            t[i] = gtrans[g0 * 16 + i];
+        for (uint32_t k = threadIdx.x; k < cnt * 16; k += G4_THREADS)
+            t16[k] = gagg[g0 * 16 + k];
         __syncthreads();
         if (threadIdx.x == 0) {
-            uint32_t state = st_state;
-            uint64_t base = st_base;
             for (uint32_t j = 0; j < cnt; ++j) {
                 gentry[g0 + j] = state;
                 gbase[g0 + j] = base;
-                const uint32_t x = t[j * 16 + state];
-                base += x >> 8;
-                state = x & 0xffu;
+                const uint32_t x = t16[j * 16 + state];
+                base += x >> 4;
+                state = x & 15u;
             }
-            st_state = state;
-            st_base = base;
         }
     }
-    __syncthreads();
     if (threadIdx.x == 0) {
-        *nwords = st_base;
-        if (st_base > cap)
+        *nwords = base;
+        if (base > cap)
             atomicOr(status, G4_STATUS_NOSPC);
     }
 }
 
-// per group: walk its chunks from the group entry -> chunk entry + base
-__global__ __launch_bounds__(G4_THREADS) void k_g4_spread(const uint32_t *__restrict__ trans, uint64_t chunks,
-                                                          const uint32_t *__restrict__ gentry,
-                                                          const uint64_t *__restrict__ gbase,
-                                                          uint32_t *__restrict__ centry, uint64_t *__restrict__ cbase)
+// per group: the tree again, then a down-sweep from the group's entry -> tiles
+__global__ __launch_bounds__(G4_THREADS) void k_g4p_spread(const uint32_t *__restrict__ agg, uint64_t tiles,
+                                                           const uint32_t *__restrict__ gentry,
+                                                           const uint64_t *__restrict__ gbase,
+                                                           uint32_t *__restrict__ tentry, uint64_t *__restrict__ tbase)
 {
-    __shared__ uint32_t t[G4_GROUP * 16];
-    const uint64_t c0 = (uint64_t)blockIdx.x * G4_GROUP;
-    const uint32_t cnt = (uint32_t)std::min<uint64_t>(G4_GROUP, chunks - c0);
-    for (uint32_t i = threadIdx.x; i < cnt * 16; i += G4_THREADS)
-        t[i] = trans[c0 * 16 + i];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t state = gentry[blockIdx.x];
-        uint64_t base = gbase[blockIdx.x];
-        for (uint32_t j = 0; j < cnt; ++j) {
-            centry[c0 + j] = state;
-            cbase[c0 + j] = base;
-            const uint32_t x = t[j * 16 + state];
-            base += x >> 8;
-            state = x & 0xffu;
+    __shared__ G4Group sm;
+    const uint64_t first = (uint64_t)blockIdx.x * G4_GROUP;
+    const uint32_t cnt = (uint32_t)std::min<uint64_t>(G4_GROUP, tiles - first);
+    g4_group_up(sm, agg, first, cnt);
+    const unsigned t = threadIdx.x;
+    if (t == 0) {
+        sm.st[1] = gentry[blockIdx.x];
+        sm.bs[1] = gbase[blockIdx.x];
+    }
+#pragma unroll 1
+    for (uint32_t lvl = 1; lvl < G4_GROUP; lvl <<= 1) {
+        __syncthreads();
+        if (t < lvl) {
+            const uint32_t i = lvl + t, s = sm.st[i];
+            const uint32_t e = sm.node[2 * i][s];
+            sm.st[2 * i] = s;
+            sm.bs[2 * i] = sm.bs[i];
+            sm.st[2 * i + 1] = e & 15u;
+            sm.bs[2 * i + 1] = sm.bs[i] + (e >> 4);
         }
+    }
+    __syncthreads();
+    if (t < cnt) {
+        tentry[first + t] = sm.st[G4_GROUP + t];
+        tbase[first + t] = sm.bs[G4_GROUP + t];
     }
 }
 
-__global__ __launch_bounds__(G4_THREADS) void k_g4_emit(const int32_t *__restrict__ src, uint64_t n,
-                                                        const uint32_t *__restrict__ trans,
-                                                        const uint32_t *__restrict__ centry,
-                                                        const uint64_t *__restrict__ cbase, int32_t *__restrict__ out,
-                                                        uint64_t cap, uint32_t *__restrict__ status)
+__global__ __launch_bounds__(G4_THREADS) void k_g4p_emit(const uint8_t *__restrict__ vb, uint64_t n,
+                                                         const uint32_t *__restrict__ tentry,
+                                                         const uint64_t *__restrict__ tbase,
+                                                         int32_t *__restrict__ out, uint64_t cap,
+                                                         const uint32_t *__restrict__ status)
 {
-    __shared__ G4Smem sm;
-    const uint64_t c = blockIdx.x;
-    const uint64_t start = c * G4_CHUNK;
-    const uint32_t len = (uint32_t)std::min<uint64_t>(G4_CHUNK, n - start);
-    g4_build(sm, src, n, start, len, status);
-    const uint32_t entry = centry[c];
-    const uint64_t base = cbase[c];
-    const uint32_t words = trans[c * 16 + entry] >> 8;
+    __shared__ G4Tile sm;
+    __shared__ uint8_t st[2 * G4_THREADS];
+    __shared__ uint16_t bs[2 * G4_THREADS];
+    __shared__ uint32_t wbuf[G4_TILE / 3 + 2];
     if (*status != 0)  // out-of-domain value or too small an output: write nothing
         return;
-    for (uint32_t j = threadIdx.x; j < words; j += G4_THREADS) {
-        uint32_t p = entry;
+    const uint64_t start = (uint64_t)blockIdx.x * G4_TILE;
+    g4_load<false, true>(sm, nullptr, const_cast<uint8_t *>(vb), n, start, nullptr);
+    const unsigned t = threadIdx.x;
+    uint32_t modes, f[16];
+    g4_segment(sm, start + G4_SEG * t, n, modes, f);
 #pragma unroll
-        for (int k = 0; k < G4_LEVELS; ++k)
-            if ((j >> k) & 1u)
-                p = sm.nxt[k][p];
-        const uint32_t step = sm.nxt[0][p] - p;
-        const int mode = step == 15 ? 0 : step == 7 ? 1 : step == 4 ? 2 : 3;
-        uint32_t code = (uint32_t)mode << 30;
-        const int top = c_g4_top[mode], b = c_g4_bits[mode];
-        for (uint32_t q = 0; q < step; ++q)  // zero-padded past n: OR of 0
-            code |= (uint32_t)sm.v[p + q] << (top - (int)q * b);
-        if (base + j < cap)
-            out[base + j] = (int32_t)code;
+    for (int e = 0; e < 16; ++e)
+        sm.node[G4_THREADS + t][e] = (uint16_t)(e == 15 ? G4_DEAD : f[e]);
+    g4_tree_up(sm);
+    const uint32_t s0 = tentry[blockIdx.x];
+    const uint32_t tile_words = sm.node[1][s0] >> 4;
+    if (t == 0) {
+        st[1] = (uint8_t)s0;
+        bs[1] = 0;
     }
+#pragma unroll 1
+    for (uint32_t lvl = 1; lvl < G4_THREADS; lvl <<= 1) {
+        __syncthreads();
+        if (t < lvl) {
+            const uint32_t i = lvl + t, s = st[i];
+            const uint32_t e = sm.node[2 * i][s];
+            st[2 * i] = (uint8_t)s;
+            bs[2 * i] = bs[i];
+            st[2 * i + 1] = (uint8_t)(e & 15u);
+            bs[2 * i + 1] = (uint16_t)(bs[i] + (e >> 4));
+        }
+    }
+    __syncthreads();
+    // this segment's words: from its entry offset while inside the segment and < n
+    uint32_t pos = st[G4_THREADS + t], j = bs[G4_THREADS + t];
+    const uint64_t seg0 = start + G4_SEG * t;
+    const uint8_t *vbytes = reinterpret_cast<const uint8_t *>(sm.v) + G4_SEG * t;
+    while (pos < G4_SEG && seg0 + pos < n) {
+        const uint32_t mode = (modes >> (2 * pos)) & 3u;
+        const int cnt = c_g4_cnt[mode], top = c_g4_top[mode], b = c_g4_bits[mode];
+        uint32_t code = mode << 30;
+        for (int q = 0; q < cnt; ++q)  // zero-padded past n: OR of 0
+            code |= (uint32_t)vbytes[pos + q] << (top - q * b);
+        wbuf[j++] = code;
+        pos += (uint32_t)cnt;
+    }
+    __syncthreads();
+    const uint64_t base = tbase[blockIdx.x];
+    for (uint32_t k = t; k < tile_words; k += G4_THREADS)
+        if (base + k < cap)
+            out[base + k] = (int32_t)wbuf[k];
 }
 
 // ---- unpack ---------------------------------------------------------------
-constexpr uint32_t G4U_PER_THREAD = 16;
-constexpr uint32_t G4U_BLOCK_WORDS = G4_THREADS * G4U_PER_THREAD;
+constexpr uint32_t G4U_PER_THREAD = 4;
+constexpr uint32_t G4U_BLOCK_WORDS = G4_THREADS * G4U_PER_THREAD;  // 1024 words -> <= 15360 values
 
 __device__ __forceinline__ uint32_t g4_count(int32_t w) { return (uint32_t)c_g4_cnt[(uint32_t)w >> 30]; }
 
+template <unsigned NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *total)
 {
-    __shared__ uint32_t wsum[G4_THREADS / 64];
+    __shared__ uint32_t wsum[NT / 64];
     const unsigned lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t inc = v;
 #pragma unroll
@@ -271,7 +371,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *total)
         wsum[wv] = inc;
     __syncthreads();
     uint32_t off = 0, tot = 0;
-    for (unsigned i = 0; i < G4_THREADS / 64; ++i) {
+    for (unsigned i = 0; i < NT / 64; ++i) {
         if (i < wv)
             off += wsum[i];
         tot += wsum[i];
@@ -287,33 +387,57 @@ __global__ void k_g4_init(uint64_t *count, uint32_t *status)
     *status = 0;
 }
 
+// this thread's 4 words (0 past nw: counted as 15 values of mode 0, so only
+// whole words may be read past the end — they are not)
+__device__ __forceinline__ int4 g4u_words(const int32_t *__restrict__ words, uint64_t nw, uint64_t w0)
+{
+    if (w0 + 4 <= nw && (reinterpret_cast<uintptr_t>(words) & 15u) == 0)
+        return *reinterpret_cast<const int4 *>(words + w0);
+    int4 r;
+    r.x = w0 < nw ? words[w0] : 0;
+    r.y = w0 + 1 < nw ? words[w0 + 1] : 0;
+    r.z = w0 + 2 < nw ? words[w0 + 2] : 0;
+    r.w = w0 + 3 < nw ? words[w0 + 3] : 0;
+    return r;
+}
+
+__device__ __forceinline__ uint32_t g4u_cnt4(const int4 &w, uint64_t nw, uint64_t w0)
+{
+    uint32_t s = 0;
+    s += w0 < nw ? g4_count(w.x) : 0u;
+    s += w0 + 1 < nw ? g4_count(w.y) : 0u;
+    s += w0 + 2 < nw ? g4_count(w.z) : 0u;
+    s += w0 + 3 < nw ? g4_count(w.w) : 0u;
+    return s;
+}
+
 __global__ __launch_bounds__(G4_THREADS) void k_g4u_sums(const int32_t *__restrict__ words, uint64_t nw,
                                                          uint32_t *__restrict__ bsum)
 {
     const uint64_t w0 = (uint64_t)blockIdx.x * G4U_BLOCK_WORDS + (uint64_t)threadIdx.x * G4U_PER_THREAD;
-    uint32_t s = 0;
-    for (uint32_t i = 0; i < G4U_PER_THREAD; ++i)
-        if (w0 + i < nw)
-            s += g4_count(words[w0 + i]);
+    const uint32_t s = g4u_cnt4(g4u_words(words, nw, w0), nw, w0);
     uint32_t tot;
-    block_excl_scan(s, &tot);
+    block_excl_scan<G4_THREADS>(s, &tot);
     if (threadIdx.x == 0)
         bsum[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(G4_THREADS) void k_g4u_scan(const uint32_t *__restrict__ bsum, uint64_t nb,
-                                                         uint64_t *__restrict__ bbase, uint64_t *__restrict__ count,
-                                                         uint64_t cap, uint32_t *__restrict__ status)
+constexpr unsigned G4U_SCAN_THREADS = 1024;
+
+__global__ __launch_bounds__(G4U_SCAN_THREADS) void k_g4u_scan(const uint32_t *__restrict__ bsum, uint64_t nb,
+                                                               uint64_t *__restrict__ bbase,
+                                                               uint64_t *__restrict__ count, uint64_t cap,
+                                                               uint32_t *__restrict__ status)
 {
     __shared__ uint64_t carry;
     if (threadIdx.x == 0)
         carry = 0;
     __syncthreads();
-    for (uint64_t b0 = 0; b0 < nb; b0 += G4_THREADS) {
+    for (uint64_t b0 = 0; b0 < nb; b0 += G4U_SCAN_THREADS) {
         const uint64_t b = b0 + threadIdx.x;
         const uint32_t v = b < nb ? bsum[b] : 0u;
         uint32_t tot;
-        const uint32_t ex = block_excl_scan(v, &tot);
+        const uint32_t ex = block_excl_scan<G4U_SCAN_THREADS>(v, &tot);
         const uint64_t c = carry;
         if (b < nb)
             bbase[b] = c + ex;
@@ -333,51 +457,59 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit(const int32_t *__restri
                                                          const uint64_t *__restrict__ bbase, int32_t *__restrict__ out,
                                                          const uint32_t *__restrict__ status)
 {
+    __shared__ uint8_t obuf[G4U_BLOCK_WORDS * 15];
     if (*status != 0)
         return;
     const uint64_t w0 = (uint64_t)blockIdx.x * G4U_BLOCK_WORDS + (uint64_t)threadIdx.x * G4U_PER_THREAD;
-    uint32_t s = 0;
-    for (uint32_t i = 0; i < G4U_PER_THREAD; ++i)
-        if (w0 + i < nw)
-            s += g4_count(words[w0 + i]);
+    const int4 w4 = g4u_words(words, nw, w0);
     uint32_t tot;
-    uint64_t o = bbase[blockIdx.x] + block_excl_scan(s, &tot);
-    for (uint32_t i = 0; i < G4U_PER_THREAD && w0 + i < nw; ++i) {
-        const uint32_t code = (uint32_t)words[w0 + i];
+    uint32_t o = block_excl_scan<G4_THREADS>(g4u_cnt4(w4, nw, w0), &tot);
+    const int32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+    for (uint32_t i = 0; i < G4U_PER_THREAD; ++i) {
+        if (w0 + i >= nw)
+            break;
+        const uint32_t code = (uint32_t)wv[i];
         const int mode = (int)(code >> 30);
         const int cnt = c_g4_cnt[mode], top = c_g4_top[mode], b = c_g4_bits[mode];
         const uint32_t mask = (1u << b) - 1u;
         for (int j = 0; j < cnt; ++j)
-            out[o + j] = (int32_t)((code >> (top - j * b)) & mask);
-        o += (uint64_t)cnt;
+            obuf[o + j] = (uint8_t)((code >> (top - j * b)) & mask);
+        o += (uint32_t)cnt;
     }
+    __syncthreads();
+    const uint64_t base = bbase[blockIdx.x];
+    for (uint32_t k = threadIdx.x; k < tot; k += G4_THREADS)
+        out[base + k] = (int32_t)obuf[k];
 }
 
 // workspace layout (bytes, 256-aligned pieces)
 struct G4Ws {
-    uint32_t *trans, *gtrans, *gentry, *centry;
-    uint64_t *gbase, *cbase;
+    uint32_t *agg, *gagg, *gentry, *tentry, *bsum;
+    uint64_t *gbase, *tbase, *bbase;
+    uint8_t *vb;
 };
 
 static inline uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
 
 static uint64_t g4_ws(uint64_t n, char *base, G4Ws *w)
 {
-    const uint64_t chunks = (n + G4_CHUNK - 1) / G4_CHUNK;
-    const uint64_t groups = (chunks + G4_GROUP - 1) / G4_GROUP;
+    const uint64_t tiles = (n + G4_TILE - 1) / G4_TILE;
+    const uint64_t groups = (tiles + G4_GROUP - 1) / G4_GROUP;
     uint64_t off = 0;
     auto take = [&](uint64_t bytes) {
         char *p = base ? base + off : nullptr;
         off += al256(bytes);
         return p;
     };
-    G4Ws t;
-    t.trans = (uint32_t *)take(chunks * 64);
-    t.gtrans = (uint32_t *)take(groups * 64);
+    G4Ws t{};
+    t.agg = (uint32_t *)take(tiles * 64);
+    t.gagg = (uint32_t *)take(groups * 64);
     t.gentry = (uint32_t *)take(groups * 4);
     t.gbase = (uint64_t *)take(groups * 8);
-    t.centry = (uint32_t *)take(chunks * 4);
-    t.cbase = (uint64_t *)take(chunks * 8);
+    t.tentry = (uint32_t *)take(tiles * 4);
+    t.tbase = (uint64_t *)take(tiles * 8);
+    t.vb = (uint8_t *)take(tiles * G4_TILE);  // whole tiles: the dword stores past n stay inside
     if (w)
         *w = t;
     return off;
@@ -393,8 +525,8 @@ static uint64_t g4u_ws(uint64_t nw, char *base, G4Ws *w)
         return p;
     };
     G4Ws t{};
-    t.trans = (uint32_t *)take(nb * 4);   // block sums
-    t.gbase = (uint64_t *)take(nb * 8);   // block bases
+    t.bsum = (uint32_t *)take(nb * 4);   // block sums
+    t.bbase = (uint64_t *)take(nb * 8);  // block bases
     if (w)
         *w = t;
     return off;
@@ -419,22 +551,28 @@ int gc_greedy4_pack_device(const int32_t *src, uint64_t n, int32_t *out, uint64_
     GC_REQUIRE(workspace && nwords && status, "gc_greedy4_pack_device: null workspace / nwords / status");
     GC_REQUIRE(n == 0 || (src && out), "gc_greedy4_pack_device: null pointer");
     GC_REQUIRE(n < (1ull << 40), "gc_greedy4_pack_device: n too large");
+    GC_REQUIRE(aligned16(workspace), "gc_greedy4_pack_device: workspace must be 16-byte aligned");
     hipStream_t st = as_stream(stream);
     G4Ws w;
     g4_ws(n, reinterpret_cast<char *>(workspace), &w);
     hipLaunchKernelGGL(k_g4_init, dim3(1), dim3(1), 0, st, nwords, status);
     if (n == 0)
         return launch_status("gc_greedy4_pack_device");
-    const uint64_t chunks = (n + G4_CHUNK - 1) / G4_CHUNK;
-    const uint64_t groups = (chunks + G4_GROUP - 1) / G4_GROUP;
-    hipLaunchKernelGGL(k_g4_chunk, dim3((unsigned)chunks), dim3(G4_THREADS), 0, st, src, n, w.trans, status);
-    hipLaunchKernelGGL(k_g4_group, dim3((unsigned)groups), dim3(G4_THREADS), 0, st, w.trans, chunks, w.gtrans);
-    hipLaunchKernelGGL(k_g4_walk, dim3(1), dim3(G4_THREADS), 0, st, w.gtrans, groups, w.gentry, w.gbase, nwords, cap,
+    const uint64_t tiles = (n + G4_TILE - 1) / G4_TILE;
+    const uint64_t groups = (tiles + G4_GROUP - 1) / G4_GROUP;
+    if (aligned16(src))
+        hipLaunchKernelGGL(k_g4p_tile<true>, dim3((unsigned)tiles), dim3(G4_THREADS), 0, st, src, n, w.vb, w.agg,
+                           status);
+    else
+        hipLaunchKernelGGL(k_g4p_tile<false>, dim3((unsigned)tiles), dim3(G4_THREADS), 0, st, src, n, w.vb, w.agg,
+                           status);
+    hipLaunchKernelGGL(k_g4p_group, dim3((unsigned)groups), dim3(G4_THREADS), 0, st, w.agg, tiles, w.gagg);
+    hipLaunchKernelGGL(k_g4p_top, dim3(1), dim3(G4_THREADS), 0, st, w.gagg, groups, w.gentry, w.gbase, nwords, cap,
                        status);
-    hipLaunchKernelGGL(k_g4_spread, dim3((unsigned)groups), dim3(G4_THREADS), 0, st, w.trans, chunks, w.gentry,
-                       w.gbase, w.centry, w.cbase);
-    hipLaunchKernelGGL(k_g4_emit, dim3((unsigned)chunks), dim3(G4_THREADS), 0, st, src, n, w.trans, w.centry,
-                       w.cbase, out, cap, status);
+    hipLaunchKernelGGL(k_g4p_spread, dim3((unsigned)groups), dim3(G4_THREADS), 0, st, w.agg, tiles, w.gentry,
+                       w.gbase, w.tentry, w.tbase);
+    hipLaunchKernelGGL(k_g4p_emit, dim3((unsigned)tiles), dim3(G4_THREADS), 0, st, w.vb, n, w.tentry, w.tbase, out,
+                       cap, status);
     return launch_status("gc_greedy4_pack_device");
 }
 
@@ -451,9 +589,9 @@ int gc_greedy4_unpack_device(const int32_t *words, uint64_t nwords, int32_t *out
     if (nwords == 0)
         return launch_status("gc_greedy4_unpack_device");
     const uint64_t nb = (nwords + G4U_BLOCK_WORDS - 1) / G4U_BLOCK_WORDS;
-    hipLaunchKernelGGL(k_g4u_sums, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.trans);
-    hipLaunchKernelGGL(k_g4u_scan, dim3(1), dim3(G4_THREADS), 0, st, w.trans, nb, w.gbase, count, cap, status);
-    hipLaunchKernelGGL(k_g4u_emit, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.gbase, out, status);
+    hipLaunchKernelGGL(k_g4u_sums, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bsum);
+    hipLaunchKernelGGL(k_g4u_scan, dim3(1), dim3(G4U_SCAN_THREADS), 0, st, w.bsum, nb, w.bbase, count, cap, status);
+    hipLaunchKernelGGL(k_g4u_emit, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bbase, out, status);
     return launch_status("gc_greedy4_unpack_device");
 }
 

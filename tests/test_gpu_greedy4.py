@@ -1,9 +1,11 @@
 """Device greedy 4-mode packer (gc_greedy4_*_device) — the reference's
 bitpacking format (extensions/Extension CPU/bitpacking.cpp:5-124), produced
-by parallel list ranking.  Bit-exact against the reference extension's own
-known-answer vectors (tests/golden/packers.npz) and against the oracle /
-host packer on inputs that stress the chunk boundaries (2048-element chunks,
-256-chunk groups): all-mode-0 runs, all-mode-3 runs, mixes, ragged ends."""
+by a scan over segment tables.  Bit-exact against the reference extension's
+own known-answer vectors (tests/golden/packers.npz) and against the oracle /
+host packer on inputs that stress the boundaries (16-position segments,
+4096-position tiles, 256-tile groups, 64-group chunks of the top walk):
+all-mode-0 runs, all-mode-3 runs, mixes, ragged ends, and the QSGDBP call
+site's ResNet50 bucket (23,520,842 sign bits and 4-bit magnitudes)."""
 import os
 
 import numpy as np
@@ -51,6 +53,16 @@ def _inputs():
         a[2048 * c - 7:2048 * c + 3] = 200
     yield "edges", a
     yield "qsgd4", np.abs(rng.normal(0, 4, 3_000_000)).clip(0, 15).astype(np.int32)
+    # runs that flip modes right at segment / tile boundaries, unaligned starts
+    b = np.zeros(4096 * 5 + 9, np.int32)
+    for c in range(1, 5):
+        b[4096 * c - 16:4096 * c + 1] = 130
+        b[4096 * c + 7:4096 * c + 8] = 17
+    b[::16] = 5
+    yield "tile_edges", b
+    yield "mode3_all", rng.integers(128, 256, 4096 * 3 + 31).astype(np.int32)
+    # more than one 64-group chunk of the top walk (> 64 x 256 x 4096 positions)
+    yield "chunks2", rng.choice([0, 1, 2, 3, 7, 15], 70_000_000, p=[.4, .2, .15, .15, .05, .05]).astype(np.int32)
 
 
 @pytest.mark.parametrize("name,src", list(_inputs()), ids=lambda v: v if isinstance(v, str) else "")
@@ -70,3 +82,31 @@ def test_device_packer_rejects_out_of_domain():
     for bad in ([1, 2, 256], [-1, 3]):
         with pytest.raises(gcodec.GCodecError):
             codec.greedy4_pack(torch.tensor(bad, dtype=torch.int32, device=DEV))
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+def test_qsgdbp_resnet50_bucket_packs_exactly(bits):
+    """The QSGDBP call site at the ResNet50 bucket size (23,520,842): the sign
+    bits and the magnitudes packed on the device equal the host packer's words
+    (the reference format), and unpack returns the values."""
+    n = 23_520_842
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(n, device=DEV, generator=g).mul_(0.01)
+    norm = codec.absmax(x)
+    xi, sg = codec.qsgd_quantize_split(x, norm, bits, gcodec.Generator(9, "philox").reserve(n))
+    for src in (xi, sg):
+        host_words = codec.greedy4_pack(src.cpu())
+        dev_words = codec.greedy4_pack(src)
+        assert np.array_equal(dev_words.cpu().numpy(), host_words.numpy())
+        u = codec.greedy4_unpack(dev_words)
+        assert torch.equal(u[:n], src)
+
+
+def test_device_packer_unaligned_source():
+    """src not 16-byte aligned (a slice at +1 element): the scalar-load path."""
+    rng = np.random.default_rng(8)
+    a = rng.choice([0, 1, 3, 9, 15, 100, 255], 300_001, p=[.3, .2, .15, .15, .1, .05, .05]).astype(np.int32)
+    d = torch.from_numpy(a).to(DEV)[1:]
+    assert d.data_ptr() % 16 != 0
+    host = codec.greedy4_pack(torch.from_numpy(a[1:].copy()))
+    assert np.array_equal(codec.greedy4_pack(d).cpu().numpy(), host.numpy())
