@@ -9,12 +9,12 @@
 // [0, 255] (the reference corrupts negatives and loops forever on >= 256).
 //
 // The word starts form a chain next(i) = i + CNT[mode(i)] from i = 0: a scan
-// whose elements are FUNCTIONS.  Cut the positions into segments of 16; a
+// whose elements are FUNCTIONS.  Cut the positions into segments of 32; a
 // word that starts in one segment ends at most 14 positions into the next, so
 // a segment maps the offset its first word starts at (0..14, or 15 = past n)
 // to the offset its chain leaves at and the words it emitted: a 16-entry
 // table, and tables compose associatively.
-//   k_g4p_tile     per 4096-element tile (256 threads x one segment): window
+//   k_g4p_tile     per 8192-element tile (256 threads x one segment): window
 //                  flags by SWAR byte tests, the segment table by a backward
 //                  recurrence held in registers (static indices only), then a
 //                  reduction tree of the 256 tables in LDS -> the tile's
@@ -39,16 +39,18 @@
 namespace gc {
 
 constexpr unsigned G4_THREADS = 256;
-constexpr uint32_t G4_SEG = 16;                         // positions per segment (one thread)
-constexpr uint32_t G4_TILE = G4_SEG * G4_THREADS;       // 4096 positions per tile
+constexpr uint32_t G4_SEG = 32;                         // positions per segment (one thread)
+constexpr uint32_t G4_TILE = G4_SEG * G4_THREADS;       // 8192 positions per tile
 constexpr uint32_t G4_GROUP = 256;                      // tiles per group
 constexpr uint32_t G4_DEAD = 15;                        // table state: the chain has passed n
 constexpr uint32_t G4_TOP_CHUNK = 64;                   // group tables staged in LDS per top step
 constexpr uint32_t G4_STATUS_RANGE = 1u, G4_STATUS_NOSPC = 2u;
 
-__constant__ int c_g4_cnt[4] = {15, 7, 4, 3};
-__constant__ int c_g4_bits[4] = {2, 4, 7, 8};
-__constant__ int c_g4_top[4] = {28, 26, 23, 22};
+// per-mode constants as nibble / byte tables in an immediate (a per-lane mode
+// index into __constant__ arrays became vector memory loads in the emit loops)
+__device__ __forceinline__ uint32_t g4_cnt(uint32_t m) { return (0x347fu >> (4 * m)) & 15u; }   // 15 7 4 3
+__device__ __forceinline__ uint32_t g4_bits(uint32_t m) { return (0x8742u >> (4 * m)) & 15u; }  // 2 4 7 8
+__device__ __forceinline__ uint32_t g4_top(uint32_t m) { return (0x16171a1cu >> (8 * m)) & 0xffu; }  // 28 26 23 22
 
 // 4 byte-threshold flags of one dword (bytes b0..b3): bit j set iff byte j has
 // a bit of `hi` set (hi = ~(lim - 1) for a power-of-two limit)
@@ -60,68 +62,86 @@ __device__ __forceinline__ uint32_t byte_flags(uint32_t w, uint32_t hi)
 }
 
 // table entries: exit offset (4 bits) | words << 4
-__device__ __forceinline__ uint32_t g4_compose(uint32_t a, const uint16_t *b)
-{
-    const uint32_t e = b[a & 15u];
-    return (e & 15u) | (((a >> 4) + (e >> 4)) << 4);
-}
-__device__ __forceinline__ uint32_t g4_compose32(uint32_t a, const uint32_t *b)
-{
-    const uint32_t e = b[a & 15u];
-    return (e & 15u) | (((a >> 4) + (e >> 4)) << 4);
-}
 
 struct G4Tile {
     uint32_t v[(G4_TILE + 32) / 4];  // values as bytes (0 past n), 32-byte halo
     uint16_t node[2 * G4_THREADS][16];  // reduction tree: leaves 256..511, root 1
 };
 
-// modes of this thread's 16 positions (2 bits each) from the LDS bytes, and
-// its segment table (16 entries, exit | words << 4) by the backward recurrence
-// f[p] = 1 word + f[p + cnt(p)] (an exit past the segment: offset p + cnt - 16).
+// modes of this thread's G4_SEG positions (2 bits each) from the LDS bytes,
+// and its segment table (entries 0..14, exit | words << 4) by the backward
+// recurrence f[p] = 1 word + f[p + cnt(p)], where a successor past the
+// segment is its offset there, p + cnt - G4_SEG (0..14).  All indices are
+// static (the recurrence is unrolled), so f stays in registers.
 // seg0 = global position of the segment, n = bucket size.
-__device__ __forceinline__ void g4_segment(const G4Tile &sm, uint64_t seg0, uint64_t n, uint32_t &modes,
-                                           uint32_t f[16])
+__device__ __forceinline__ void g4_segment(const G4Tile &sm, uint64_t seg0, uint64_t n, uint64_t &modes,
+                                           uint32_t f[G4_SEG])
 {
+    constexpr int DW = G4_SEG / 4 + 4;  // the segment's dwords + 16 bytes of the next (windows reach +14)
     const unsigned t = threadIdx.x;
-    const uint4 a = *reinterpret_cast<const uint4 *>(&sm.v[4 * t]);
-    const uint4 b = *reinterpret_cast<const uint4 *>(&sm.v[4 * t + 4]);
-    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint32_t ge4 = 0, ge16 = 0, ge128 = 0;  // bit j: byte j of the 32 (positions seg .. seg+31)
+    uint32_t w[DW];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        ge4 |= byte_flags(w[k], 0xfcfcfcfcu) << (4 * k);
-        ge16 |= byte_flags(w[k], 0xf0f0f0f0u) << (4 * k);
-        ge128 |= byte_flags(w[k], 0x80808080u) << (4 * k);
+    for (int k = 0; k < DW; k += 4)
+        *reinterpret_cast<uint4 *>(&w[k]) = *reinterpret_cast<const uint4 *>(&sm.v[(G4_SEG / 4) * t + k]);
+    uint64_t ge4 = 0, ge16 = 0, ge128 = 0;  // bit j: byte j (position seg0 + j)
+#pragma unroll
+    for (int k = 0; k < DW; ++k) {
+        ge4 |= (uint64_t)byte_flags(w[k], 0xfcfcfcfcu) << (4 * k);
+        ge16 |= (uint64_t)byte_flags(w[k], 0xf0f0f0f0u) << (4 * k);
+        ge128 |= (uint64_t)byte_flags(w[k], 0x80808080u) << (4 * k);
     }
     modes = 0;
-    const uint32_t live = seg0 >= n ? 0u : (uint32_t)std::min<uint64_t>(16, n - seg0);  // positions < n
+    const uint32_t live = seg0 >= n ? 0u : (uint32_t)std::min<uint64_t>(G4_SEG, n - seg0);  // positions < n
 #pragma unroll
-    for (int p = 15; p >= 0; --p) {
+    for (int p = G4_SEG - 1; p >= 0; --p) {
         const uint32_t m = ((ge4 >> p) & 0x7fffu) == 0 ? 0u : ((ge16 >> p) & 0x7fu) == 0 ? 1u
                                                              : ((ge128 >> p) & 0xfu) == 0 ? 2u : 3u;
-        modes |= m << (2 * p);
-        // the four possible successors (static indices): past the segment -> its offset there
-        const uint32_t s3 = p + 3 < 16 ? f[(p + 3) & 15] : (uint32_t)(p + 3 - 16);
-        const uint32_t s4 = p + 4 < 16 ? f[(p + 4) & 15] : (uint32_t)(p + 4 - 16);
-        const uint32_t s7 = p + 7 < 16 ? f[(p + 7) & 15] : (uint32_t)(p + 7 - 16);
-        const uint32_t s15v = p == 0 ? f[15] : (uint32_t)(p - 1);  // p + 15 >= 16 unless p == 0
-        const uint32_t nx = m == 0 ? s15v : m == 1 ? s7 : m == 2 ? s4 : s3;
+        modes |= (uint64_t)m << (2 * p);
+        // the four possible successors (static indices)
+        const uint32_t s3 = p + 3 < (int)G4_SEG ? f[(p + 3) % G4_SEG] : (uint32_t)(p + 3 - (int)G4_SEG);
+        const uint32_t s4 = p + 4 < (int)G4_SEG ? f[(p + 4) % G4_SEG] : (uint32_t)(p + 4 - (int)G4_SEG);
+        const uint32_t s7 = p + 7 < (int)G4_SEG ? f[(p + 7) % G4_SEG] : (uint32_t)(p + 7 - (int)G4_SEG);
+        const uint32_t s15 = p + 15 < (int)G4_SEG ? f[(p + 15) % G4_SEG] : (uint32_t)(p + 15 - (int)G4_SEG);
+        const uint32_t nx = m == 0 ? s15 : m == 1 ? s7 : m == 2 ? s4 : s3;
         f[p] = (uint32_t)p < live ? nx + 16u : G4_DEAD;
+    }
+}
+
+// one tree level: nodes lvl .. 2 lvl - 1, node i = left child then right
+// child.  A thread per (node, entry) pair, so 16 consecutive lanes read one
+// node's row (conflict-free; a thread per node put 16 lanes on one bank);
+// every pair's two lookups are issued before any store (the rows written
+// are never read on the same level)
+template <typename T, uint32_t NT>
+__device__ __forceinline__ void g4_level(T (*node)[16], uint32_t lvl)
+{
+    constexpr uint32_t R = 8;  // pairs per thread on the widest level (128 nodes x 16 / 256)
+    const uint32_t items = lvl * 16, t = threadIdx.x;
+    uint32_t res[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t k = t + r * NT;
+        if (k < items) {
+            const uint32_t i = lvl + (k >> 4), e = k & 15u;
+            const uint32_t x = node[2 * i][e], y = node[2 * i + 1][x & 15u];
+            res[r] = (y & 15u) | (((x >> 4) + (y >> 4)) << 4);
+        }
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t k = t + r * NT;
+        if (k < items)
+            node[lvl + (k >> 4)][k & 15u] = (T)res[r];
     }
 }
 
 // reduction tree over the 256 leaves node[256 + t] -> node[1]
 __device__ __forceinline__ void g4_tree_up(G4Tile &sm)
 {
-    const unsigned t = threadIdx.x;
 #pragma unroll 1
     for (uint32_t lvl = G4_THREADS / 2; lvl >= 1; lvl >>= 1) {
         __syncthreads();
-        for (uint32_t k = t; k < lvl * 16; k += G4_THREADS) {
-            const uint32_t i = lvl + (k >> 4), e = k & 15u;
-            sm.node[i][e] = (uint16_t)g4_compose(sm.node[2 * i][e], sm.node[2 * i + 1]);
-        }
+        g4_level<uint16_t, G4_THREADS>(sm.node, lvl);
     }
     __syncthreads();
 }
@@ -176,7 +196,8 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4p_tile(const int32_t *__restri
     __shared__ G4Tile sm;
     const uint64_t start = (uint64_t)blockIdx.x * G4_TILE;
     g4_load<true, ALIGNED>(sm, src, vb, n, start, status);
-    uint32_t modes, f[16];
+    uint64_t modes;
+    uint32_t f[G4_SEG];
     g4_segment(sm, start + G4_SEG * threadIdx.x, n, modes, f);
     (void)modes;
 #pragma unroll
@@ -205,10 +226,7 @@ __device__ __forceinline__ void g4_group_up(G4Group &sm, const uint32_t *__restr
 #pragma unroll 1
     for (uint32_t lvl = G4_GROUP / 2; lvl >= 1; lvl >>= 1) {
         __syncthreads();
-        for (uint32_t k = t; k < lvl * 16; k += G4_THREADS) {
-            const uint32_t i = lvl + (k >> 4), e = k & 15u;
-            sm.node[i][e] = g4_compose32(sm.node[2 * i][e], sm.node[2 * i + 1]);
-        }
+        g4_level<uint32_t, G4_THREADS>(sm.node, lvl);
     }
     __syncthreads();
 }
@@ -255,20 +273,49 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4p_top(const uint32_t *__restri
     }
 }
 
-// per group: the tree again, then a down-sweep from the group's entry -> tiles
+// per group: the tree again, then a down-sweep from the group's entry -> tiles.
+// WALK (groups <= G4_TOP_CHUNK, k_g4p_top not launched): the block finds its
+// group's entry itself by walking the tables of the groups before it (LDS),
+// and the last block writes the total.
+template <bool WALK>
 __global__ __launch_bounds__(G4_THREADS) void k_g4p_spread(const uint32_t *__restrict__ agg, uint64_t tiles,
+                                                           const uint32_t *__restrict__ gagg,
                                                            const uint32_t *__restrict__ gentry,
                                                            const uint64_t *__restrict__ gbase,
-                                                           uint32_t *__restrict__ tentry, uint64_t *__restrict__ tbase)
+                                                           uint32_t *__restrict__ tentry, uint64_t *__restrict__ tbase,
+                                                           uint64_t *__restrict__ nwords, uint64_t cap,
+                                                           uint32_t *__restrict__ status)
 {
     __shared__ G4Group sm;
+    __shared__ uint32_t gt[WALK ? G4_TOP_CHUNK * 16 : 1];
     const uint64_t first = (uint64_t)blockIdx.x * G4_GROUP;
     const uint32_t cnt = (uint32_t)std::min<uint64_t>(G4_GROUP, tiles - first);
-    g4_group_up(sm, agg, first, cnt);
     const unsigned t = threadIdx.x;
+    if (WALK)
+        for (uint32_t k = t; k < blockIdx.x * 16u; k += G4_THREADS)
+            gt[k] = gagg[k];
+    g4_group_up(sm, agg, first, cnt);  // starts and ends with a barrier
     if (t == 0) {
-        sm.st[1] = gentry[blockIdx.x];
-        sm.bs[1] = gbase[blockIdx.x];
+        uint32_t state = 0;
+        uint64_t base = 0;
+        if (WALK) {
+            for (uint32_t j = 0; j < blockIdx.x; ++j) {
+                const uint32_t x = gt[j * 16 + state];
+                base += x >> 4;
+                state = x & 15u;
+            }
+            if (blockIdx.x + 1 == gridDim.x) {
+                const uint64_t total = base + (sm.node[1][state] >> 4);
+                *nwords = total;
+                if (total > cap)
+                    atomicOr(status, G4_STATUS_NOSPC);
+            }
+        } else {
+            state = gentry[blockIdx.x];
+            base = gbase[blockIdx.x];
+        }
+        sm.st[1] = state;
+        sm.bs[1] = base;
     }
 #pragma unroll 1
     for (uint32_t lvl = 1; lvl < G4_GROUP; lvl <<= 1) {
@@ -304,7 +351,8 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4p_emit(const uint8_t *__restri
     const uint64_t start = (uint64_t)blockIdx.x * G4_TILE;
     g4_load<false, true>(sm, nullptr, const_cast<uint8_t *>(vb), n, start, nullptr);
     const unsigned t = threadIdx.x;
-    uint32_t modes, f[16];
+    uint64_t modes;
+    uint32_t f[G4_SEG];
     g4_segment(sm, start + G4_SEG * t, n, modes, f);
 #pragma unroll
     for (int e = 0; e < 16; ++e)
@@ -332,15 +380,23 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4p_emit(const uint8_t *__restri
     // this segment's words: from its entry offset while inside the segment and < n
     uint32_t pos = st[G4_THREADS + t], j = bs[G4_THREADS + t];
     const uint64_t seg0 = start + G4_SEG * t;
-    const uint8_t *vbytes = reinterpret_cast<const uint8_t *>(sm.v) + G4_SEG * t;
-    while (pos < G4_SEG && seg0 + pos < n) {
-        const uint32_t mode = (modes >> (2 * pos)) & 3u;
-        const int cnt = c_g4_cnt[mode], top = c_g4_top[mode], b = c_g4_bits[mode];
+    const uint32_t live = seg0 >= n ? 0u : (uint32_t)std::min<uint64_t>(G4_SEG, n - seg0);
+    while (pos < live) {
+        const uint32_t mode = (uint32_t)(modes >> (2 * pos)) & 3u;
+        // bytes pos .. pos+15 of this segment (zero past n): 5 aligned dwords, byte-aligned
+        const uint32_t *d = &sm.v[(G4_SEG / 4) * t + (pos >> 2)];
+        const uint32_t sh = pos & 3u;
+        const uint32_t u0 = d[0], u1 = d[1], u2 = d[2], u3 = d[3], u4 = d[4];
+        const uint32_t x[4] = {__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
+                               __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
+        const uint32_t b = g4_bits(mode), top = g4_top(mode), cnt = g4_cnt(mode);
         uint32_t code = mode << 30;
-        for (int q = 0; q < cnt; ++q)  // zero-padded past n: OR of 0
-            code |= (uint32_t)vbytes[pos + q] << (top - q * b);
+#pragma unroll
+        for (uint32_t q = 0; q < 15; ++q)  // values past cnt belong to the next word: left out
+            if (q < cnt)
+                code |= ((x[q >> 2] >> (8 * (q & 3))) & 0xffu) << (top - q * b);
         wbuf[j++] = code;
-        pos += (uint32_t)cnt;
+        pos += cnt;
     }
     __syncthreads();
     const uint64_t base = tbase[blockIdx.x];
@@ -353,7 +409,7 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4p_emit(const uint8_t *__restri
 constexpr uint32_t G4U_PER_THREAD = 4;
 constexpr uint32_t G4U_BLOCK_WORDS = G4_THREADS * G4U_PER_THREAD;  // 1024 words -> <= 15360 values
 
-__device__ __forceinline__ uint32_t g4_count(int32_t w) { return (uint32_t)c_g4_cnt[(uint32_t)w >> 30]; }
+__device__ __forceinline__ uint32_t g4_count(int32_t w) { return g4_cnt((uint32_t)w >> 30); }
 
 template <unsigned NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *total)
@@ -471,11 +527,13 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit(const int32_t *__restri
             break;
         const uint32_t code = (uint32_t)wv[i];
         const int mode = (int)(code >> 30);
-        const int cnt = c_g4_cnt[mode], top = c_g4_top[mode], b = c_g4_bits[mode];
+        const uint32_t cnt = g4_cnt(mode), top = g4_top(mode), b = g4_bits(mode);
         const uint32_t mask = (1u << b) - 1u;
-        for (int j = 0; j < cnt; ++j)
-            obuf[o + j] = (uint8_t)((code >> (top - j * b)) & mask);
-        o += (uint32_t)cnt;
+#pragma unroll
+        for (uint32_t j = 0; j < 15; ++j)
+            if (j < cnt)
+                obuf[o + j] = (uint8_t)((code >> (top - j * b)) & mask);
+        o += cnt;
     }
     __syncthreads();
     const uint64_t base = bbase[blockIdx.x];
@@ -567,10 +625,15 @@ int gc_greedy4_pack_device(const int32_t *src, uint64_t n, int32_t *out, uint64_
         hipLaunchKernelGGL(k_g4p_tile<false>, dim3((unsigned)tiles), dim3(G4_THREADS), 0, st, src, n, w.vb, w.agg,
                            status);
     hipLaunchKernelGGL(k_g4p_group, dim3((unsigned)groups), dim3(G4_THREADS), 0, st, w.agg, tiles, w.gagg);
-    hipLaunchKernelGGL(k_g4p_top, dim3(1), dim3(G4_THREADS), 0, st, w.gagg, groups, w.gentry, w.gbase, nwords, cap,
-                       status);
-    hipLaunchKernelGGL(k_g4p_spread, dim3((unsigned)groups), dim3(G4_THREADS), 0, st, w.agg, tiles, w.gentry,
-                       w.gbase, w.tentry, w.tbase);
+    if (groups <= G4_TOP_CHUNK) {
+        hipLaunchKernelGGL(k_g4p_spread<true>, dim3((unsigned)groups), dim3(G4_THREADS), 0, st, w.agg, tiles, w.gagg,
+                           w.gentry, w.gbase, w.tentry, w.tbase, nwords, cap, status);
+    } else {
+        hipLaunchKernelGGL(k_g4p_top, dim3(1), dim3(G4_THREADS), 0, st, w.gagg, groups, w.gentry, w.gbase, nwords,
+                           cap, status);
+        hipLaunchKernelGGL(k_g4p_spread<false>, dim3((unsigned)groups), dim3(G4_THREADS), 0, st, w.agg, tiles,
+                           w.gagg, w.gentry, w.gbase, w.tentry, w.tbase, nwords, cap, status);
+    }
     hipLaunchKernelGGL(k_g4p_emit, dim3((unsigned)tiles), dim3(G4_THREADS), 0, st, w.vb, n, w.tentry, w.tbase, out,
                        cap, status);
     return launch_status("gc_greedy4_pack_device");

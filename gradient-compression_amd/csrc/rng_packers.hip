@@ -136,6 +136,77 @@ __global__ __launch_bounds__(kBlock) void k_byteunpack8(const int64_t *__restric
     }
 }
 
+// the big-endian byte word of 4 values' low bytes: v0 in bits 31:24 .. v3 in 7:0
+__device__ __forceinline__ uint32_t be_bytes4(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3)
+{
+    const uint32_t lo = __builtin_amdgcn_perm(v2, v3, 0x0c0c0400u);  // [v3.b0 v2.b0 0 0] (low to high)
+    const uint32_t hi = __builtin_amdgcn_perm(v0, v1, 0x0c0c0400u);  // [v1.b0 v0.b0 0 0]
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);               // [v3 v2 v1 v0] = v0 << 24 | ...
+}
+
+// 16-byte vector forms (src and out 16-byte aligned): a thread packs 16
+// values into two words with one 16-byte store; int8 sources are one 16-byte
+// load + two byte swaps.  The last partial group goes through the scalar code.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_bytepack8_v(const T *__restrict__ src, uint64_t n,
+                                                        int64_t *__restrict__ out)
+{
+    const uint64_t groups = n >> 4;  // full 16-value groups
+    for (uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x; p <= groups; p += (uint64_t)gridDim.x * kBlock) {
+        if (p == groups) {  // the tail: words 2p and 2p+1 if they hold values
+            for (uint64_t w = 2 * p; w < (n + 7) >> 3; ++w) {
+                uint64_t code = 0;
+                for (int j = 0; j < 8; ++j)
+                    if (w * 8 + j < n)
+                        code |= ((uint64_t)(int64_t)src[w * 8 + j] & 0xffull) << (8 * (7 - j));
+                out[w] = (int64_t)code;
+            }
+            continue;
+        }
+        uint32_t h[4];  // big-endian 4-byte pieces: words 2p = h0:h1, 2p+1 = h2:h3 (high half first)
+        if constexpr (sizeof(T) == 1) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(src + 16 * p);
+            h[0] = __builtin_bswap32(v.x);
+            h[1] = __builtin_bswap32(v.y);
+            h[2] = __builtin_bswap32(v.z);
+            h[3] = __builtin_bswap32(v.w);
+        } else if constexpr (sizeof(T) == 4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(src + 16 * p + 4 * k);
+                h[k] = be_bytes4(v.x, v.y, v.z, v.w);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int64_t *q = reinterpret_cast<const int64_t *>(src) + 16 * p + 4 * k;
+                const ulonglong2 a = *reinterpret_cast<const ulonglong2 *>(q);
+                const ulonglong2 b = *reinterpret_cast<const ulonglong2 *>(q + 2);
+                h[k] = be_bytes4((uint32_t)a.x, (uint32_t)a.y, (uint32_t)b.x, (uint32_t)b.y);
+            }
+        }
+        // int64 word = h_hi << 32 | h_lo; little-endian dwords: (lo, hi)
+        *reinterpret_cast<uint4 *>(out + 2 * p) = make_uint4(h[1], h[0], h[3], h[2]);
+    }
+}
+
+// 16 bytes per thread: two words -> one 16-byte store
+__global__ __launch_bounds__(kBlock) void k_byteunpack8_v(const int64_t *__restrict__ src, uint64_t nw,
+                                                          int8_t *__restrict__ out)
+{
+    const uint64_t pairs = nw >> 1;
+    for (uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x; p <= pairs; p += (uint64_t)gridDim.x * kBlock) {
+        if (p == pairs) {
+            if (nw & 1)
+                *reinterpret_cast<uint64_t *>(out + 8 * (nw - 1)) = __builtin_bswap64((uint64_t)src[nw - 1]);
+            continue;
+        }
+        const uint4 v = *reinterpret_cast<const uint4 *>(src + 2 * p);  // (lo0, hi0, lo1, hi1)
+        *reinterpret_cast<uint4 *>(out + 16 * p) =
+            make_uint4(__builtin_bswap32(v.y), __builtin_bswap32(v.x), __builtin_bswap32(v.w), __builtin_bswap32(v.z));
+    }
+}
+
 }  // namespace gc
 
 using namespace gc;
@@ -168,6 +239,19 @@ int gc_bytepack8(const void *src, uint32_t src_dtype, uint64_t n, int64_t *out, 
     if (n == 0)
         return GC_OK;
     hipStream_t st = as_stream(stream);
+    if (aligned16(src) && aligned16(out)) {  // the 16-byte vector kernels
+        const unsigned g = grid_for((n >> 4) + 1);
+        if (src_dtype == GC_I8)
+            hipLaunchKernelGGL((k_bytepack8_v<int8_t>), dim3(g), dim3(kBlock), 0, st,
+                               reinterpret_cast<const int8_t *>(src), n, out);
+        else if (src_dtype == GC_I32)
+            hipLaunchKernelGGL((k_bytepack8_v<int32_t>), dim3(g), dim3(kBlock), 0, st,
+                               reinterpret_cast<const int32_t *>(src), n, out);
+        else
+            hipLaunchKernelGGL((k_bytepack8_v<int64_t>), dim3(g), dim3(kBlock), 0, st,
+                               reinterpret_cast<const int64_t *>(src), n, out);
+        return launch_status("gc_bytepack8");
+    }
     const unsigned grid = grid_for((n + 7) >> 3);
     if (src_dtype == GC_I8)
         hipLaunchKernelGGL((k_bytepack8<int8_t>), dim3(grid), dim3(kBlock), 0, st,
@@ -187,7 +271,12 @@ int gc_byteunpack8(const int64_t *src, uint64_t nwords, int8_t *out, gc_stream_t
     GC_REQUIRE(aligned16(out) || (reinterpret_cast<uintptr_t>(out) & 7u) == 0, "gc_byteunpack8: out must be 8-byte aligned");
     if (nwords == 0)
         return GC_OK;
-    hipLaunchKernelGGL(k_byteunpack8, dim3(grid_for(nwords)), dim3(kBlock), 0, as_stream(stream), src, nwords, out);
+    if (aligned16(src) && aligned16(out))
+        hipLaunchKernelGGL(k_byteunpack8_v, dim3(grid_for((nwords >> 1) + 1)), dim3(kBlock), 0, as_stream(stream), src,
+                           nwords, out);
+    else
+        hipLaunchKernelGGL(k_byteunpack8, dim3(grid_for(nwords)), dim3(kBlock), 0, as_stream(stream), src, nwords,
+                           out);
     return launch_status("gc_byteunpack8");
 }
 

@@ -401,9 +401,13 @@ class Segments:
     reference's TensorBuffer (reducer.py:46-68) as a device table, so flatten,
     max-norm, decode and setgrad address the tensors in place.  Built once per
     parameter list (one small H2D copy) and reused.  It holds NO reference to
-    the tensors: a table is valid for any list whose key_of (data pointers,
-    sizes, dtype, device) equals self.key, which callers check on every use —
-    so a cached table never pins freed gradients in device memory."""
+    the tensors: a table is valid for any list whose key_of (data pointers and
+    sizes: exactly what the table records) equals self.key, which callers
+    check on every use — so a cached table never pins freed gradients in
+    device memory.  dtype, device and contiguity are validated when a table is
+    built (eligible_list); a list that reuses a table's pointers and sizes is
+    taken to be the same fp32 tensors (in-place metadata changes of a gradient,
+    e.g. t_() or set_() keeping the storage, are not supported)."""
 
     CHUNK_SHIFT = 12
 
@@ -440,11 +444,20 @@ class Segments:
 
     @staticmethod
     def key_of(tensors):
-        """(data pointers, sizes, dtypes, device indices) of a tensor list.
-        Per-attribute maps: a reducer step computes this for two lists of
-        ~50-160 tensors, and per-tensor tuples cost ~2x as much host time."""
-        return (tuple(map(torch.Tensor.data_ptr, tensors)), tuple(map(torch.Tensor.numel, tensors)),
-                frozenset(map(_dtype_of, tensors)), frozenset(map(torch.Tensor.get_device, tensors)))
+        """(data pointers, sizes) of a tensor list: what the table records.
+        Two attribute maps: a reducer step computes this for two lists of
+        ~50-160 tensors every step (the former key with dtype and device sets
+        cost ~4x as much host time)."""
+        return tuple(map(torch.Tensor.data_ptr, tensors)), tuple(map(torch.Tensor.numel, tensors))
+
+    @staticmethod
+    def eligible_list(tensors) -> bool:
+        """Contiguous fp32 tensors on one GPU (checked once per new table)."""
+        return (all(map(torch.Tensor.is_contiguous, tensors)) and frozenset(map(_dtype_of, tensors)) == _F32_SET
+                and len(devs := frozenset(map(torch.Tensor.get_device, tensors))) == 1 and min(devs) >= 0)
+
+
+_F32_SET = frozenset((torch.float32,))
 
 
 def segments_flatten_absmax(segs: Segments, flat: torch.Tensor | None = None, norm: torch.Tensor | None = None,
@@ -835,7 +848,7 @@ def _mt_bufs(device, path: str = "draws", stream=None):
     if b is None:
         with torch.cuda.stream(stream or torch.cuda.current_stream(device)):
             b = d[path] = (torch.empty(625, dtype=torch.int32).pin_memory(),
-                           [torch.empty(625, dtype=torch.int32).pin_memory() for _ in range(2)],
+                           [torch.empty(625, dtype=torch.int32).pin_memory() for _ in range(MT_MAX_SLOTS)],
                            torch.empty(625, dtype=torch.int32, device=device))
     return b
 
@@ -914,16 +927,38 @@ def qsgd_encode_torch(x, norm, bits, world=1, out=None, lanes=None) -> torch.Ten
 
 _MT_SIDE = {}  # device index -> (jump stream, generator stream) the torch-mode draws are made on
 _MT_LAST = {}  # device index -> (624 words, read index) last written back to torch
-_MT_SPEC = {}  # device index -> the speculative run of the next same-size call
+_MT_SPEC = {}  # device index -> the speculative runs of the next same-size calls (oldest first)
+_MT_SLOT = {}  # device index -> runs enqueued so far (a run's slot = that count mod the slots in use)
 _MT_END = {}   # (device index, end block B) -> device coefficients of x^(624 B - 1) mod P
 _MT_WSS = {}   # (device index, slot) -> workspace of the runs in that slot
 _MT_BUSY = {}  # (device index, slot) -> event after the last generators that read the slot's workspace
 _MT_PREV = {}  # device index -> the count of the last mt19937_draws call
-MT_SPECULATE = True  # generate the draws of the next same-size torch-mode call ahead (mt19937_draws)
-# a speculative run holds 4 * count bytes of draws + one generator workspace on the device until the
-# next call; it is started only after two calls in a row of the same count, and never above this count
+MT_SPECULATE = True  # generate the draws of the next same-size torch-mode calls ahead (mt19937_draws)
+# how many calls ahead: each speculative run holds 4 * count bytes of draws + one generator workspace
+# on the device until its call; runs start only after two calls in a row of the same count, and never
+# above MT_SPECULATE_MAX_DRAWS
+MT_SPECULATE_DEPTH = 2
 MT_SPECULATE_MAX_DRAWS = 1 << 30
+MT_MAX_SLOTS = 8  # workspace / pinned-state slots of the runs in flight (depth + 2 are used)
+# generators per pipelined run (mt19937_draws): None = mt_pipe_generators(count).  With the runs
+# made calls ahead, a generator's latency no longer bounds the call; fewer generators cut the
+# jump work, which shares the chip with the encodes
+MT_PIPE_GENERATORS = None
 MT_WAIT_NEXT_JUMPS = False  # consumers also wait for the speculative run's jumps (mt19937_draws)
+
+
+def mt_pipe_generators(count: int) -> int:
+    """Generators of one pipelined torch-mode run: about one per 780k draws
+    (128 for 1e8), at least the latency rule's count for small calls."""
+    if MT_PIPE_GENERATORS:
+        return int(MT_PIPE_GENERATORS)
+    return max(1, min(MT_MAX_GENERATORS, -(-count // 781_250)))
+
+
+def mt_pipe_generator_draws(count: int) -> int:
+    """Draws per generator J (a multiple of 624) of a pipelined run."""
+    g = mt_pipe_generators(count)
+    return 624 * max(1, -(-count // (624 * g)))
 
 
 def _mt_side(device):
@@ -987,7 +1022,7 @@ def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int) -> _MtRun:
     """Phase 1 on the jump stream: sequence + jumps + the end state (written
     over st_dev, gc_mt19937_generate_split_j) and its copy into hout[slot];
     phase 2 on the generator stream, after phase 1: the draws."""
-    J = mt_generator_draws(count)
+    J = mt_pipe_generator_draws(count)
     gens = -(-count // J)
     js, gs = _mt_side(dev)
     table, tgens = _mt_jump_table(dev, gens - 1, J, stream=js) if gens > 1 else (None, 0)
@@ -1036,69 +1071,84 @@ def mt19937_draws(count: int, device) -> torch.Tensor:
     phase 2 (generator stream) = the latency-bound generators.  The host waits
     only for the end state (phase 1 and a 2.5 KB copy), never for the draws or
     the caller's queued work; the caller's stream waits for the draws.  With
-    MT_SPECULATE the next call's run (same count, from this call's end state)
-    is enqueued right behind, so its jumps run beside this call's generators
-    and its generators beside this call's consumer; a speculative run is used
-    only if torch's generator is exactly where the previous call left it and
-    the count matches, else it is dropped and the state is sent to the device
-    again."""
+    MT_SPECULATE the runs of the next MT_SPECULATE_DEPTH same-size calls are
+    kept enqueued behind this one (each from the previous run's end state), so
+    a call's draws are made while the calls before it encode; a speculative
+    run is used only if torch's generator is exactly where the previous call
+    left it and the count matches, else every queued run is dropped and the
+    state is sent to the device again."""
     from .rng import set_torch_mt_state, torch_mt_state
 
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     if device.index is None:
         device = torch.device("cuda", torch.cuda.current_device())
+    d = device.index
     words, idx = torch_mt_state()
     js, _ = _mt_side(device)
     hin, hout, dst = _mt_bufs(device, "draws", stream=js)
     cur = torch.cuda.current_stream(device)
-    repeat = _MT_PREV.get(device.index) == count
-    _MT_PREV[device.index] = count
-    last = _MT_LAST.get(device.index)
+    repeat = _MT_PREV.get(d) == count
+    _MT_PREV[d] = count
+    last = _MT_LAST.get(d)
     untouched = last is not None and last[1] == idx and np.array_equal(last[0], words)
-    spec = _MT_SPEC.pop(device.index, None)
+    queue = _MT_SPEC.pop(d, [])
+    depth = max(0, min(int(MT_SPECULATE_DEPTH), MT_MAX_SLOTS - 2))
+    nslot = depth + 2
+
+    def next_slot():
+        k = _MT_SLOT.get(d, 0)
+        _MT_SLOT[d] = k + 1
+        return k % nslot
+
     if count == 0:
-        if spec is not None:  # a dropped run still moves dst on: send the state next time
-            _MT_LAST.pop(device.index, None)
+        if queue:  # dropped runs still moved dst on: send the state next time
+            _MT_LAST.pop(d, None)
         return torch.empty(0, dtype=torch.int32, device=device)
-    if spec is not None and untouched and spec.count == count:
-        run = spec
+    if queue and untouched and queue[0].count == count:
+        run = queue.pop(0)
     else:
-        if spec is not None or not untouched:  # dst is not torch's state: send it
+        if queue or not untouched:  # dst is not torch's state: send it
             with torch.cuda.stream(js):
                 h = hin.numpy().view(np.uint32)  # free: earlier copies from it were waited for
                 h[:624] = words
                 h[624] = idx
                 dst.copy_(hin, non_blocking=True)
-        run = _mt_enqueue(device, dst, count, int(idx), hout, spec.slot ^ 1 if spec is not None else 0)
-    spec_ok = MT_SPECULATE and repeat and count <= MT_SPECULATE_MAX_DRAWS
-    nxt = _mt_enqueue(device, dst, count, run.idx_end, hout, run.slot ^ 1) if spec_ok else None
+        queue = []
+        run = _mt_enqueue(device, dst, count, int(idx), hout, next_slot())
+    if MT_SPECULATE and repeat and count <= MT_SPECULATE_MAX_DRAWS:
+        tail = queue[-1] if queue else run
+        while len(queue) < depth:
+            tail = _mt_enqueue(device, dst, count, tail.idx_end, hout, next_slot())
+            queue.append(tail)
+    else:
+        queue = []  # (none were kept: a queue exists only after a repeat)
     cur.wait_event(run.done)
-    if nxt is not None and MT_WAIT_NEXT_JUMPS:
-        cur.wait_event(nxt.p1)
+    if queue and MT_WAIT_NEXT_JUMPS:
+        cur.wait_event(queue[0].p1)
     run.out.record_stream(cur)
-    if nxt is not None:
-        _MT_SPEC[device.index] = nxt
+    if queue:
+        _MT_SPEC[d] = queue
     run.state_ready.synchronize()
     new = hout[run.slot].numpy().view(np.uint32)
     w2, i2 = new[:624].copy(), int(new[624])
     set_torch_mt_state(w2, i2)
-    _MT_LAST[device.index] = (w2, i2)
+    _MT_LAST[d] = (w2, i2)
     return run.out
 
 
 def mt_release(device=None):
     """Drop the torch-mode state kept between calls on `device` (all devices
-    if None): the speculative run (4 * count bytes of draws), the generator
-    workspaces and the device state buffers.  Called when a generator leaves
-    torch mode; the next torch-mode call starts from torch's state again."""
+    if None): the speculative runs (4 * count bytes of draws each), the
+    generator workspaces and the device state buffers.  Called when a
+    generator leaves torch mode; the next torch-mode call starts from torch's
+    state again."""
     keys = [device.index] if device is not None else sorted({k for k in _MT_SPEC} | {k[0] for k in _MT_WSS}
                                                                | set(_MT_PIN) | set(_MT_LAST))
     for d in keys:
         for k in [k for k in _MT_BUSY if k[0] == d]:
             _MT_BUSY.pop(k).synchronize()  # queued generators may still read the workspaces
-        spec = _MT_SPEC.pop(d, None)
-        if spec is not None:
-            spec.done.synchronize()
+        for run in _MT_SPEC.pop(d, []):
+            run.done.synchronize()
         for k in [k for k in _MT_WSS if k[0] == d]:
             del _MT_WSS[k]
         _MT_PIN.pop(d, None)

@@ -88,10 +88,12 @@ class GlobalRandKMaxNormCompressor(QSGDMaxNormCompressor):
         rng = self._reserve(idx.numel(), 1, tensor.device)
         return self.backend.randk_encode_w1(tensor, idx, self._quantization_level, rng, out=out)
 
-    def encode_w1_segments(self, segs, idx, out=None):
-        """encode_w1 with the tensor given as the per-parameter tensors of segs."""
+    def encode_w1_segments(self, segs, idx, out=None, xk=None, norm=None):
+        """encode_w1 with the tensor given as the per-parameter tensors of segs
+        (out / xk / norm: preallocated words, gathered subset and norm)."""
         rng = self._reserve(idx.numel(), 1, segs.device)
-        return self.backend.randk_encode_w1_segments(segs, idx, self._quantization_level, rng, out=out)
+        return self.backend.randk_encode_w1_segments(segs, idx, self._quantization_level, rng, xk=xk, norm=norm,
+                                                     out=out)
 
     def decode_scatter_segments(self, norm, words, idx, segs, world=1, alpha=1.0):
         """decode(..., idx=idx) writing element idx[i] straight into its tensor."""

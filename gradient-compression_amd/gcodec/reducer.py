@@ -112,20 +112,23 @@ class Reducer:
         None when the codec has none or a tensor is not contiguous fp32 on the
         GPU — then the reducer takes the TensorBuffer path."""
         make = getattr(self._codec, "Segments", None)
-        tensors = list(tensors)
-        if not self._fused or make is None or not tensors:
+        if not self._fused or make is None:
             return None
-        if not all(map(torch.Tensor.is_contiguous, tensors)):
+        if not isinstance(tensors, (list, tuple)):
+            tensors = list(tensors)
+        if not tensors:
             return None
-        # keyed by the tensors' data pointers and sizes: a table stays valid while
-        # the list it describes lives at the same addresses (the caching
-        # allocator usually hands a re-created p.grad the same block every step);
-        # LRU, so the stable send-buffer entry survives reallocated grad lists
+        # keyed by the tensors' data pointers and sizes (what the table holds): a
+        # table stays valid while the list it describes lives at the same
+        # addresses (the caching allocator usually hands a re-created p.grad the
+        # same block every step); LRU, so the stable send-buffer entry survives
+        # reallocated grad lists.  fp32 / one GPU / contiguous is checked when a
+        # table is built (Segments.eligible_list), not on every hit.
         key = make.key_of(tensors)
-        if key[2] != _F32_ONLY or len(key[3]) != 1 or min(key[3]) < 0:  # fp32, one GPU
-            return None
         segs = self._seg_cache.get(key)
         if segs is None:
+            if not make.eligible_list(tensors):
+                return None
             if len(self._seg_cache) >= self.SEG_CACHE:
                 self._seg_cache.popitem(last=False)
             segs = self._seg_cache[key] = make(tensors)
@@ -151,9 +154,6 @@ class Reducer:
             if local is None or idx is not None:
                 local = self._codec.absmax(flat.buffer, idx=idx)
             return self._all_reduce(local, dist.ReduceOp.MAX)
-
-
-_F32_ONLY = frozenset((torch.float32,))
 
 
 class TensorBuffer:
@@ -234,6 +234,7 @@ class GlobalRandKMaxNormReducer(Reducer):
         self._seed = seed
         self._K = K
         self._indices_queue = []
+        self._bufs = {}
 
     def _next_indices(self, n, device):
         """reducer.py:717-722: on refill set_seed, torch.randperm(n) (CPU
@@ -250,6 +251,23 @@ class GlobalRandKMaxNormReducer(Reducer):
             self._indices_queue = list(perm.split(self._K))
         return self._indices_queue.pop()
 
+    def _step_buffers(self, k, device, world):
+        """(gathered subset, norm, packed words) for a K-subset, allocated once
+        per (K, device, W) and reused every step: the kernels that read the
+        previous step's buffers are queued ahead on the same stream, and the
+        collectives are waited for in stream order (a fresh torch.empty of each
+        cost host time every step; the refill's last chunk has its own K)."""
+        key = (k, device, world)
+        b = self._bufs.get(key)
+        if b is None:
+            lanes = self._codec.qsgd_layout(k, self._quantization_level, world)
+            if len(self._bufs) >= 4:
+                self._bufs.clear()
+            b = self._bufs[key] = (torch.empty(k, dtype=torch.float32, device=device),
+                                   torch.empty(1, dtype=torch.float32, device=device),
+                                   torch.empty(lanes.plane_words, dtype=torch.int32, device=device))
+        return b
+
     def _randk_compressor(self):
         return self._compressor(C.GlobalRandKMaxNormCompressor, self._quantization_level)
 
@@ -263,15 +281,16 @@ class GlobalRandKMaxNormReducer(Reducer):
         idx = self._next_indices(in_segs.n, in_segs.device)
         k = idx.numel()
         codec = self._codec
+        xk, norm, words = self._step_buffers(k, in_segs.device, W)
         if codec.randk_fused_ok(k, self._quantization_level, W):
             with self._timer("reduce.compress", verbosity=2):
-                words, norm = comp.encode_w1_segments(in_segs, idx)
+                words, norm = comp.encode_w1_segments(in_segs, idx, out=words, xk=xk, norm=norm)
         else:
             with self._timer("reduce.norm", verbosity=2):
-                xk, local = codec.randk_gather_absmax_segments(in_segs, idx)
+                xk, local = codec.randk_gather_absmax_segments(in_segs, idx, xk=xk, norm=norm)
                 norm = self._all_reduce(local, dist.ReduceOp.MAX)
             with self._timer("reduce.compress", verbosity=2):
-                words = comp.encode(norm, xk, world=W)
+                words = comp.encode(norm, xk, world=W, out=words)
         with self._timer("reduce.reduce.vector", verbosity=2):
             self._all_reduce(words)
         bits = self.n_bits(norm) + self.n_bits(words)

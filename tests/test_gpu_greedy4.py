@@ -2,8 +2,8 @@
 bitpacking format (extensions/Extension CPU/bitpacking.cpp:5-124), produced
 by a scan over segment tables.  Bit-exact against the reference extension's
 own known-answer vectors (tests/golden/packers.npz) and against the oracle /
-host packer on inputs that stress the boundaries (16-position segments,
-4096-position tiles, 256-tile groups, 64-group chunks of the top walk):
+host packer on inputs that stress the boundaries (32-position segments,
+8192-position tiles, 256-tile groups, 64-group chunks of the top walk):
 all-mode-0 runs, all-mode-3 runs, mixes, ragged ends, and the QSGDBP call
 site's ResNet50 bucket (23,520,842 sign bits and 4-bit magnitudes)."""
 import os
@@ -54,15 +54,15 @@ def _inputs():
     yield "edges", a
     yield "qsgd4", np.abs(rng.normal(0, 4, 3_000_000)).clip(0, 15).astype(np.int32)
     # runs that flip modes right at segment / tile boundaries, unaligned starts
-    b = np.zeros(4096 * 5 + 9, np.int32)
+    b = np.zeros(8192 * 5 + 9, np.int32)
     for c in range(1, 5):
-        b[4096 * c - 16:4096 * c + 1] = 130
+        b[8192 * c - 16:8192 * c + 1] = 130
         b[4096 * c + 7:4096 * c + 8] = 17
     b[::16] = 5
     yield "tile_edges", b
-    yield "mode3_all", rng.integers(128, 256, 4096 * 3 + 31).astype(np.int32)
-    # more than one 64-group chunk of the top walk (> 64 x 256 x 4096 positions)
-    yield "chunks2", rng.choice([0, 1, 2, 3, 7, 15], 70_000_000, p=[.4, .2, .15, .15, .05, .05]).astype(np.int32)
+    yield "mode3_all", rng.integers(128, 256, 8192 * 3 + 31).astype(np.int32)
+    # more than one 64-group chunk of the top walk (> 64 x 256 x 8192 positions)
+    yield "chunks2", rng.choice([0, 1, 2, 3, 7, 15], 140_000_000, p=[.4, .2, .15, .15, .05, .05]).astype(np.int32)
 
 
 @pytest.mark.parametrize("name,src", list(_inputs()), ids=lambda v: v if isinstance(v, str) else "")

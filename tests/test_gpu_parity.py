@@ -612,6 +612,32 @@ def test_bytepack_kernels_match_reference_vectors():
         assert bits_eq(codec.byteunpack8(w).cpu().numpy(), z[f"bp/{nm}/unpacked"])
 
 
+@pytest.mark.parametrize("dt", [torch.int8, torch.int32, torch.int64])
+@pytest.mark.parametrize("n,shift", [(16, 0), (17, 0), (33, 0), (1_000_003, 0), (23_520_842, 0), (1001, 1), (4099, 3)])
+def test_bytepack_vector_and_scalar_paths_match_host(dt, n, shift):
+    """The 16-byte vector kernels (aligned src / out) and the scalar kernels
+    (shifted src) against the host byte packer (Extension CPU BP/bytepacking.cpp:6-64
+    restated, pinned by the reference vectors in test_capi), for int8 / int32 /
+    int64 sources, ragged n, and the ResNet50 bucket size."""
+    from gcodec.packing import bytepacking
+    rng = np.random.default_rng(n + shift)
+    a = rng.integers(-300, 300, n + shift).astype(np.int64)
+    src = torch.from_numpy(a).to(dt)
+    d = src.to(DEV)[shift:]
+    host = bytepacking.packing(src[shift:].to(torch.int64))
+    w = codec.bytepack8(d)
+    assert torch.equal(w.cpu(), host)
+    u = codec.byteunpack8(w)
+    assert torch.equal(u.cpu(), bytepacking.unpacking(host))
+    if shift == 0:  # unpack into a shifted (8-byte aligned) output: the scalar path
+        out = torch.empty(8 * w.numel() + 8, dtype=torch.int8, device=DEV)[8:]
+        from gcodec import _lib
+        import ctypes as C
+        assert _lib.load().gc_byteunpack8(C.c_void_p(w.data_ptr()), w.numel(), C.c_void_p(out.data_ptr()),
+                                          codec._stream(DEV)) == 0
+        assert torch.equal(out.cpu(), u.cpu())
+
+
 # --------------------------------------------------------------------------- full-size properties
 def test_full_size_properties_100m():
     """BASELINE config 2 size: no oracle run at 1e8; size-independent checks —

@@ -1,19 +1,24 @@
-"""Per-call time of the torch-parity (MT19937) encode at 1e8, 4-bit, W = 1:
-the draw-buffer path (compressor / reducer default) and the fused generator
-quantize, each over REPS back-to-back calls (includes the torch state hand-off)."""
+"""Per-call time of the torch-parity (MT19937) encode at 1e8, 4-bit, W = 1,
+back to back (REPS calls, the fastest of RUNS loops; includes the torch state
+hand-off), swept over the pipelined run's generator count and the
+speculation depth (codec.MT_PIPE_GENERATORS / MT_SPECULATE_DEPTH), encode
+only and absmax + encode; then the Philox step in the same harness, and the
+fused generator-quantize path for contrast.
+
+    python tools/time_torch_mode.py [G,G,...] [D,D,...]
+"""
 import os
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gradient-compression_amd"))
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import gcodec  # noqa: E402
 from gcodec import codec  # noqa: E402
 
-REPS = 20
+REPS, RUNS = 20, 3
 dev = torch.device("cuda", 0)
 n = 100_000_000
 x = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(1)).mul_(0.01)
@@ -21,58 +26,53 @@ nm = codec.absmax(x)
 lanes = codec.qsgd_layout(n, 4, 1)
 words = torch.empty(lanes.plane_words, dtype=torch.int32, device=dev)
 gen = gcodec.Generator(0, "torch")
+px = gcodec.Generator(5, "philox")
 torch.manual_seed(42)
-for f in ("buffer", "fused", "buffer", "fused"):
-    call = ((lambda: codec.qsgd_encode(x, nm, 4, gen.reserve(n), 1, out=words, lanes=lanes)) if f == "buffer"
-            else (lambda: codec.qsgd_encode_torch(x, nm, 4, 1, out=words, lanes=lanes)))
-    call()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(REPS):
-        call()
-    torch.cuda.synchronize()
-    print(f"{f}: {(time.perf_counter() - t0) / REPS * 1e3:.3f} ms per call")
+GS = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 96, 128, 192, 256, 383]
+DS = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 3]
 
-# generator length: the package's per-count J against the fixed default
-st = torch.from_numpy(codec.mt19937_seed_state(7).view(np.int32)).to(dev)
-for cnt in (10_000_000, 23_520_842 * 2, 100_000_000):
-    out = torch.empty(cnt, dtype=torch.int32, device=dev)
-    for J in (gcodec._lib.GC_MT_JUMP_DRAWS, codec.mt_generator_draws(cnt)):
-        codec.mt19937_generate(st, cnt, out=out, J=J)
-        torch.cuda.synchronize()
+
+def per_call(fn):
+    for _ in range(6):
+        fn()
+    torch.cuda.synchronize()
+    best = []
+    for _ in range(RUNS):
         t0 = time.perf_counter()
         for _ in range(REPS):
-            codec.mt19937_generate(st, cnt, out=out, J=J)
+            fn()
         torch.cuda.synchronize()
-        print(f"mt19937 {cnt} draws, J = {J} ({-(-cnt // J)} generators): "
-              f"{(time.perf_counter() - t0) / REPS * 1e3:.3f} ms")
+        best.append((time.perf_counter() - t0) / REPS * 1e3)
+    return min(best)
 
-# the draw-buffer path with the generators on the side stream: the encode of
-# call i runs under the generation of call i + 1, so the balance of jump and
-# generator time moves; per-call time for a few generator counts
-orig = codec.mt_generator_draws
-for G in (256, 320, 383, 448, 512, 640):
-    codec.mt_generator_draws = lambda c, G=G: 624 * max(1, -(-c // (624 * G)))
-    call = lambda: codec.qsgd_encode(x, nm, 4, gen.reserve(n), 1, out=words, lanes=lanes)  # noqa: E731
-    call()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(REPS):
-        call()
-    torch.cuda.synchronize()
-    print(f"buffer path, {G} generators: {(time.perf_counter() - t0) / REPS * 1e3:.3f} ms per call")
-codec.mt_generator_draws = orig
 
-# speculation on / off, and what the consumer waits for (the next run's jumps
-# or just this run's draws)
-for spec, wj in ((True, True), (True, False), (False, False)):
-    codec.MT_SPECULATE, codec.MT_WAIT_NEXT_JUMPS = spec, wj
-    call = lambda: codec.qsgd_encode(x, nm, 4, gen.reserve(n), 1, out=words, lanes=lanes)  # noqa: E731
-    call()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(REPS):
-        call()
-    torch.cuda.synchronize()
-    print(f"buffer path, speculate={spec}, wait next jumps={wj}: {(time.perf_counter() - t0) / REPS * 1e3:.3f} ms per call")
-codec.MT_SPECULATE, codec.MT_WAIT_NEXT_JUMPS = True, False
+def enc():
+    codec.qsgd_encode(x, nm, 4, gen.reserve(n), 1, out=words, lanes=lanes)
+
+
+def step():
+    codec.absmax(x, out=nm)
+    enc()
+
+
+for G in GS:
+    for D in DS:
+        codec.MT_PIPE_GENERATORS = G or None
+        codec.MT_SPECULATE_DEPTH = D
+        codec.mt_release()
+        e, s = per_call(enc), per_call(step)
+        print(f"generators {G or codec.mt_pipe_generators(n)} depth {D}: encode {e:.3f} ms, absmax + encode "
+              f"{s:.3f} ms per call", flush=True)
+codec.MT_PIPE_GENERATORS, codec.MT_SPECULATE_DEPTH = None, 2
+codec.mt_release()
+pe = per_call(lambda: codec.qsgd_encode(x, nm, 4, px.reserve(n), 1, out=words, lanes=lanes))
+
+
+def pstep():
+    codec.absmax(x, out=nm)
+    codec.qsgd_encode(x, nm, 4, px.reserve(n), 1, out=words, lanes=lanes)
+
+
+print(f"philox: encode {pe:.3f} ms, absmax + encode {per_call(pstep):.3f} ms per call", flush=True)
+print(f"fused generator-quantize: {per_call(lambda: codec.qsgd_encode_torch(x, nm, 4, 1, out=words, lanes=lanes)):.3f}"
+      " ms per call", flush=True)
