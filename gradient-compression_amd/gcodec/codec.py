@@ -925,7 +925,7 @@ def qsgd_encode_torch(x, norm, bits, world=1, out=None, lanes=None) -> torch.Ten
     return out
 
 
-_MT_SIDE = {}  # device index -> (jump stream, generator stream) the torch-mode draws are made on
+_MT_SIDE = {}  # device index -> (jump stream, [generator stream per slot]) the torch-mode draws are made on
 _MT_LAST = {}  # device index -> (624 words, read index) last written back to torch
 _MT_SPEC = {}  # device index -> the speculative runs of the next same-size calls (oldest first)
 _MT_SLOT = {}  # device index -> runs enqueued so far (a run's slot = that count mod the slots in use)
@@ -962,16 +962,16 @@ def mt_pipe_generator_draws(count: int) -> int:
 
 
 def _mt_side(device):
-    """Two high-priority streams: the jumps (LDS-bound; they also produce the
-    end state) and the generators (latency-bound).  The draw generation is the
-    serial chain of the torch-mode encode; the encodes it overlaps fill the
-    CUs it leaves idle, and the next call's jumps run beside this call's
-    generators."""
+    """High-priority streams: one for the jumps (LDS-bound; they also produce
+    the end state, so run c+1's jumps follow run c's) and one per slot for the
+    generators (latency-bound), so the generators of the runs in flight run
+    side by side instead of one after another.  The encodes the draws feed
+    fill the CUs they leave idle."""
     s = _MT_SIDE.get(device.index)
     if s is None:
         lo, hi = torch.cuda.Stream.priority_range()
         s = _MT_SIDE[device.index] = (torch.cuda.Stream(device, priority=min(lo, hi)),
-                                      torch.cuda.Stream(device, priority=min(lo, hi)))
+                                      [torch.cuda.Stream(device, priority=min(lo, hi)) for _ in range(MT_MAX_SLOTS)])
     return s
 
 
@@ -1006,7 +1006,7 @@ def _mt_ws_slot(dev, slot: int, count: int, J: int, js) -> torch.Tensor:
         _MT_WSS.pop(key, None)
         with torch.cuda.stream(js):
             ws = _MT_WSS[key] = torch.empty(need, dtype=torch.uint8, device=dev)
-        ws.record_stream(_mt_side(dev)[1])
+        ws.record_stream(_mt_side(dev)[1][slot])
     return ws
 
 
@@ -1024,7 +1024,8 @@ def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int) -> _MtRun:
     phase 2 on the generator stream, after phase 1: the draws."""
     J = mt_pipe_generator_draws(count)
     gens = -(-count // J)
-    js, gs = _mt_side(dev)
+    js, gss = _mt_side(dev)
+    gs = gss[slot]
     table, tgens = _mt_jump_table(dev, gens - 1, J, stream=js) if gens > 1 else (None, 0)
     block = (idx + count - 1) // 624
     end = _mt_end_coef(dev, block)

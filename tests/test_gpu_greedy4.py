@@ -3,7 +3,7 @@ bitpacking format (extensions/Extension CPU/bitpacking.cpp:5-124), produced
 by a scan over segment tables.  Bit-exact against the reference extension's
 own known-answer vectors (tests/golden/packers.npz) and against the oracle /
 host packer on inputs that stress the boundaries (32-position segments,
-8192-position tiles, 256-tile groups, 64-group chunks of the top walk):
+8192-position tiles, 128-tile groups, the top walk past 64 groups):
 all-mode-0 runs, all-mode-3 runs, mixes, ragged ends, and the QSGDBP call
 site's ResNet50 bucket (23,520,842 sign bits and 4-bit magnitudes)."""
 import os
@@ -61,7 +61,7 @@ def _inputs():
     b[::16] = 5
     yield "tile_edges", b
     yield "mode3_all", rng.integers(128, 256, 8192 * 3 + 31).astype(np.int32)
-    # more than one 64-group chunk of the top walk (> 64 x 256 x 8192 positions)
+    # more groups than the emit walks itself (> 64): k_g4p_top, over two 128-group chunks (> 128 x 128 x 8192)
     yield "chunks2", rng.choice([0, 1, 2, 3, 7, 15], 140_000_000, p=[.4, .2, .15, .15, .05, .05]).astype(np.int32)
 
 

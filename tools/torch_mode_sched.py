@@ -47,7 +47,8 @@ def per_call(caller=None):
 for js_p, gs_p, cs_p in ((HIGH, HIGH, None), (HIGH, NORM, None), (NORM, HIGH, None), (NORM, NORM, None),
                          (HIGH, HIGH, HIGH), (NORM, HIGH, HIGH), (HIGH, NORM, HIGH)):
     torch.cuda.synchronize()
-    codec._MT_SIDE[dev.index] = (torch.cuda.Stream(dev, priority=js_p), torch.cuda.Stream(dev, priority=gs_p))
+    codec._MT_SIDE[dev.index] = (torch.cuda.Stream(dev, priority=js_p),
+                                 [torch.cuda.Stream(dev, priority=gs_p) for _ in range(codec.MT_MAX_SLOTS)])
     codec._MT_SPEC.pop(dev.index, None)
     codec._MT_LAST.pop(dev.index, None)  # the dropped run moved the device state: send torch's again
     caller = torch.cuda.Stream(dev, priority=cs_p) if cs_p is not None else None
