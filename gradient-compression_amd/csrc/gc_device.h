@@ -136,11 +136,105 @@ __device__ __forceinline__ uint4 philox4x32_10_g(uint32_t g, uint32_t y, uint32_
     return c;
 }
 
+// ---------------------------------------------------------------------------
+// KIND 2: the dense two-level Philox stream of the 2-level multi-scale /
+// two-scale codecs (levels 0 and 1 only).  The 16 draws of elements
+// 8g..8g+7 at both levels are 24-bit fields of 3 Philox4x32-10 blocks,
+// counter (lo32 g, (hi16 g) | b << 16, lo32 offset, hi32 offset), b = 0, 1, 2,
+// key = seed: with w_0..w_11 the blocks' words in order, draw (level l,
+// element 8g + e) is bits 24 (8 l + e) .. +23 of w_0 | w_1 << 32 | ... .  The
+// rounding reads only the low 24 bits of a draw (r & 0xFFFFFF), so 16 draws
+// cost 3 blocks instead of 4 (ms2_octet: 1.5 blocks per 4 elements and level
+// pair).  Quad h (elements 8g + 4h ..) at level l is the 3 words from
+// w_(6l + 3h): draws (a, alignbit(b, a, 24), alignbit(c, b, 16), c >> 8)
+// (the top byte of the first three is not part of the draw).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 ms2_quad(uint32_t a, uint32_t b, uint32_t c)
+{
+    return make_uint4(a, __builtin_amdgcn_alignbit(b, a, 24), __builtin_amdgcn_alignbit(c, b, 16), c >> 8);
+}
+
+template <int IMPL = GC_PHILOX_IMPL>
+__device__ __forceinline__ uint4 ms2_block(const RngArgs &r, uint64_t g, uint32_t b)
+{
+    if constexpr (IMPL == 1) {
+        if (g < (1ull << 32))
+            return philox4x32_10_g((uint32_t)g, b << 16, (uint32_t)r.offset, (uint32_t)(r.offset >> 32),
+                                   (uint32_t)r.seed, (uint32_t)(r.seed >> 32));
+    }
+    uint4 c;
+    c.x = (uint32_t)g;
+    c.y = ((uint32_t)(g >> 32) & 0xffffu) | (b << 16);
+    c.z = (uint32_t)r.offset;
+    c.w = (uint32_t)(r.offset >> 32);
+    return philox4x32_10<IMPL>(c, (uint32_t)r.seed, (uint32_t)(r.seed >> 32));
+}
+
+// both levels' draws of the 8 elements 8g..8g+7: d[l][h] = quad h at level l
+__device__ __forceinline__ void ms2_octet(const RngArgs &r, uint64_t g, uint4 (&d)[2][2])
+{
+    const uint4 b0 = ms2_block(r, g, 0), b1 = ms2_block(r, g, 1), b2 = ms2_block(r, g, 2);
+    d[0][0] = ms2_quad(b0.x, b0.y, b0.z);
+    d[0][1] = ms2_quad(b0.w, b1.x, b1.y);
+    d[1][0] = ms2_quad(b1.z, b1.w, b2.x);
+    d[1][1] = ms2_quad(b2.y, b2.z, b2.w);
+}
+
+// one level's draws of the 8 elements (2 blocks: 0 and 1, or 1 and 2)
+__device__ __forceinline__ void ms2_octet_level(const RngArgs &r, uint64_t g, uint32_t level, uint4 (&d)[2])
+{
+    if (level == 0) {
+        const uint4 b0 = ms2_block(r, g, 0), b1 = ms2_block(r, g, 1);
+        d[0] = ms2_quad(b0.x, b0.y, b0.z);
+        d[1] = ms2_quad(b0.w, b1.x, b1.y);
+    } else {
+        const uint4 b1 = ms2_block(r, g, 1), b2 = ms2_block(r, g, 2);
+        d[0] = ms2_quad(b1.z, b1.w, b2.x);
+        d[1] = ms2_quad(b2.y, b2.z, b2.w);
+    }
+}
+
 // Four draws for elements i0..i0+3 (i0 % 4 == 0) at scale `level`.
+// KIND 0: Philox, one block per quad and level; 1: a draw stream; 2: the
+// dense two-level Philox stream above (one or two blocks per quad and level:
+// the generic kernels' path; the octet kernels of ms_fast.h share blocks);
+// 3: a draw stream packed to 24 bits (GC_RNG_STREAM24).
 template <int KIND, int IMPL = GC_PHILOX_IMPL>
 __device__ __forceinline__ uint4 draws4(const RngArgs &r, uint32_t level, uint64_t i0)
 {
-    if constexpr (KIND == 0) {
+    if constexpr (KIND == 2) {
+        // block numbers stay wave-uniform (philox4x32_10_g keeps y on the
+        // scalar unit); the quad half h = bit 2 of i0 is per lane
+        const uint64_t g = i0 >> 3;
+        const bool h = (i0 & 4u) != 0;
+        if (level == 0) {  // words 0-2 (h = 0) or 3-5
+            const uint4 a = ms2_block<IMPL>(r, g, 0);
+            if (!h)
+                return ms2_quad(a.x, a.y, a.z);
+            const uint4 b = ms2_block<IMPL>(r, g, 1);
+            return ms2_quad(a.w, b.x, b.y);
+        }
+        const uint4 c = ms2_block<IMPL>(r, g, 2);  // level 1: words 6-8 (h = 0) or 9-11
+        if (h)
+            return ms2_quad(c.y, c.z, c.w);
+        const uint4 b = ms2_block<IMPL>(r, g, 1);
+        return ms2_quad(b.z, b.w, c.x);
+    } else if constexpr (KIND == 3) {
+        // GC_RNG_STREAM24: draw j = bytes 3j .. 3j+2; a quad's 12 bytes start
+        // 4-byte aligned (level n + i0 is a multiple of 4: one level)
+        const uint64_t j = (uint64_t)level * r.n + i0;
+        const uint64_t left = i0 < r.n ? r.n - i0 : 0;
+        const uint8_t *b = reinterpret_cast<const uint8_t *>(r.stream) + 3 * j;
+        if (left >= 4) {
+            const uint3 w = *reinterpret_cast<const uint3 *>(b);
+            return ms2_quad(w.x, w.y, w.z);
+        }
+        uint4 d = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t *dp = &d.x;
+        for (uint32_t e = 0; e < (uint32_t)left; ++e)
+            dp[e] = b[3 * e] | (uint32_t)b[3 * e + 1] << 8 | (uint32_t)b[3 * e + 2] << 16;
+        return d;
+    } else if constexpr (KIND == 0) {
         const uint64_t g = i0 >> 2;
         uint4 c;
         c.x = (uint32_t)g;
@@ -173,10 +267,13 @@ __device__ __forceinline__ uint4 draws4(const RngArgs &r, uint32_t level, uint64
 template <int KIND>
 __device__ __forceinline__ uint32_t draw1(const RngArgs &r, uint32_t level, uint64_t i)
 {
-    if constexpr (KIND == 0) {
-        const uint4 d = draws4<0>(r, level, i & ~(uint64_t)3);
+    if constexpr (KIND == 0 || KIND == 2) {
+        const uint4 d = draws4<KIND>(r, level, i & ~(uint64_t)3);
         const uint32_t j = (uint32_t)(i & 3);
         return j == 0 ? d.x : (j == 1 ? d.y : (j == 2 ? d.z : d.w));
+    } else if constexpr (KIND == 3) {
+        const uint8_t *b = reinterpret_cast<const uint8_t *>(r.stream) + 3 * ((uint64_t)level * r.n + i);
+        return b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16;
     } else {
         return r.stream[(uint64_t)level * r.n + i];
     }

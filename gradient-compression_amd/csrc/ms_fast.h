@@ -70,6 +70,11 @@ enum : int {
     MSV_DEFER = 16,     // lab: the one-pass kernel with the generic path deferred to after the plane loop
     MSV_EAGER0 = 32,    // the one-pass fast path computes level 0's draws for every quad, interleaved
                         // with the upper levels' (no wave-level branch; same draws and outputs)
+    MSV_PREFETCH = 64,  // octet one-pass kernel: the next plane's loads are issued before this plane's
+                        // math (the product: 29.1 against 31.6 us, profiles/r04n_lab_ms.log)
+    MSV_ROLL = 128,     // octet mask / select kernels: the plane loop is not unrolled (the product:
+                        // fewer VGPRs, more waves; mask 22.7 against 27.4 us, with the q cache 32.4
+                        // against 45.0 us, profiles/r04n_lab_ms.log)
 };
 
 template <int KIND, int VAR>
@@ -299,10 +304,12 @@ __device__ __forceinline__ uint4 cache_cells(const uint2 &u)
 // the select would compute at that level.  The fast and generic paths are
 // whole branches (each with its own draws), so the common fast path carries
 // no per-level divergence.
-template <int KIND, int NL, int VAR = 0, bool CACHE = false>
-__device__ __forceinline__ void mask_plane_v(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
+// DR: the draws, dr(l) = level l's uint4 for elements i0..i0+3 (ms_draws4,
+// or an octet kernel's shared blocks)
+template <int NL, int VAR, bool CACHE, typename DR>
+__device__ __forceinline__ void mask_plane_d(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
                                              uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
-                                             const RngArgs &rng, uint32_t bit, uint4 (&mb)[NL - 1], int32_t cq = 0,
+                                             const DR &dr, uint32_t bit, uint4 (&mb)[NL - 1], int32_t cq = 0,
                                              uint32_t cb = 0, uint4 *cv = nullptr)
 {
     RangeLo rg;
@@ -321,7 +328,7 @@ __device__ __forceinline__ void mask_plane_v(const float4 &v, uint32_t n, uint32
         bool k0 = false, k1 = false, k2 = false, k3 = false;  // some level >= l qualifies
 #pragma unroll
         for (int l = NL - 1; l >= (CACHE ? 0 : 1); --l) {
-            const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
+            const uint4 r = dr(l);
             const gc_f2 S = {fa.S24[l], fa.S24[l]};
             const gc_f2 a = q01 * S, b = q23 * S;
             const int32_t t0 = ms_t(a.x, r.x), t1 = ms_t(a.y, r.y), t2 = ms_t(b.x, r.z), t3 = ms_t(b.y, r.w);
@@ -363,7 +370,7 @@ __device__ __forceinline__ void mask_plane_v(const float4 &v, uint32_t n, uint32
         uint4 m = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (int l = CACHE ? 0 : 1; l < NL; ++l) {
-            const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
+            const uint4 r = dr(l);
             const float s = lv.s[l];
             const int32_t x0 = xi_from_q(ql.x, s, r.x), x1 = xi_from_q(ql.y, s, r.y);
             const int32_t x2 = xi_from_q(ql.z, s, r.z), x3 = xi_from_q(ql.w, s, r.w);
@@ -396,6 +403,17 @@ __device__ __forceinline__ void mask_plane_v(const float4 &v, uint32_t n, uint32
     }
     if constexpr (CACHE)
         *cv = c;  // sum_l -q_l << (l cb): the caller's ms_cells turns it into the cells
+}
+
+template <int KIND, int NL, int VAR = 0, bool CACHE = false>
+__device__ __forceinline__ void mask_plane_v(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                             uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                             const RngArgs &rng, uint32_t bit, uint4 (&mb)[NL - 1], int32_t cq = 0,
+                                             uint32_t cb = 0, uint4 *cv = nullptr)
+{
+    mask_plane_d<NL, VAR, CACHE>(v, n, i0, dv, lo2, hi2, lv, fa,
+                                 [&](int l) { return ms_draws4<KIND, VAR>(rng, (uint32_t)l, i0); }, bit, mb, cq, cb,
+                                 cv);
 }
 
 template <int KIND, int NL, int VAR = 0, bool CACHE = false>
@@ -467,18 +485,14 @@ __device__ __forceinline__ uint32_t ms_lane(float x, float Ls, uint32_t r, int32
     return lane_of_t(x, ms_t(Ls, r), qmax);
 }
 
-// lane values of 4 elements at their common levels (0 past n)
-template <int KIND, int NL, int VAR = 0>
-__device__ __forceinline__ uint4 select_plane(const float *__restrict__ x, uint32_t n, uint32_t i0,
-                                              const MaskArg &mk, const FastDiv &fd, const DivNorm &dv, uint32_t lo2,
-                                              uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
-                                              const RngArgs &rng, int32_t qmax)
+// lane values of 4 elements at levels m, with their draws r at those levels
+template <int NL, int VAR = 0>
+__device__ __forceinline__ uint4 select_lanes(const float4 &v, const uint4 &m, const uint4 &r, uint32_t n, uint32_t i0,
+                                              const DivNorm &dv, uint32_t lo2, const LevelsArg &lv,
+                                              const MsFastArg &fa, int32_t qmax)
 {
-    const float4 v = load4_nt_tail<0>(x, i0, n);
-    const uint4 m = mask_levels4_fast<NL>(mk, fd, i0);
     RangeLo rg;
     rg.add4(v);
-    const uint4 r = draws_at<KIND, NL, VAR>(rng, i0, m);  // the selected level's draw, either path
     uint4 ln;
     const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
     if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.tiny(lo2) && q_in_unit(q01, q23)))) {
@@ -506,6 +520,19 @@ __device__ __forceinline__ uint4 select_plane(const float *__restrict__ x, uint3
         ln.w = i0 + 3 < n ? ln.w : 0u;
     }
     return ln;
+}
+
+// lane values of 4 elements at their common levels (0 past n)
+template <int KIND, int NL, int VAR = 0>
+__device__ __forceinline__ uint4 select_plane(const float *__restrict__ x, uint32_t n, uint32_t i0,
+                                              const MaskArg &mk, const FastDiv &fd, const DivNorm &dv, uint32_t lo2,
+                                              uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                              const RngArgs &rng, int32_t qmax)
+{
+    const float4 v = load4_nt_tail<0>(x, i0, n);
+    const uint4 m = mask_levels4_fast<NL>(mk, fd, i0);
+    const uint4 r = draws_at<KIND, NL, VAR>(rng, i0, m);  // the selected level's draw, either path
+    return select_lanes<NL, VAR>(v, m, r, n, i0, dv, lo2, lv, fa, qmax);
 }
 
 // decoded floats of 4 elements (compressors.py:819-826 order 0; 668-680 order 1) * alpha
@@ -553,7 +580,7 @@ constexpr uint32_t kMsQuadsPerBlock = 64;  // word quads per block (one per lane
 // mask encode: thermometer fields of the resolution level (compressors.py:799-807)
 // ---------------------------------------------------------------------------
 // CBY = 0: mask only; 1 / 2: also the q cache cells (CBY bytes per element)
-// GC_MS_WPE (measurement builds only, tools/Makefile lab_ms_w8): pin the
+// GC_MS_WPE (measurement builds only: hipcc -DGC_MS_WPE=N of tools/lab_ms.hip): pin the
 // Philox-bound kernels' occupancy with amdgpu_waves_per_eu
 #ifdef GC_MS_WPE
 #define GC_MS_OCC __attribute__((amdgpu_waves_per_eu(GC_MS_WPE, GC_MS_WPE)))
@@ -803,19 +830,19 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
 // level"; a level is only ever chosen with xi <= maxv <= 127, so the chosen
 // T >> 24 is a sign-extended byte.  -q = (T >> 24) * sign(x) (0 for +-0,
 // whose T is >= 0 anyway).
-template <int KIND, int NL, int VAR = 0>
-__device__ __forceinline__ void fused_quad_fast(const float4 &v, const gc_f2 &q01, const gc_f2 &q23, uint32_t i0,
-                                                const MsFastArg &fa, const RngArgs &rng, uint32_t bitP,
+template <int NL, int VAR, typename DR>
+__device__ __forceinline__ void fused_quad_fast(const float4 &v, const gc_f2 &q01, const gc_f2 &q23,
+                                                const MsFastArg &fa, const DR &dr, uint32_t bitP,
                                                 uint4 (&mb)[NL - 1], int4 &nq)
 {
     uint4 r0e;
     if constexpr ((VAR & MSV_EAGER0) != 0)
-        r0e = ms_draws4<KIND, VAR>(rng, 0, i0);  // independent of the upper levels': the chains interleave
+        r0e = dr(0);  // independent of the upper levels': the chains interleave
     int4 T;
     bool k0 = false, k1 = false, k2 = false, k3 = false;  // some level >= 1 qualifies
 #pragma unroll
     for (int l = NL - 1; l >= 1; --l) {  // the highest qualifying level wins
-        const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
+        const uint4 r = dr(l);
         const gc_f2 S = {fa.S24[l], fa.S24[l]};
         const gc_f2 a = q01 * S, b = q23 * S;
         const int32_t u0 = ms_t_v(a.x, r.x), u1 = ms_t_v(a.y, r.y), u2 = ms_t_v(b.x, r.z), u3 = ms_t_v(b.y, r.w);
@@ -840,7 +867,7 @@ __device__ __forceinline__ void fused_quad_fast(const float4 &v, const gc_f2 &q0
         if constexpr ((VAR & MSV_EAGER0) != 0)
             r = r0e;
         else
-            r = ms_draws4<KIND, VAR>(rng, 0, i0);
+            r = dr(0);
         const gc_f2 S = {fa.S24[0], fa.S24[0]};
         const gc_f2 a = q01 * S, b = q23 * S;
         const int32_t w0 = ms_t_v(a.x, r.x), w1 = ms_t_v(a.y, r.y), w2 = ms_t_v(b.x, r.z), w3 = ms_t_v(b.y, r.w);
@@ -857,9 +884,9 @@ __device__ __forceinline__ void fused_quad_fast(const float4 &v, const gc_f2 &q0
 
 // generic path of 4 elements (range-check failures, norms outside the
 // Markstein range, MSV_WIDE): the same bits and -q from the per-element rounding
-template <int KIND, int NL, int VAR = 0>
-__device__ __forceinline__ void fused_quad_slow(const float4 &v, uint32_t i0, const DivNorm &dv, const LevelsArg &lv,
-                                                const RngArgs &rng, uint32_t bitP, uint4 (&mb)[NL - 1], int4 &nq,
+template <int NL, int VAR, typename DR>
+__device__ __forceinline__ void fused_quad_slow(const float4 &v, const DivNorm &dv, const LevelsArg &lv,
+                                                const DR &dr, uint32_t bitP, uint4 (&mb)[NL - 1], int4 &nq,
                                                 int32_t qmax)
 {
     const float4 ql = quot4_exact(v, dv);
@@ -867,7 +894,7 @@ __device__ __forceinline__ void fused_quad_slow(const float4 &v, uint32_t i0, co
     int4 q = make_int4(0, 0, 0, 0);
 #pragma unroll
     for (int l = 1; l < NL; ++l) {
-        const uint4 r = ms_draws4<KIND, VAR>(rng, l, i0);
+        const uint4 r = dr(l);
         const float s = lv.s[l];
         const int32_t x0 = xi_from_q(ql.x, s, r.x), x1 = xi_from_q(ql.y, s, r.y);
         const int32_t x2 = xi_from_q(ql.z, s, r.z), x3 = xi_from_q(ql.w, s, r.w);
@@ -877,7 +904,7 @@ __device__ __forceinline__ void fused_quad_slow(const float4 &v, uint32_t i0, co
         if (x3 <= lv.maxv) { m.w = l; q.w = sgn_of(v.w) * x3; }
     }
     if (m.x == 0u || m.y == 0u || m.z == 0u || m.w == 0u) {
-        const uint4 r = ms_draws4<KIND, VAR>(rng, 0, i0);
+        const uint4 r = dr(0);
         const float s = lv.s[0];
         q.x = m.x == 0u ? sgn_of(v.x) * xi_from_q(ql.x, s, r.x) : q.x;
         q.y = m.y == 0u ? sgn_of(v.y) * xi_from_q(ql.y, s, r.y) : q.y;
@@ -926,11 +953,11 @@ __device__ __forceinline__ void fused_accumulate(uint32_t n, uint32_t i0, uint32
     acc.w += (uint32_t)nq.w << sh;
 }
 
-template <int KIND, int NL, int VAR>
-__device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
-                                              uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
-                                              const RngArgs &rng, uint32_t bitP, uint32_t sh,
-                                              uint4 (&macc)[NL - 1], uint4 &acc, int32_t qmax)
+template <int NL, int VAR, typename DR>
+__device__ __forceinline__ void fused_plane_d(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                              uint32_t lo2, const LevelsArg &lv, const MsFastArg &fa, const DR &dr,
+                                              uint32_t bitP, uint32_t sh, uint4 (&macc)[NL - 1], uint4 &acc,
+                                              int32_t qmax)
 {
     RangeLo rg;
     rg.add4(v);
@@ -938,10 +965,21 @@ __device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint3
     int4 nq;
     const gc_f2 q01 = quot2_signed(v.x, v.y, dv), q23 = quot2_signed(v.z, v.w, dv);
     if ((VAR & MSV_WIDE) == 0 && ((VAR & MSV_NOSLOW) || (dv.fast && !rg.tiny(lo2) && q_in_unit(q01, q23))))
-        fused_quad_fast<KIND, NL, VAR>(v, q01, q23, i0, fa, rng, bitP, mb, nq);
+        fused_quad_fast<NL, VAR>(v, q01, q23, fa, dr, bitP, mb, nq);
     else
-        fused_quad_slow<KIND, NL, VAR>(v, i0, dv, lv, rng, bitP, mb, nq, qmax);
+        fused_quad_slow<NL, VAR>(v, dv, lv, dr, bitP, mb, nq, qmax);
     fused_accumulate<NL>(n, i0, sh, mb, nq, macc, acc);
+}
+
+template <int KIND, int NL, int VAR>
+__device__ __forceinline__ void fused_plane_r(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
+                                              uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
+                                              const RngArgs &rng, uint32_t bitP, uint32_t sh,
+                                              uint4 (&macc)[NL - 1], uint4 &acc, int32_t qmax)
+{
+    fused_plane_d<NL, VAR>(v, n, i0, dv, lo2, lv, fa,
+                           [&](int l) { return ms_draws4<KIND, VAR>(rng, (uint32_t)l, i0); }, bitP, sh, macc, acc,
+                           qmax);
 }
 
 __device__ __forceinline__ float4 load4_guard(const float *__restrict__ x, uint32_t i0, uint32_t n)
@@ -1038,6 +1076,277 @@ __global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(con
                     o = make_uint4(o.x | a.x, o.y | a.y, o.z | a.z, o.w | a.w);
                 }
                 st_nt4u(mask_words + (uint64_t)f * Mm + 4u * t, o);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Octet kernels: 2 levels with the dense Philox stream (draws4<2>, gc_device.h).
+// A lane owns 2 adjacent word quads of a plane, i.e. the 8 elements of one
+// draw group (plane sizes that are multiples of 8 words: the host checks), so
+// one ms2_octet (3 Philox blocks) gives both levels' draws of all 8, against
+// 2 blocks per quad (4 per octet) of the per-quad kernels above.  The mask
+// without the q cache needs level 1 only (ms2_octet_level, 2 blocks per octet,
+// no worse than per quad).  Same outputs as the per-quad kernels with KIND 2,
+// bit for bit: the per-element arithmetic is the same code (mask_plane_d,
+// fused_plane_d, select_lanes), only the draws are shared.
+// ---------------------------------------------------------------------------
+// the octet at element i0 (i0 % 8 == 0): 0 past n
+__device__ __forceinline__ void load8_nt(const float *__restrict__ x, uint32_t i0, uint32_t n, float4 &v0, float4 &v1)
+{
+    if (i0 + 8 <= n) {
+        v0 = ld_nt(reinterpret_cast<const float4 *>(x + i0));
+        v1 = ld_nt(reinterpret_cast<const float4 *>(x + i0 + 4));
+        return;
+    }
+    v0 = load4_nt_tail<0>(x, i0, n);
+    v1 = i0 + 4 < n ? load4_nt_tail<0>(x, i0 + 4, n) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+// mask encode (k_ms_mask_fast with NL = 2): the block owns 64 octets, its 4
+// waves the planes p = wave + 4 j
+template <int LM, int VAR = 0, int CBY = 0>
+__global__ GC_MS_OCC __launch_bounds__(kBlock) void k_ms_mask_fast_o2(const float *__restrict__ x, uint32_t n,
+                                                            const float *__restrict__ normp, LevelsArg lv,
+                                                            MsFastArg fa, RngArgs rng, uint32_t M, uint32_t w,
+                                                            uint32_t *__restrict__ mask_words,
+                                                            void *__restrict__ cache = nullptr, int32_t cq = 0,
+                                                            uint32_t cb = 0)
+{
+    const float norm = *normp;
+    const DivNorm dv = make_div(norm);
+    const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
+    const uint32_t octs = M >> 3;
+    constexpr int PW = (LM + 3) / 4;
+    __shared__ uint4 part[3][2][kMsQuadsPerBlock];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    uint32_t Cf = 0;
+    if constexpr (CBY != 0)
+        Cf = (uint32_t)cq + ((uint32_t)cq << cb);
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < octs; tb += gridDim.x * kMsQuadsPerBlock) {
+        const uint32_t t = tb + lane;
+        uint4 acc[2] = {};
+        if (t < octs) {
+#pragma unroll
+            for (int j = 0; j < ((VAR & MSV_ROLL) ? 1 : PW); ++j) {
+#pragma unroll 1
+            for (int j1 = 0; j1 < ((VAR & MSV_ROLL) ? PW : 1); ++j1) {
+                const uint32_t p = wave + 4u * (j + j1);
+                if (p >= (uint32_t)LM)
+                    break;
+                const uint32_t i0 = p * M + 8u * t;
+                if (i0 >= n)
+                    break;
+                float4 v[2];
+                load8_nt(x, i0, n, v[0], v[1]);
+                uint4 d[2][2];
+                if constexpr (CBY != 0)
+                    ms2_octet(rng, i0 >> 3, d);
+                else
+                    ms2_octet_level(rng, i0 >> 3, 1, d[1]);
+#pragma unroll
+                for (int hq = 0; hq < 2; ++hq) {
+                    const uint32_t iq = i0 + 4u * hq;
+                    if (hq == 1 && iq >= n)
+                        break;
+                    uint4 mb[1];
+                    if constexpr (CBY != 0) {
+                        uint4 cv;
+                        mask_plane_d<2, VAR, true>(v[hq], n, iq, dv, lo2, hi2, lv, fa,
+                                                   [&](int l) { return d[l][hq]; }, 1u << (p * w), mb, cq, cb, &cv);
+                        cache_store<CBY>(cache, iq, n, make_uint4(Cf - cv.x, Cf - cv.y, Cf - cv.z, Cf - cv.w));
+                    } else {
+                        mask_plane_d<2, VAR, false>(v[hq], n, iq, dv, lo2, hi2, lv, fa,
+                                                    [&](int l) { return d[1][hq]; }, 1u << (p * w), mb);
+                    }
+                    acc[hq].x |= mb[0].x;
+                    acc[hq].y |= mb[0].y;
+                    acc[hq].z |= mb[0].z;
+                    acc[hq].w |= mb[0].w;
+                }
+            }
+            }
+        }
+        if (wave) {
+            part[wave - 1][0][lane] = acc[0];
+            part[wave - 1][1][lane] = acc[1];
+        }
+        __syncthreads();
+        if (wave == 0 && t < octs) {
+#pragma unroll
+            for (int hq = 0; hq < 2; ++hq) {
+                const uint4 a = part[0][hq][lane], b = part[1][hq][lane], c = part[2][hq][lane];
+                st_nt4u(mask_words + 8u * t + 4u * hq,
+                        make_uint4(acc[hq].x | a.x | b.x | c.x, acc[hq].y | a.y | b.y | c.y,
+                                   acc[hq].z | a.z | b.z | c.z, acc[hq].w | a.w | b.w | c.w));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// select encode (k_ms_select_fast with NL = 2)
+template <int LQ, int VAR = 0>
+__global__ __launch_bounds__(kBlock) void k_ms_select_fast_o2(const float *__restrict__ x, uint32_t n,
+                                                              const float *__restrict__ normp, LevelsArg lv,
+                                                              MsFastArg fa, RngArgs rng, MaskArg mk, FastDiv fd,
+                                                              uint32_t Mq, uint32_t wq, int32_t qmax,
+                                                              uint32_t *__restrict__ words)
+{
+    const float norm = *normp;
+    const DivNorm dv = make_div(norm);
+    const uint32_t lo2 = 2u * dv.lo1;
+    const uint32_t octs = Mq >> 3;
+    constexpr int PW = (LQ + 3) / 4;
+    __shared__ uint4 part[3][2][kMsQuadsPerBlock];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < octs; tb += gridDim.x * kMsQuadsPerBlock) {
+        const uint32_t t = tb + lane;
+        uint4 acc[2] = {};
+        if (t < octs) {
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                const uint32_t p = wave + 4u * j;
+                if (p >= (uint32_t)LQ)
+                    break;
+                const uint32_t i0 = p * Mq + 8u * t;
+                if (i0 >= n)
+                    break;
+                float4 v[2];
+                load8_nt(x, i0, n, v[0], v[1]);
+                uint4 m[2];
+                m[0] = mask_levels4_fast<2>(mk, fd, i0);
+                m[1] = i0 + 4 < n ? mask_levels4_fast<2>(mk, fd, i0 + 4) : make_uint4(0u, 0u, 0u, 0u);
+                uint4 d[2][2];
+                ms2_octet(rng, i0 >> 3, d);
+                const uint32_t sh = p * wq;
+#pragma unroll
+                for (int hq = 0; hq < 2; ++hq) {
+                    const uint32_t iq = i0 + 4u * hq;
+                    if (hq == 1 && iq >= n)
+                        break;
+                    const uint4 &mm = m[hq];
+                    const uint4 r = make_uint4(mm.x ? d[1][hq].x : d[0][hq].x, mm.y ? d[1][hq].y : d[0][hq].y,
+                                               mm.z ? d[1][hq].z : d[0][hq].z, mm.w ? d[1][hq].w : d[0][hq].w);
+                    const uint4 ln = select_lanes<2, VAR>(v[hq], mm, r, n, iq, dv, lo2, lv, fa, qmax);
+                    acc[hq].x += ln.x << sh;
+                    acc[hq].y += ln.y << sh;
+                    acc[hq].z += ln.z << sh;
+                    acc[hq].w += ln.w << sh;
+                }
+            }
+        }
+        if (wave) {
+            part[wave - 1][0][lane] = acc[0];
+            part[wave - 1][1][lane] = acc[1];
+        }
+        __syncthreads();
+        if (wave == 0 && t < octs) {
+#pragma unroll
+            for (int hq = 0; hq < 2; ++hq) {
+                const uint4 a = part[0][hq][lane], b = part[1][hq][lane], c = part[2][hq][lane];
+                st_nt4u(words + 8u * t + 4u * hq, make_uint4(acc[hq].x + a.x + b.x + c.x, acc[hq].y + a.y + b.y + c.y,
+                                                             acc[hq].z + a.z + b.z + c.z, acc[hq].w + a.w + b.w + c.w));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// W = 1 one-pass encode (k_ms_fused_w1 with NL = 2): lanes = octets of the
+// mask stream's quads, wave h = q stream h as there
+template <int VAR = 0>
+__global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1_o2(
+    const float *__restrict__ x, uint32_t n, const float *__restrict__ normp, LevelsArg lv, MsFastArg fa, RngArgs rng,
+    uint32_t Mm, uint32_t r, uint32_t Lq, uint32_t wq, int32_t qmax, uint32_t Cw, uint32_t pend,
+    uint32_t *__restrict__ mask_words, uint32_t *__restrict__ words)
+{
+    const float norm = *normp;
+    const DivNorm dv = make_div(norm);
+    const uint32_t lo2 = 2u * dv.lo1;
+    const uint32_t octs = Mm >> 3;
+    const uint32_t h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t kend = h < pend ? min(Lq, (pend - h + r - 1) / r) : 0u;
+    const uint32_t kfull = h + 1 < pend ? min(kend, (pend - 1 - h + r - 1) / r) : 0u;
+    __shared__ uint4 part[kMsFusedMaxR - 1][2][kMsQuadsPerBlock];
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < octs; tb += gridDim.x * kMsQuadsPerBlock) {
+        const uint32_t t = tb + lane;
+        uint4 macc[2][1] = {};
+        uint4 acc[2] = {};
+        if (t < octs) {
+            uint32_t i0 = h * Mm + 8u * t;
+            const uint32_t step = r * Mm;
+            auto load = [&](uint32_t k, uint32_t i, float4 (&v)[2]) {
+                if (k < kfull) {
+                    v[0] = ld_nt(reinterpret_cast<const float4 *>(x + i));
+                    v[1] = ld_nt(reinterpret_cast<const float4 *>(x + i + 4));
+                } else {
+                    v[0] = load4_guard(x, i, n);
+                    v[1] = load4_guard(x, i + 4, n);
+                }
+            };
+            float4 vn[2];
+            if constexpr ((VAR & MSV_PREFETCH) != 0) {
+                if (kend > 0)
+                    load(0, i0, vn);
+            }
+#pragma unroll 1
+            for (uint32_t k = 0; k < kend; ++k) {
+                float4 v[2];
+                if constexpr ((VAR & MSV_PREFETCH) != 0) {
+                    v[0] = vn[0];
+                    v[1] = vn[1];
+                    if (k + 1 < kend)
+                        load(k + 1, i0 + step, vn);
+                } else {
+                    load(k, i0, v);
+                }
+                uint4 d[2][2];
+                ms2_octet(rng, i0 >> 3, d);
+                const uint32_t bitP = 1u << (h + r * k), sh = k * wq;
+#pragma unroll
+                for (int hq = 0; hq < 2; ++hq)
+                    fused_plane_d<2, VAR>(v[hq], n, i0 + 4u * hq, dv, lo2, lv, fa, [&](int l) { return d[l][hq]; },
+                                          bitP, sh, macc[hq], acc[hq], qmax);
+                i0 += step;
+            }
+        }
+        if (t < octs) {
+            const uint64_t Mq = (uint64_t)r * Mm;
+#pragma unroll
+            for (int hq = 0; hq < 2; ++hq) {
+                const uint64_t j0 = (uint64_t)h * Mm + 8u * t + 4u * hq;
+                uint4 C = make_uint4(Cw, Cw, Cw, Cw);
+                if (j0 + 3 + (uint64_t)(Lq - 1) * Mq >= n) {  // lanes of elements past n stay 0
+                    C = make_uint4(0u, 0u, 0u, 0u);
+                    for (uint32_t k = 0; k < Lq; ++k) {
+                        const uint64_t e = j0 + (uint64_t)k * Mq;
+                        const uint32_t c = (uint32_t)qmax << (k * wq);
+                        C.x += e < n ? c : 0u;
+                        C.y += e + 1 < n ? c : 0u;
+                        C.z += e + 2 < n ? c : 0u;
+                        C.w += e + 3 < n ? c : 0u;
+                    }
+                }
+                st_nt4u(words + j0, make_uint4(C.x - acc[hq].x, C.y - acc[hq].y, C.z - acc[hq].z, C.w - acc[hq].w));
+            }
+        }
+        if (h) {
+            part[h - 1][0][lane] = macc[0][0];
+            part[h - 1][1][lane] = macc[1][0];
+        }
+        __syncthreads();
+        if (h == 0 && t < octs) {
+#pragma unroll
+            for (int hq = 0; hq < 2; ++hq) {
+                uint4 o = macc[hq][0];
+                for (uint32_t q = 0; q + 1 < r; ++q) {
+                    const uint4 a = part[q][hq][lane];
+                    o = make_uint4(o.x | a.x, o.y | a.y, o.z | a.z, o.w | a.w);
+                }
+                st_nt4u(mask_words + 8u * t + 4u * hq, o);
             }
         }
         __syncthreads();

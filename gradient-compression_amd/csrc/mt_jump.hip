@@ -300,7 +300,7 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
                                                          const float *__restrict__ x, const float *__restrict__ normp,
                                                          float s)
 {
-    __shared__ uint32_t buf[2][kMtN];
+    __shared__ __attribute__((aligned(16))) uint32_t buf[2][kMtN];
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
     const uint64_t g = blockIdx.x;
     if (g == 0)
@@ -326,8 +326,9 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
     // for the compiler's memory-counter tracking, so the tempering waves'
     // prefetched x loads stay in flight across blocks.
     typedef typename std::conditional<MODE == 2, int32_t, int8_t>::type QT;
-    __shared__ QT qbuf[2][kMtN];  // quantize modes: q of block t in qbuf[t & 1], stored by the twisting waves
-    __shared__ float xring[MODE ? kMtPre : 1][MODE ? kMtTemperThreads * kMtRounds : 1];  // x, kMtPre blocks ahead
+    constexpr bool QUANT = MODE == 1 || MODE == 2;  // the quantize modes (0: draws, 3: 24-bit packed draws)
+    __shared__ QT qbuf[QUANT ? 2 : 1][QUANT ? kMtN : 1];  // q of block t in qbuf[t & 1], stored by the twisting waves
+    __shared__ float xring[QUANT ? kMtPre : 1][QUANT ? kMtTemperThreads * kMtRounds : 1];  // x, kMtPre blocks ahead
     if (wave < kMtTwistWaves) {
         // block t's q (t >= 1) lands in qbuf[t & 1] during iteration t and is
         // stored to HBM by these waves during iteration t + 1: the global stores
@@ -341,14 +342,14 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
         };
         for (uint32_t t = 0; t < twists; ++t) {
             twist_column(buf[t & 1u], buf[(t + 1) & 1u], tid);
-            if (MODE != 0 && t > 0)
+            if (QUANT && t > 0)
                 store_q(t - 1);
             lds_barrier();
         }
-        if (MODE != 0 && twists > 0)
+        if (QUANT && twists > 0)
             store_q(twists - 1);
         lds_barrier();
-        if (MODE != 0)
+        if (QUANT)
             store_q(twists);
     } else if constexpr (MODE == 0) {
         for (uint32_t i = ct; i < head; i += kMtTemperThreads)
@@ -369,6 +370,32 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
                 for (uint32_t i = ct; i < take; i += kMtTemperThreads)
                     mt_emit<0>(out, at + i, mtj_temper(cur[i]), x, DivNorm{}, s);
             }
+            lds_barrier();
+        }
+    } else if constexpr (MODE == 3) {
+        // 24-bit packed draws (GC_RNG_STREAM24): thread ct tempers draws
+        // 4q .. 4q+3 of a block and stores their low 24 bits as 3 words.  The
+        // caller's read index and count are multiples of 4 (host-checked), so
+        // head, every block start `at` and every `take` are too
+        uint32_t *o = reinterpret_cast<uint32_t *>(out);
+        auto emit4 = [&](uint64_t e, const uint32_t *src) {
+            const uint4 w = *reinterpret_cast<const uint4 *>(src);  // 16-byte aligned: ptr0 % 4 == 0
+            const uint32_t a = mtj_temper(w.x), b = mtj_temper(w.y), c = mtj_temper(w.z), d = mtj_temper(w.w);
+            uint3 p;
+            p.x = (a & 0xFFFFFFu) | (b << 24);
+            p.y = ((b >> 8) & 0xFFFFu) | (c << 16);
+            p.z = ((c >> 16) & 0xFFu) | (d << 8);
+            *reinterpret_cast<uint3 *>(o + (e >> 2) * 3) = p;
+        };
+        for (uint32_t q = ct; 4 * q < head; q += kMtTemperThreads)
+            emit4(pos0 + 4 * q, &buf[0][ptr0 + 4 * q]);
+        lds_barrier();
+        for (uint32_t t = 1; t <= twists; ++t) {
+            const uint32_t *cur = buf[t & 1u];
+            const uint64_t at = pos0 + head + (uint64_t)(t - 1) * kMtN;
+            const uint32_t take = (uint32_t)min((uint64_t)kMtN, end - at);
+            for (uint32_t q = ct; 4 * q < take; q += kMtTemperThreads)
+                emit4(at + 4 * q, cur + 4 * q);
             lds_barrier();
         }
     } else {
@@ -501,8 +528,11 @@ static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_
     else if (mode == 1)
         hipLaunchKernelGGL(k_mt_gen<1>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
                            J, count, out, gstate, x, norm, s);
-    else
+    else if (mode == 2)
         hipLaunchKernelGGL(k_mt_gen<2>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
+                           J, count, out, gstate, x, norm, s);
+    else
+        hipLaunchKernelGGL(k_mt_gen<3>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
                            J, count, out, gstate, x, norm, s);
     return launch_status(what);
 }
@@ -530,6 +560,20 @@ int gc_mt19937_generate_split_j(uint32_t *state_dev, const uint32_t *table_dev, 
     GC_REQUIRE(count > 0, "gc_mt19937_generate_split_j: count must be positive");
     return mt_run("gc_mt19937_generate_split_j", 0, state_dev, table_dev, table_gens, J, out, count, workspace, stream,
                   nullptr, nullptr, 0.0f, phase, true, end_coef, end_block);
+}
+
+int gc_mt19937_generate_split24_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                  const uint32_t *end_coef, uint64_t end_block, uint32_t *out, uint64_t count,
+                                  uint64_t idx, void *workspace, int phase, gc_stream_t stream)
+{
+    const char *what = "gc_mt19937_generate_split24_j";
+    GC_REQUIRE(phase >= 1 && phase <= 3, "%s: phase must be 1, 2 or 3", what);
+    GC_REQUIRE(count > 0 && count % 4 == 0 && idx % 4 == 0 && idx <= kMtN,
+               "%s: count (%llu) and the read index (%llu) must be multiples of 4", what, (unsigned long long)count,
+               (unsigned long long)idx);
+    GC_REQUIRE(!out || ((uintptr_t)out & 3u) == 0, "%s: out must be 4-byte aligned", what);
+    return mt_run(what, 3, state_dev, table_dev, table_gens, J, out, count, workspace, stream, nullptr, nullptr, 0.0f,
+                  phase, true, end_coef, end_block);
 }
 
 int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,

@@ -456,10 +456,17 @@ int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_leve
     hipLaunchKernelGGL((k_ms_fused_w1<KIND_, NL_, __VA_ARGS__>), dim3(g), dim3(64 * r), 0, st, x, (uint32_t)n, norm, la, \
                        fa, ra, Mm, r, q_lanes->per_word, q_lanes->bits, qmax, Cw, pend, mask_words, words)
     if (levels->count == 2) {
-        if (rng->kind == GC_RNG_PHILOX) {
-            if (wide) { GC_FW(0, 2, MSV_WIDE); }
-            else if (ms_fused_u() == 2) { GC_FW(0, 2, MSV_EAGER0, 2); }
-            else { GC_FW(0, 2, MSV_EAGER0); }
+        if (rng->kind == GC_RNG_PHILOX && Mm % 8 == 0) {  // the octet kernel: dense draws shared by 8 elements
+            const unsigned g8 = (unsigned)std::max<uint64_t>(1, (ms_grid(Mm >> 3) + ms_tiles() - 1) / ms_tiles());
+#define GC_FW8(VAR_)                                                                                                \
+    hipLaunchKernelGGL((k_ms_fused_w1_o2<VAR_>), dim3(g8), dim3(64 * r), 0, st, x, (uint32_t)n, norm, la, fa, ra, Mm, r, \
+                       q_lanes->per_word, q_lanes->bits, qmax, Cw, pend, mask_words, words)
+            if (wide) { GC_FW8(MSV_WIDE | MSV_PREFETCH); } else { GC_FW8(MSV_PREFETCH); }
+#undef GC_FW8
+        } else if (rng->kind == GC_RNG_PHILOX) {
+            if (wide) { GC_FW(2, 2, MSV_WIDE); }
+            else if (ms_fused_u() == 2) { GC_FW(2, 2, MSV_EAGER0, 2); }
+            else { GC_FW(2, 2, MSV_EAGER0); }
         }
         else { if (wide) { GC_FW(1, 2, MSV_WIDE); } else { GC_FW(1, 2, 0); } }
     } else {
@@ -506,12 +513,22 @@ int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const floa
     GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_fast<LL, KIND_, NL_>), dim3(g), dim3(kBlock), 0, \
                                                             st, x, (uint32_t)n, norm, la, fa, ra, (uint32_t)M, w,  \
                                                             fields, mask_words, (void *)nullptr, 0, 0u))
-        if (levels->count == 2) {
-            if (rng->kind == GC_RNG_PHILOX) { GC_MF(0, 2); } else { GC_MF(1, 2); }
+        if (levels->count == 2 && rng->kind == GC_RNG_PHILOX && M % 8 == 0) {
+            const unsigned g8 = (unsigned)std::max<uint64_t>(1, (ms_grid(M >> 3) + ms_tiles() - 1) / ms_tiles());
+#define GC_MF8(VAR_)                                                                                               \
+    GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_fast_o2<LL, VAR_>), dim3(g8), dim3(kBlock), 0, \
+                                                            st, x, (uint32_t)n, norm, la, fa, ra, (uint32_t)M, w,      \
+                                                            mask_words, (void *)nullptr, 0, 0u))
+            if (wide) { GC_MF8(MSV_WIDE | MSV_ROLL); } else { GC_MF8(MSV_ROLL); }
+#undef GC_MF8
+        } else if (levels->count == 2) {
+            if (rng->kind == GC_RNG_PHILOX) { GC_MF(2, 2); } else { GC_MF(1, 2); }
         } else {
             if (rng->kind == GC_RNG_PHILOX) { GC_MF(0, 3); } else { GC_MF(1, 3); }
         }
 #undef GC_MF
+    } else if (rng->kind == GC_RNG_PHILOX && levels->count == 2) {
+        if (mode == 0) { GC_ME(2, 0); } else if (mode == 1) { GC_ME(2, 1); } else { GC_ME(2, 2); }
     } else if (rng->kind == GC_RNG_PHILOX) {
         if (mode == 0) { GC_ME(0, 0); } else if (mode == 1) { GC_ME(0, 1); } else { GC_ME(0, 2); }
     } else {
@@ -561,12 +578,22 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_fast<LL, KIND_, NL_>), dim3(g), dim3(kBlock), 0,   \
                                                          st, x, (uint32_t)n, norm, la, fa, ra, mk, fd, (uint32_t)Mq, \
                                                          wq, qmax, words))
-        if (levels->count == 2) {
-            if (rng->kind == GC_RNG_PHILOX) { GC_SF(0, 2); } else { GC_SF(1, 2); }
+        if (levels->count == 2 && rng->kind == GC_RNG_PHILOX && Mq % 8 == 0) {
+            const unsigned g8 = (unsigned)std::max<uint64_t>(1, (ms_grid(Mq >> 3) + ms_tiles() - 1) / ms_tiles());
+#define GC_SF8(VAR_)                                                                                                \
+    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_fast_o2<LL, VAR_>), dim3(g8), dim3(kBlock), 0, st, \
+                                                         x, (uint32_t)n, norm, la, fa, ra, mk, fd, (uint32_t)Mq, wq,  \
+                                                         qmax, words))
+            if (wide) { GC_SF8(MSV_WIDE | MSV_ROLL); } else { GC_SF8(MSV_ROLL); }
+#undef GC_SF8
+        } else if (levels->count == 2) {
+            if (rng->kind == GC_RNG_PHILOX) { GC_SF(2, 2); } else { GC_SF(1, 2); }
         } else {
             if (rng->kind == GC_RNG_PHILOX) { GC_SF(0, 3); } else { GC_SF(1, 3); }
         }
 #undef GC_SF
+    } else if (rng->kind == GC_RNG_PHILOX && levels->count == 2) {
+        if (mode == 0) { GC_SE(2, 0); } else if (mode == 1) { GC_SE(2, 1); } else { GC_SE(2, 2); }
     } else if (rng->kind == GC_RNG_PHILOX) {
         if (mode == 0) { GC_SE(0, 0); } else if (mode == 1) { GC_SE(0, 1); } else { GC_SE(0, 2); }
     } else {
@@ -616,12 +643,24 @@ int gc_ms_mask_encode_cached(const float *x, uint64_t n, const float *norm, cons
 #define GC_MFC_V(KIND_, NL_, CBY_) \
     if (wide) { GC_MFC(KIND_, NL_, MSV_WIDE, CBY_); } else { GC_MFC(KIND_, NL_, 0, CBY_); }
 #define GC_MFC_K(NL_, CBY_) \
-    if (rng->kind == GC_RNG_PHILOX) { GC_MFC_V(0, NL_, CBY_); } else { GC_MFC_V(1, NL_, CBY_); }
-    if (levels->count == 2) {
+    if (rng->kind == GC_RNG_PHILOX) { GC_MFC_V(NL_ == 2 ? 2 : 0, NL_, CBY_); } else { GC_MFC_V(1, NL_, CBY_); }
+#define GC_MFC8(VAR_, CBY_)                                                                                           \
+    GC_DISPATCH_L2(mask_lanes->per_word,                                                                             \
+                   hipLaunchKernelGGL((k_ms_mask_fast_o2<LL, VAR_, CBY_>), dim3(g8), dim3(kBlock), 0, st, x, (uint32_t)n, \
+                                      norm, la, fa, ra, M, w, mask_words, cache, cg.qmax, cg.cb))
+    if (levels->count == 2 && rng->kind == GC_RNG_PHILOX && M % 8 == 0) {  // octets: dense draws, 3 blocks per 8
+        const unsigned g8 = (unsigned)std::max<uint64_t>(1, (ms_grid(M >> 3) + ms_tiles() - 1) / ms_tiles());
+        if (cg.bytes == 1) {
+            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL, 1); } else { GC_MFC8(MSV_ROLL, 1); }
+        } else {
+            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL, 2); } else { GC_MFC8(MSV_ROLL, 2); }
+        }
+    } else if (levels->count == 2) {
         if (cg.bytes == 1) { GC_MFC_K(2, 1) } else { GC_MFC_K(2, 2) }
     } else {
         if (cg.bytes == 1) { GC_MFC_K(3, 1) } else { GC_MFC_K(3, 2) }
     }
+#undef GC_MFC8
 #undef GC_MFC_K
 #undef GC_MFC_V
 #undef GC_MFC
@@ -768,7 +807,10 @@ int gc_ms_quantize_mask(const float *x, uint64_t n, const float *norm, const gc_
     const RngArgs ra = rng_args_ms(rng, n);
     const unsigned grid = grid_for((n + 3) >> 2);
     const bool vec = aligned16(x);
-    if (rng->kind == GC_RNG_PHILOX) {
+    if (rng->kind == GC_RNG_PHILOX && levels->count == 2) {
+        if (vec) hipLaunchKernelGGL((k_ms_quantize_mask<2, 0>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, ra, mask);
+        else hipLaunchKernelGGL((k_ms_quantize_mask<2, 1>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, ra, mask);
+    } else if (rng->kind == GC_RNG_PHILOX) {
         if (vec) hipLaunchKernelGGL((k_ms_quantize_mask<0, 0>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, ra, mask);
         else hipLaunchKernelGGL((k_ms_quantize_mask<0, 1>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, ra, mask);
     } else {
@@ -796,7 +838,10 @@ int gc_ms_select_quantize(const float *x, uint64_t n, const float *norm, const g
 #define GC_SQ(KIND_, MODE_, QT_)                                                                                \
     hipLaunchKernelGGL((k_ms_select_quantize<KIND_, MODE_, QT_>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, la, \
                        ra, mask, reinterpret_cast<QT_ *>(q))
-    if (rng->kind == GC_RNG_PHILOX) {
+    if (rng->kind == GC_RNG_PHILOX && levels->count == 2) {
+        if (q_dtype == GC_I8) { if (vec) GC_SQ(2, 0, int8_t); else GC_SQ(2, 1, int8_t); }
+        else { if (vec) GC_SQ(2, 0, int32_t); else GC_SQ(2, 1, int32_t); }
+    } else if (rng->kind == GC_RNG_PHILOX) {
         if (q_dtype == GC_I8) { if (vec) GC_SQ(0, 0, int8_t); else GC_SQ(0, 1, int8_t); }
         else { if (vec) GC_SQ(0, 0, int32_t); else GC_SQ(0, 1, int32_t); }
     } else {

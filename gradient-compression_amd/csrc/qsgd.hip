@@ -330,11 +330,14 @@ static RngArgs rng_args(const gc_rng *r, uint64_t n)
     return a;
 }
 
-static int check_rng(const gc_rng *r, const char *what)
+static int check_rng(const gc_rng *r, const char *what, bool stream24 = false)
 {
     GC_REQUIRE(r, "%s: null rng", what);
-    GC_REQUIRE(r->kind == GC_RNG_PHILOX || r->kind == GC_RNG_STREAM, "%s: unknown rng kind %u", what, r->kind);
-    GC_REQUIRE(r->kind != GC_RNG_STREAM || r->stream, "%s: STREAM rng without a stream pointer", what);
+    GC_REQUIRE(r->kind == GC_RNG_PHILOX || r->kind == GC_RNG_STREAM || (stream24 && r->kind == GC_RNG_STREAM24),
+               "%s: unknown rng kind %u", what, r->kind);
+    GC_REQUIRE(r->kind == GC_RNG_PHILOX || r->stream, "%s: STREAM rng without a stream pointer", what);
+    GC_REQUIRE(r->kind != GC_RNG_STREAM24 || ((uintptr_t)r->stream & 3u) == 0,
+               "%s: STREAM24 draws must be 4-byte aligned", what);
     return GC_OK;
 }
 
@@ -412,7 +415,7 @@ int gc_qsgd_encode(const float *x, const int64_t *idx, uint64_t n, const float *
 {
     int rc;
     if ((rc = check_bits(bits, "gc_qsgd_encode")) || (rc = check_lanes(lanes, n, "gc_qsgd_encode")) ||
-        (rc = check_rng(rng, "gc_qsgd_encode")))
+        (rc = check_rng(rng, "gc_qsgd_encode", true)))
         return rc;
     const uint32_t s = (1u << bits) - 1u;
     GC_REQUIRE(lanes->offset == s && lanes->range == 2ull * s, "gc_qsgd_encode: lanes not made by gc_qsgd_layout");
@@ -426,7 +429,15 @@ int gc_qsgd_encode(const float *x, const int64_t *idx, uint64_t n, const float *
     const int mode = idx ? 2 : (aligned16(x) ? 0 : 1);
     const float sf = (float)s;
     const int32_t qmax = (int32_t)s;
-    if (rng->kind == GC_RNG_PHILOX) {
+    if (rng->kind == GC_RNG_STREAM24) {
+        if (mode == 0) {
+            GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 3, 0>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
+        } else if (mode == 1) {
+            GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 3, 1>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
+        } else {
+            GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 3, 2>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
+        }
+    } else if (rng->kind == GC_RNG_PHILOX) {
         if (mode == 0) {
             GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 0, 0>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
         } else if (mode == 1) {

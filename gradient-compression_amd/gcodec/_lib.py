@@ -21,7 +21,7 @@ GC_ENOSPC = -4
 GC_ENODEV = -5
 
 GC_I8, GC_I32, GC_I64 = 1, 4, 8
-GC_RNG_PHILOX, GC_RNG_STREAM = 0, 1
+GC_RNG_PHILOX, GC_RNG_STREAM, GC_RNG_STREAM24 = 0, 1, 2
 GC_MAX_LEVELS = 8
 GC_MT_JUMP_DRAWS = 262080  # include/gcodec.h: draws per generator of the parallel MT19937 stream
 
@@ -134,6 +134,7 @@ SIGNATURES = {
     "gc_mt19937_generate_jumped_j": (C.c_int, [P, P, u64, u64, P, u64, P, P]),
     "gc_mt19937_generate_phase_j": (C.c_int, [P, P, u64, u64, P, u64, P, C.c_int, P]),
     "gc_mt19937_generate_split_j": (C.c_int, [P, P, u64, u64, P, u64, P, u64, P, C.c_int, P]),
+    "gc_mt19937_generate_split24_j": (C.c_int, [P, P, u64, u64, P, u64, P, u64, u64, P, C.c_int, P]),
     "gc_randk_workspace_size": (C.c_size_t, []),
     "gc_randk_gather_absmax": (C.c_int, [P, P, u64, P, P, P, P]),
     "gc_randk_encode_w1": (C.c_int, [P, P, u64, P, P, u32, LANESP, RNGP, P, P, P]),

@@ -1015,13 +1015,14 @@ class _MtRun:
     slot its end state goes to, and events after its jumps (p1), after that
     state's copy to the host (state_ready) and after its generators (done)."""
 
-    __slots__ = ("count", "out", "slot", "idx_end", "p1", "state_ready", "done")
+    __slots__ = ("count", "packed", "out", "slot", "idx_end", "p1", "state_ready", "done")
 
 
-def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int) -> _MtRun:
+def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int, packed: bool = False) -> _MtRun:
     """Phase 1 on the jump stream: sequence + jumps + the end state (written
     over st_dev, gc_mt19937_generate_split_j) and its copy into hout[slot];
-    phase 2 on the generator stream, after phase 1: the draws."""
+    phase 2 on the generator stream, after phase 1: the draws (packed: their
+    low 24 bits, 3 bytes each, gc_mt19937_generate_split24_j)."""
     J = mt_pipe_generator_draws(count)
     gens = -(-count // J)
     js, gss = _mt_side(dev)
@@ -1033,7 +1034,7 @@ def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int) -> _MtRun:
     busy = _MT_BUSY.get((dev.index, slot))
     lib = _lib.load()
     run = _MtRun()
-    run.count, run.slot, run.idx_end = count, slot, idx + count - 624 * block
+    run.count, run.packed, run.slot, run.idx_end = count, packed, slot, idx + count - 624 * block
     with torch.cuda.stream(js):
         if busy is not None:
             js.wait_event(busy)  # that slot's previous generators have read the workspace
@@ -1052,19 +1053,39 @@ def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int) -> _MtRun:
             t.record_stream(gs)
     with torch.cuda.stream(gs):
         gs.wait_event(run.p1)
-        run.out = torch.empty(count, dtype=torch.int32, device=dev)
-        check(lib.gc_mt19937_generate_split_j(_p(st_dev), _p(table), tgens, J, _p(end), block, _p(run.out), count,
-                                              _p(ws), 2, _stream(dev)), "gc_mt19937_generate_split_j")
+        if packed:
+            run.out = torch.empty(count // 4 * 3, dtype=torch.int32, device=dev)
+            check(lib.gc_mt19937_generate_split24_j(_p(st_dev), _p(table), tgens, J, _p(end), block, _p(run.out),
+                                                    count, idx, _p(ws), 2, _stream(dev)),
+                  "gc_mt19937_generate_split24_j")
+        else:
+            run.out = torch.empty(count, dtype=torch.int32, device=dev)
+            check(lib.gc_mt19937_generate_split_j(_p(st_dev), _p(table), tgens, J, _p(end), block, _p(run.out),
+                                                  count, _p(ws), 2, _stream(dev)), "gc_mt19937_generate_split_j")
         run.done = torch.cuda.Event()
         run.done.record()
     _MT_BUSY[(dev.index, slot)] = run.done
     return run
 
 
-def mt19937_draws(count: int, device) -> torch.Tensor:
+def mt19937_packable(count: int, idx: int) -> bool:
+    """Whether a run of `count` draws from read index `idx` can be packed to
+    24 bits (whole quads of draws: count and idx multiples of 4)."""
+    return count > 0 and count % 4 == 0 and idx % 4 == 0
+
+
+def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     """`count` draws of torch's CPU generator, produced on `device`; torch's
     generator state advances exactly as torch.bernoulli would advance it
     (synchronously: the new state is in torch's generator when this returns).
+
+    packed24: where mt19937_packable (count and torch's read index multiples
+    of 4), return only each draw's low 24 bits, 3 bytes per draw little-endian
+    (3 count / 4 int32 words: GC_RNG_STREAM24, the QSGD encode reads a 12-byte
+    quad per 4 elements), else the plain draws; the caller tells the two apart
+    by numel.  torch's rounding reads only those 24 bits (compressors.py:301
+    via torch.rand), so the encode is bit-identical either way and moves 25 %
+    fewer draw bytes (written once, read once).
 
     The draws are generated on two high-priority side streams
     (gc_mt19937_generate_split_j): phase 1 (jump stream) = the state's
@@ -1105,7 +1126,8 @@ def mt19937_draws(count: int, device) -> torch.Tensor:
         if queue:  # dropped runs still moved dst on: send the state next time
             _MT_LAST.pop(d, None)
         return torch.empty(0, dtype=torch.int32, device=device)
-    if queue and untouched and queue[0].count == count:
+    packed = bool(packed24) and mt19937_packable(count, int(idx))
+    if queue and untouched and queue[0].count == count and queue[0].packed == packed:
         run = queue.pop(0)
     else:
         if queue or not untouched:  # dst is not torch's state: send it
@@ -1115,11 +1137,12 @@ def mt19937_draws(count: int, device) -> torch.Tensor:
                 h[624] = idx
                 dst.copy_(hin, non_blocking=True)
         queue = []
-        run = _mt_enqueue(device, dst, count, int(idx), hout, next_slot())
+        run = _mt_enqueue(device, dst, count, int(idx), hout, next_slot(), packed)
     if MT_SPECULATE and repeat and count <= MT_SPECULATE_MAX_DRAWS:
         tail = queue[-1] if queue else run
         while len(queue) < depth:
-            tail = _mt_enqueue(device, dst, count, tail.idx_end, hout, next_slot())
+            tail = _mt_enqueue(device, dst, count, tail.idx_end, hout, next_slot(),
+                               packed and mt19937_packable(count, tail.idx_end))
             queue.append(tail)
     else:
         queue = []  # (none were kept: a queue exists only after a repeat)

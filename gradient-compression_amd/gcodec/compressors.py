@@ -43,7 +43,9 @@ class _Base:
         self._device = device
         self._gen = generator or default_generator
 
-    def _reserve(self, n: int, levels: int, device):
+    def _reserve(self, n: int, levels: int, device, packed24: bool = False):
+        if packed24:  # torch mode: 24-bit packed draws where the run allows (rng.Generator.reserve)
+            return self._gen.reserve(n, levels, device=device, backend=self.backend, packed24=True)
         return self._gen.reserve(n, levels, device=device, backend=self.backend)
 
 
@@ -69,7 +71,7 @@ class QSGDMaxNormCompressor(_Base):
     # packed, SUM-all-reduce-compatible stream (carry-free lanes for `world`)
     def encode(self, norm, tensor, world=1, idx=None, out=None):
         n = idx.numel() if idx is not None else tensor.numel()
-        rng = self._reserve(n, 1, tensor.device)
+        rng = self._reserve(n, 1, tensor.device, packed24=True)
         return self.backend.qsgd_encode(tensor, norm, self._quantization_level, rng, world, idx, out)
 
     def decode(self, norm, words, n, world=1, alpha=1.0, idx=None, out=None):

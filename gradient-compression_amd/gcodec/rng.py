@@ -112,8 +112,11 @@ class Generator:
         """The Philox key the next reservation uses (seed, + rank if per_rank)."""
         return self.seed + (_process_rank() if self.per_rank else 0)
 
-    def reserve(self, n: int, levels: int = 1, device=None, backend=None) -> Reservation:
-        """Reserve n*levels draws (advances the stream like torch's generator)."""
+    def reserve(self, n: int, levels: int = 1, device=None, backend=None, packed24: bool = False) -> Reservation:
+        """Reserve n*levels draws (advances the stream like torch's generator).
+        packed24 (torch mode, one level): the draws' low 24 bits packed 3 bytes
+        each where the run allows it (codec.mt19937_draws); only the QSGD
+        encode (gc_qsgd_encode) takes such a reservation."""
         count = n * levels
         if self.mode == "philox":
             r = Reservation(_lib.GC_RNG_PHILOX, self.reserve_key(), self.offset, None, n, levels)
@@ -121,6 +124,10 @@ class Generator:
             return r
         if backend is None:
             from . import codec as backend
+        if packed24 and levels == 1:
+            stream = backend.mt19937_draws(count, device, packed24=True)
+            kind = _lib.GC_RNG_STREAM24 if count and stream.numel() != count else _lib.GC_RNG_STREAM
+            return Reservation(kind, 0, 0, stream, n, levels)
         stream = backend.mt19937_draws(count, device)
         return Reservation(_lib.GC_RNG_STREAM, 0, 0, stream, n, levels)
 

@@ -71,11 +71,16 @@ extern "C" {
 /* random streams for the stochastic rounding */
 #define GC_RNG_PHILOX 0u /* Philox4x32-10 keyed by seed, counter (element>>2, level, offset) */
 #define GC_RNG_STREAM 1u /* caller-supplied 32-bit draws, level-major: stream[level*n + i] */
+/* caller-supplied draws packed to their low 24 bits, 3 bytes each, little-endian
+ * (element i at bytes 3i .. 3i+2; the rounding reads only those bits), one
+ * level: gc_qsgd_encode only (the torch-mode encode's draws from
+ * gc_mt19937_generate_split24_j); stream 4-byte aligned */
+#define GC_RNG_STREAM24 2u
 
 typedef void *gc_stream_t; /* hipStream_t */
 
 typedef struct gc_rng {
-    uint32_t kind;          /* GC_RNG_PHILOX | GC_RNG_STREAM */
+    uint32_t kind;          /* GC_RNG_PHILOX | GC_RNG_STREAM | GC_RNG_STREAM24 */
     uint32_t reserved;      /* 0 */
     uint64_t seed;          /* PHILOX key */
     uint64_t offset;        /* PHILOX: draws consumed before this call (counter high words) */
@@ -379,6 +384,13 @@ int gc_mt19937_generate_phase_j(uint32_t *state_dev, const uint32_t *table_dev, 
 int gc_mt19937_generate_split_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
                                 const uint32_t *end_coef, uint64_t end_block, uint32_t *out, uint64_t count,
                                 void *workspace, int phase, gc_stream_t stream);
+/* gc_mt19937_generate_split_j with the draws packed to 24 bits (the
+ * GC_RNG_STREAM24 layout: 3 count / 4 words of out).  idx = the state's read
+ * index (state_dev[624], which the caller sent); idx and count must be
+ * multiples of 4, so every 4 draws fill 3 whole words. */
+int gc_mt19937_generate_split24_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                  const uint32_t *end_coef, uint64_t end_block, uint32_t *out, uint64_t count,
+                                  uint64_t idx, void *workspace, int phase, gc_stream_t stream);
 /* torch-mode QSGD quantize with the MT19937 draws consumed in-kernel (never
  * stored): q[i] = sign(x_i)*xi_i exactly as compressors.py:299-316 computes it
  * under torch.bernoulli (one draw per element, in order), as GC_I8 (bits <= 7)

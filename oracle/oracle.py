@@ -59,6 +59,7 @@ def lib():
             "or_mt_seed": (None, [P, u64]),
             "or_mt_fill": (None, [P, P, u64]),
             "or_philox_draw": (u32, [u64, u64, u32, u64]),
+            "or_ms2_draw": (u32, [u64, u64, u32, u64]),
             "or_absmax": (f32, [P, u64]),
             "or_absmax_par": (f32, [P, u64, u32]),
             "or_qsgd_encode_par": (None, [P, u64, f32, u32, u32, P, P, u32]),
@@ -123,6 +124,11 @@ def stream_rng(draws: np.ndarray):
 
 def philox_draw(seed: int, offset: int, level: int, i: int) -> int:
     return int(lib().or_philox_draw(seed, offset, level, i))
+
+
+def ms2_draw(seed: int, offset: int, level: int, i: int) -> int:
+    """The dense two-level stream of the 2-level multi-scale codecs (24 bits)."""
+    return int(lib().or_ms2_draw(seed, offset, level, i))
 
 
 # --------------------------------------------------------------------------

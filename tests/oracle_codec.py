@@ -131,8 +131,9 @@ def ms_decode(words, mask_words, n, norm, levels, world=1, order=0, alpha=1.0, i
     return _place(dec, idx, out)
 
 
-def mt19937_draws(count, device=None):
-    """torch CPU-generator draws via the oracle MT; advances torch's state."""
+def mt19937_draws(count, device=None, packed24=False):
+    """torch CPU-generator draws via the oracle MT; advances torch's state
+    (always the plain 32-bit draws: packed24 is a device-side layout)."""
     from gcodec.rng import set_torch_mt_state, torch_mt_state
 
     words, idx = torch_mt_state()

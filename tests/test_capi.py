@@ -258,3 +258,24 @@ def test_ms_layouts_cached_and_exact():
         for a, b in ((ql, q2), (ml, m2)):
             assert bytes(a) == bytes(b)
     assert codec.ms_layouts(1000, (2, 4), 1)[0] is not codec.ms_layouts(1000, (2, 4), 2)[0]
+
+
+def test_stream24_contract_checked_on_host():
+    """The 24-bit packed draw layout (GC_RNG_STREAM24) is refused on the host
+    where it cannot hold: counts / read indices not multiples of 4 in the
+    generator, misaligned draws in the encode, any kind the multi-scale codecs
+    do not take.  Every refusal happens before a launch."""
+    from gcodec import _lib
+
+    lib = _lib.load()
+    fake = C.c_void_p(0x1000)
+    for count, idx in ((6, 0), (8, 2), (0, 0), (8, 625)):
+        assert lib.gc_mt19937_generate_split24_j(fake, fake, 1, 262_080, fake, 1, fake, count, idx, fake, 3,
+                                                 None) == _lib.GC_EINVAL
+        assert b"multiples of 4" in lib.gc_last_error()
+    lanes = _lib.gc_lanes()
+    assert lib.gc_qsgd_layout(1000, 4, 1, C.byref(lanes)) == _lib.GC_OK
+    rng = _lib.gc_rng(_lib.GC_RNG_STREAM24, 0, 0, 0, C.c_void_p(0x1002))
+    w = C.c_void_p(0x2000)
+    assert lib.gc_qsgd_encode(fake, None, 1000, fake, 4, C.byref(lanes), C.byref(rng), w, None) == _lib.GC_EINVAL
+    assert b"4-byte aligned" in lib.gc_last_error()

@@ -152,3 +152,53 @@ def test_release_drops_speculation_and_stays_exact():
         got = codec.mt19937_draws(200_003, DEV)
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint32), ref), i
+
+
+@pytest.mark.parametrize("count", [4, 624, 1_000_000, 2 * 262_080 + 8])
+def test_packed24_draws_are_the_low_bytes(count):
+    """gc_mt19937_generate_split24_j: 3 bytes per draw, little-endian, the
+    low 24 bits of exactly the draws the plain generator makes, and the same
+    state afterwards."""
+    torch.manual_seed(77)
+    ref, w2, i2 = _oracle_next(count)
+    got = codec.mt19937_draws(count, DEV, packed24=True)
+    torch.cuda.synchronize()
+    assert got.numel() == count // 4 * 3
+    b = got.cpu().numpy().view(np.uint8).reshape(-1, 3).astype(np.uint32)
+    assert np.array_equal(b[:, 0] | b[:, 1] << 8 | b[:, 2] << 16, ref & 0xFFFFFF)
+    words, idx = torch_mt_state()
+    assert idx == i2 and np.array_equal(words, w2)
+
+
+def test_packed24_encode_back_to_back_matches_plain_and_falls_back():
+    """The torch-mode encode with packed draws (the product's form, speculation
+    used on repeats) gives the same words as the plain draws, call after call;
+    a read index that is not a multiple of 4 (torch.rand(1) in between) falls
+    back to the plain draws, and the stream stays exact."""
+    n, bits = 1_000_000, 4
+    x = torch.from_numpy(O.gen_input(n, seed=8)).to(DEV)
+    nm = codec.absmax(x)
+    lanes = codec.qsgd_layout(n, bits, 1)
+    gen = gcodec.Generator(0, "torch")
+    from gcodec import _lib
+
+    def run(packed, steps):
+        torch.manual_seed(1234)
+        outs, kinds = [], []
+        for i in range(steps):
+            if i == 3:
+                torch.rand(1)  # read index now 1 mod 4
+            if i == 5:
+                torch.rand(3)  # and back to a multiple of 4
+            r = gen.reserve(n, packed24=packed)
+            kinds.append(r.kind)
+            outs.append(codec.qsgd_encode(x, nm, bits, r, 1, lanes=lanes).cpu().numpy())
+        return outs, kinds, torch_mt_state()
+
+    a, ka, sa = run(True, 8)
+    b, kb, sb = run(False, 8)
+    assert ka[:3] == [_lib.GC_RNG_STREAM24] * 3 and ka[3] == _lib.GC_RNG_STREAM and ka[5] == _lib.GC_RNG_STREAM24
+    assert set(kb) == {_lib.GC_RNG_STREAM}
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert np.array_equal(u, v), i
+    assert sa[1] == sb[1] and np.array_equal(sa[0], sb[0])

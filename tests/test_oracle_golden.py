@@ -238,3 +238,46 @@ def test_qsgdbp_golden_vs_oracle():
         sgn = np.where(sign == 1, np.float32(-1), np.float32(1))
         dec = (np.float32(norm) / np.float32(s) * sgn).astype(np.float32) * np.abs(q).astype(np.float32)
         assert dec.astype(np.float32).tobytes() == z[f"{c}/dec"].tobytes(), c
+
+
+# ---------------------------------------------------------------------------
+# Philox4x32-10: the published known-answer vectors (Salmon et al., SC'11;
+# Random123 kat_vectors) and the two draw layouts built on it
+# ---------------------------------------------------------------------------
+def _philox_py(ctr, key):
+    c, (k0, k1) = list(ctr), key
+    M = 0xFFFFFFFF
+    for _ in range(10):
+        p0, p1 = 0xD2511F53 * c[0], 0xCD9E8D57 * c[2]
+        c = [((p1 >> 32) ^ c[1] ^ k0) & M, p1 & M, ((p0 >> 32) ^ c[3] ^ k1) & M, p0 & M]
+        k0, k1 = (k0 + 0x9E3779B9) & M, (k1 + 0xBB67AE85) & M
+    return c
+
+
+@pytest.mark.parametrize("ctr,key,out", [
+    ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+    ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+    ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+     (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+])
+def test_philox_known_answers(ctr, key, out):
+    assert tuple(_philox_py(ctr, key)) == out
+    if ctr[1] == 0:  # the per-quad draw counter: (i >> 2, level << 16, offset), key = seed
+        seed, off = key[0] | key[1] << 32, ctr[2] | ctr[3] << 32
+        assert tuple(O.philox_draw(seed, off, 0, 4 * ctr[0] + e) for e in range(4)) == out
+
+
+def test_ms2_dense_draws_layout():
+    """Elements 8g..8g+7 at levels 0/1: 24-bit fields d = 8 level + e of the
+    3 blocks (g, b << 16, offset), b = 0..2 (gc_device.h ms2_*)."""
+    seed, off = 0x1234_5678_9ABC_DEF0, 0x0000_0003_0000_0007
+    for g in (0, 1, 77, 2**32 - 1, 2**32 + 5):
+        w = []
+        for b in range(3):
+            w += _philox_py((g & 0xFFFFFFFF, ((g >> 32) & 0xFFFF) | b << 16, off & 0xFFFFFFFF, off >> 32),
+                            (seed & 0xFFFFFFFF, seed >> 32))
+        bits = sum(v << (32 * k) for k, v in enumerate(w))
+        for lvl in (0, 1):
+            for e in range(8):
+                want = (bits >> (24 * (8 * lvl + e))) & 0xFFFFFF
+                assert O.ms2_draw(seed, off, lvl, 8 * g + e) == want

@@ -267,15 +267,78 @@ int main(int argc, char **argv)
         CK(hipMemcpy(hb.data(), b, bytes, hipMemcpyDeviceToHost));
         printf("%-40s == product: %s\n", nm, memcmp(ha.data(), hb.data(), bytes) == 0 ? "yes" : "NO");
     };
+    // launch shapes: per-quad kernels one quad per lane, octet kernels (dense
+    // two-level stream, ms_fast.h *_o2) two quads per lane, 64 lanes per tile
+    auto g4 = [](uint32_t M) { return dim3((M / 4 + 63) / 64); };
+    auto g8 = [](uint32_t M) { return dim3((M / 8 + 63) / 64); };
+    uint32_t cby = 0;
+    GK(gc_ms_cache_bytes(n, &lv, &cby));
+    uint8_t *cache, *cache2;
+    CK(hipMalloc(&cache, n * cby + 64));
+    CK(hipMalloc(&cache2, n * cby + 64));
+    const double cbytes = (double)n * cby;
+    auto p_maskc = [&] { GK(gc_ms_mask_encode_cached(x, n, norm, &lv, &rng, &ml, mw2, cache, nullptr)); };
+    auto p_selc = [&] { GK(gc_ms_select_cached(cache, n, &lv, mw, &ml, &ql, wq2, nullptr)); };
+    auto mask4 = [&](auto kern, uint32_t *dst, void *cdst) {
+        return [=] {
+            hipLaunchKernelGGL(kern, g4(Mm), dim3(256), 0, 0, x, n32, norm, la, fa, ra, Mm, ml.bits, lv.count - 1, dst,
+                               cdst, qmax, 3u);
+        };
+    };
+    auto mask8 = [&](auto kern, uint32_t *dst, void *cdst) {
+        return [=] {
+            hipLaunchKernelGGL(kern, g8(Mm), dim3(256), 0, 0, x, n32, norm, la, fa, ra, Mm, ml.bits, dst, cdst, qmax,
+                               3u);
+        };
+    };
+    auto sel = [&](auto kern, dim3 g, uint32_t *dst) {
+        return [=] {
+            hipLaunchKernelGGL(kern, g, dim3(256), 0, 0, x, n32, norm, la, fa, ra, mk, fd, Mq, ql.bits, qmax, dst);
+        };
+    };
+    const uint32_t rr = 32u / ql.per_word;
+    uint32_t *mw3, *wq3;
+    CK(hipMalloc(&mw3, (size_t)Mm * 4 + 64));
+    CK(hipMalloc(&wq3, (size_t)Mq * 4 + 64));
+    uint32_t Cw3 = 0;
+    for (uint32_t k = 0; k < ql.per_word; ++k)
+        Cw3 += (uint32_t)qmax << (k * ql.bits);
+    const uint32_t pend3 = (uint32_t)((n + Mm - 1) / Mm);
+    auto w1 = [&](auto kern, dim3 g) {
+        return [=] {
+            hipLaunchKernelGGL(kern, g, dim3(64 * rr), 0, 0, x, n32, norm, la, fa, ra, Mm, rr, ql.per_word, ql.bits,
+                               qmax, Cw3, pend3, mw3, wq3);
+        };
+    };
+    auto p_w1 = [&] { GK(gc_ms_encode_w1(x, n, norm, &lv, &rng, &ml, &ql, mw3, wq3, nullptr)); };
+
     p_mask();
     p_sel();
     p_dec(0)();
-    v_mask(k_ms_mask_fast<32, 0, 2, MSV_PERTHREAD>, mw2)();
-    cmp("mask PERTHREAD", mw, mw2, (size_t)Mm * 4);
-    v_sel(k_ms_select_fast<10, 0, 2, MSV_PERTHREAD>, wq2)();
-    cmp("select PERTHREAD", wq, wq2, (size_t)Mq * 4);
-    v_dec(k_ms_decode_fast<10, 0, 2, MSV_PERTHREAD>, out2)();
-    cmp("decode order 0 PERTHREAD", out, out2, n * 4);
+    mask8(k_ms_mask_fast_o2<32, 0, 0>, mw2, nullptr)();
+    cmp("mask octet unrolled", mw, mw2, (size_t)Mm * 4);
+    mask4(k_ms_mask_fast<32, 2, 2, 0, 0>, mw2, nullptr)();
+    cmp("mask per-quad dense", mw, mw2, (size_t)Mm * 4);
+    sel(k_ms_select_fast_o2<10, 0>, g8(Mq), wq2)();
+    cmp("select octet unrolled", wq, wq2, (size_t)Mq * 4);
+    sel(k_ms_select_fast<10, 2, 2, 0>, g4(Mq), wq2)();
+    cmp("select per-quad dense", wq, wq2, (size_t)Mq * 4);
+    p_maskc();
+    cmp("cached mask", mw, mw2, (size_t)Mm * 4);
+    mask8(k_ms_mask_fast_o2<32, 0, 1>, mw2, cache2)();
+    cmp("cached mask octet unrolled", mw, mw2, (size_t)Mm * 4);
+    cmp("cache cells octet unrolled", cache, cache2, (size_t)n * cby);
+    mask4(k_ms_mask_fast<32, 2, 2, 0, 1>, mw2, cache2)();
+    cmp("cache cells per-quad dense", cache, cache2, (size_t)n * cby);
+    p_selc();
+    cmp("select from cache", wq, wq2, (size_t)Mq * 4);
+    p_w1();
+    cmp("one-pass mask == two-pass", mw, mw3, (size_t)Mm * 4);
+    cmp("one-pass words == two-pass", wq, wq3, (size_t)Mq * 4);
+    w1(k_ms_fused_w1_o2<0>, g8(Mm))();
+    cmp("one-pass no-prefetch words", wq, wq3, (size_t)Mq * 4);
+    w1(k_ms_fused_w1<2, 2, MSV_EAGER0, 2>, g4(Mm))();
+    cmp("one-pass per-quad dense words", wq, wq3, (size_t)Mq * 4);
 
     // ---- settled interleaved A/B ----
     Timer T;
@@ -293,87 +356,24 @@ int main(int argc, char **argv)
     vs.push_back({"roof: read x (NT)", [&] {
                       hipLaunchKernelGGL(k_read_nt, dim3(4096), dim3(256), 0, 0, (const float4 *)x, n / 4, scratch);
                   }, xb, {}});
-    vs.push_back({"roof: 10 planes -> words (select pattern)", [&] {
-                      hipLaunchKernelGGL(k_rw_planar<10>, dim3(grid(Mq / 4)), dim3(256), 0, 0, x, Mq, wq2, n32);
-                  }, xb + qb, {}});
-    vs.push_back({"roof: 32 planes -> words (mask pattern)", [&] {
-                      hipLaunchKernelGGL(k_rw_planar<32>, dim3(grid(Mm / 4)), dim3(256), 0, 0, x, Mm, mw2, n32);
-                  }, xb + mb, {}});
-    vs.push_back({"roof: words -> 10 planes (decode pattern)", [&] {
-                      hipLaunchKernelGGL(k_wr_planar<10>, dim3(grid(Mq / 4)), dim3(256), 0, 0, wq, Mq, out2, n32);
-                  }, xb + qb, {}});
-    vs.push_back({"product mask encode", p_mask, xb + mb, {}});
-    vs.push_back({"lab mask split", v_mask64(k_ms_mask_fast<32, 0, 2, 0>, mw2), xb + mb, {}});
-    vs.push_back({"lab mask split NORNG", v_mask64(k_ms_mask_fast<32, 0, 2, MSV_NORNG>, mw2), xb + mb, {}});
-    vs.push_back({"lab mask split NOSLOW", v_mask64(k_ms_mask_fast<32, 0, 2, MSV_NOSLOW>, mw2), xb + mb, {}});
-    vs.push_back({"lab mask split NORNG|NOSLOW", v_mask64(k_ms_mask_fast<32, 0, 2, MSV_NORNG | MSV_NOSLOW>, mw2), xb + mb, {}});
-    vs.push_back({"lab mask PERTHREAD", v_mask(k_ms_mask_fast<32, 0, 2, MSV_PERTHREAD>, mw2), xb + mb, {}});
-    vs.push_back({"product select encode", p_sel, xb + mb + qb, {}});
-    vs.push_back({"lab select split NORNG", v_sel64(k_ms_select_fast<10, 0, 2, MSV_NORNG>, wq2), xb + mb + qb, {}});
-    vs.push_back({"lab select split NOSLOW", v_sel64(k_ms_select_fast<10, 0, 2, MSV_NOSLOW>, wq2), xb + mb + qb, {}});
-    vs.push_back({"lab select split NORNG|NOSLOW", v_sel64(k_ms_select_fast<10, 0, 2, MSV_NORNG | MSV_NOSLOW>, wq2), xb + mb + qb, {}});
-    vs.push_back({"lab select PERTHREAD", v_sel(k_ms_select_fast<10, 0, 2, MSV_PERTHREAD>, wq2), xb + mb + qb, {}});
-    // q cache (1 byte per element for [2, 4])
-    uint32_t cby = 0;
-    GK(gc_ms_cache_bytes(n, &lv, &cby));
-    uint8_t *cache;
-    CK(hipMalloc(&cache, n * cby + 64));
-    const double cbytes = (double)n * cby;
-    auto p_maskc = [&] { GK(gc_ms_mask_encode_cached(x, n, norm, &lv, &rng, &ml, mw2, cache, nullptr)); };
-    auto p_selc = [&] { GK(gc_ms_select_cached(cache, n, &lv, mw, &ml, &ql, wq2, nullptr)); };
-    p_maskc();
-    cmp("cached mask", mw, mw2, (size_t)Mm * 4);
-    p_selc();
-    cmp("select from cache", wq, wq2, (size_t)Mq * 4);
-    auto v_maskc = [&](auto kern) {
-        return [=] {
-            hipLaunchKernelGGL(kern, dim3((Mm / 4 + 63) / 64), dim3(256), 0, 0, x, n32, norm, la, fa, ra, Mm, ml.bits,
-                               lv.count - 1, mw2, (void *)cache, qmax, 3u);
-        };
-    };
-    vs.push_back({"product mask encode + cache", p_maskc, xb + mb + cbytes, {}});
-    vs.push_back({"lab mask + cache (product math)", v_maskc(k_ms_mask_fast<32, 0, 2, 0, 1>), xb + mb + cbytes, {}});
-    vs.push_back({"lab mask + cache NORNG", v_maskc(k_ms_mask_fast<32, 0, 2, MSV_NORNG, 1>), xb + mb + cbytes, {}});
-    vs.push_back({"lab mask + cache NORNG|NOSLOW", v_maskc(k_ms_mask_fast<32, 0, 2, MSV_NORNG | MSV_NOSLOW, 1>),
-                  xb + mb + cbytes, {}});
+    vs.push_back({"product mask encode (octet)", p_mask, xb + mb, {}});
+    vs.push_back({"mask octet unrolled", mask8(k_ms_mask_fast_o2<32, 0, 0>, mw2, nullptr), xb + mb, {}});
+    vs.push_back({"mask per-quad dense", mask4(k_ms_mask_fast<32, 2, 2, 0, 0>, mw2, nullptr), xb + mb, {}});
+    vs.push_back({"mask per-quad KIND0 (r03)", mask4(k_ms_mask_fast<32, 0, 2, 0, 0>, mw2, nullptr), xb + mb, {}});
+    vs.push_back({"product select encode (octet)", p_sel, xb + mb + qb, {}});
+    vs.push_back({"select octet unrolled", sel(k_ms_select_fast_o2<10, 0>, g8(Mq), wq2), xb + mb + qb, {}});
+    vs.push_back({"select per-quad dense", sel(k_ms_select_fast<10, 2, 2, 0>, g4(Mq), wq2), xb + mb + qb, {}});
+    vs.push_back({"select per-quad KIND0 (r03)", sel(k_ms_select_fast<10, 0, 2, 0>, g4(Mq), wq2), xb + mb + qb, {}});
+    vs.push_back({"product mask + cache (octet)", p_maskc, xb + mb + cbytes, {}});
+    vs.push_back({"mask + cache octet unrolled", mask8(k_ms_mask_fast_o2<32, 0, 1>, mw2, cache2), xb + mb + cbytes, {}});
+    vs.push_back({"mask + cache per-quad dense", mask4(k_ms_mask_fast<32, 2, 2, 0, 1>, mw2, cache2), xb + mb + cbytes, {}});
+    vs.push_back({"mask + cache per-quad KIND0 (r03)", mask4(k_ms_mask_fast<32, 0, 2, 0, 1>, mw2, cache2), xb + mb + cbytes, {}});
     vs.push_back({"product select from cache", p_selc, cbytes + mb + qb, {}});
-    vs.push_back({"lab select from cache, no mask reads", [&] {
-                      hipLaunchKernelGGL(k_sel_cache_nomask, dim3((Mq / 4 + 63) / 64), dim3(256), 0, 0, cache, n32, Mq,
-                                         ql.bits, 3u, wq2);
-                  }, cbytes + qb, {}});
-    // one-pass W = 1 encode (k_ms_fused_w1): product entry point and lab variants
-    const uint32_t rr = 32u / ql.per_word;
-    uint32_t *mw3, *wq3;
-    CK(hipMalloc(&mw3, (size_t)Mm * 4 + 64));
-    CK(hipMalloc(&wq3, (size_t)Mq * 4 + 64));
-    auto p_w1 = [&] { GK(gc_ms_encode_w1(x, n, norm, &lv, &rng, &ml, &ql, mw2, wq2, nullptr)); };
-    uint32_t Cw3 = 0;
-    for (uint32_t k = 0; k < ql.per_word; ++k)
-        Cw3 += (uint32_t)qmax << (k * ql.bits);
-    const uint32_t pend3 = (uint32_t)((n + Mm - 1) / Mm);
-    auto v_w1 = [&](auto kern) {
-        return [=] {
-            hipLaunchKernelGGL(kern, dim3((Mm / 4 + 63) / 64), dim3(64 * rr), 0, 0, x, n32, norm, la, fa, ra, Mm, rr,
-                               ql.per_word, ql.bits, qmax, Cw3, pend3, mw3, wq3);
-        };
-    };
-    p_w1();
-    cmp("one-pass mask == two-pass", mw, mw2, (size_t)Mm * 4);
-    cmp("one-pass words == two-pass", wq, wq2, (size_t)Mq * 4);
-    v_w1(k_ms_fused_w1<0, 2, MSV_NORNG>)();  // (lab variant: a different stream, run for the timing only)
-    v_w1(k_ms_fused_w1<0, 2, 0>)();  // the product's math compiled into the lab (GC_MS_WPE builds)
-    cmp("lab one-pass (product math) mask", mw3, mw2, (size_t)Mm * 4);
-    cmp("lab one-pass (product math) words", wq3, wq2, (size_t)Mq * 4);
-    vs.push_back({"product one-pass W=1 (mask + select)", p_w1, xb + mb + qb, {}});
-    vs.push_back({"lab one-pass (product math)", v_w1(k_ms_fused_w1<0, 2, 0>), xb + mb + qb, {}});
-    v_w1(k_ms_fused_w1<0, 2, MSV_EAGER0>)();
-    cmp("lab one-pass EAGER0 mask", mw3, mw2, (size_t)Mm * 4);
-    cmp("lab one-pass EAGER0 words", wq3, wq2, (size_t)Mq * 4);
-    vs.push_back({"lab one-pass EAGER0", v_w1(k_ms_fused_w1<0, 2, MSV_EAGER0>), xb + mb + qb, {}});
-    vs.push_back({"lab one-pass NORNG", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG>), xb + mb + qb, {}});
-    vs.push_back({"lab one-pass NORNG|NOSLOW", v_w1(k_ms_fused_w1<0, 2, MSV_NORNG | MSV_NOSLOW>), xb + mb + qb, {}});
+    vs.push_back({"product one-pass W=1 (octet)", p_w1, xb + mb + qb, {}});
+    vs.push_back({"one-pass octet no prefetch", w1(k_ms_fused_w1_o2<0>, g8(Mm)), xb + mb + qb, {}});
+    vs.push_back({"one-pass per-quad dense EAGER0 U2", w1(k_ms_fused_w1<2, 2, MSV_EAGER0, 2>, g4(Mm)), xb + mb + qb, {}});
+    vs.push_back({"one-pass per-quad KIND0 EAGER0 U2 (r03)", w1(k_ms_fused_w1<0, 2, MSV_EAGER0, 2>, g4(Mm)), xb + mb + qb, {}});
     vs.push_back({"product decode order 0", p_dec(0), xb + mb + qb, {}});
-    vs.push_back({"product decode order 1", p_dec(1), xb + mb + qb, {}});
     vs.push_back({"product absmax", [&] { gc_absmax_f32(x, nullptr, n, norm, nullptr, nullptr); }, xb, {}});
     for (auto &v : vs) {  // each variant once, synchronised, named first (a fault names its variant)
         printf("run-check %s\n", v.name);

@@ -31,7 +31,10 @@ def _short(name):
         if k in name:
             if k == "k_ms_mask_fast":  # <LM, KIND, NL, VAR, CBY>: CBY > 0 also writes the q cache
                 targs = name.split("<", 1)[1].split(">", 1)[0].split(",") if "<" in name else []
-                if len(targs) >= 5 and targs[4].strip() != "0":
+                # the octet kernel k_ms_mask_fast_o2<LM, VAR, CBY>
+                cby = targs[2] if "k_ms_mask_fast_o2" in name and len(targs) >= 3 else (
+                    targs[4] if len(targs) >= 5 else "0")
+                if cby.strip() != "0":
                     return k + "_cache"
             return k
     return name[:60]

@@ -46,8 +46,11 @@ def per_call(fn):
     return min(best)
 
 
+PACKED = os.environ.get("PACKED24", "1") == "1"  # the product's 24-bit packed draws (0: 32-bit draws)
+
+
 def enc():
-    codec.qsgd_encode(x, nm, 4, gen.reserve(n), 1, out=words, lanes=lanes)
+    codec.qsgd_encode(x, nm, 4, gen.reserve(n, packed24=PACKED), 1, out=words, lanes=lanes)
 
 
 def step():
