@@ -36,6 +36,14 @@ def _qdtype(bits: int) -> torch.dtype:
     return torch.int8 if bits < 8 else torch.int32
 
 
+# torch mode: whether the QSGD encode asks for 24-bit packed draws
+# (rng.Generator.reserve packed24).  Off: on MI355X the packed generator made
+# the back-to-back 1e8 encode slower, 0.39 against 0.34 ms per call
+# (profiles/r04p_torch_mode_ab.log) although it moves 200 MB less per call —
+# the call is bound by the side streams' jump + generator chain, not HBM.
+PACKED24_DRAWS = False
+
+
 class _Base:
     backend = _codec
 
@@ -71,7 +79,7 @@ class QSGDMaxNormCompressor(_Base):
     # packed, SUM-all-reduce-compatible stream (carry-free lanes for `world`)
     def encode(self, norm, tensor, world=1, idx=None, out=None):
         n = idx.numel() if idx is not None else tensor.numel()
-        rng = self._reserve(n, 1, tensor.device, packed24=True)
+        rng = self._reserve(n, 1, tensor.device, packed24=PACKED24_DRAWS)
         return self.backend.qsgd_encode(tensor, norm, self._quantization_level, rng, world, idx, out)
 
     def decode(self, norm, words, n, world=1, alpha=1.0, idx=None, out=None):

@@ -106,7 +106,7 @@ def qsgd_hook(state: QSGDHookState, bucket) -> torch.futures.Future:
     state.buckets += 1
     if state.levels is not None:
         return _multiscale(state, x, n, norm)
-    rng = state.gen.reserve(n, 1, device=x.device, backend=codec, packed24=True)
+    rng = state.gen.reserve(n, 1, device=x.device, backend=codec)
     words = codec.qsgd_encode(x, norm, state.bits, rng, W)
     state.bits_sent += 32 + 32 * words.numel()
 

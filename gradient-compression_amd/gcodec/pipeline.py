@@ -88,7 +88,7 @@ class ChunkedQSGDAllReduce:
         norm_ready.record(compute)
         self.dec_stream.wait_event(norm_ready)
         for (s, e), ln, wd in zip(self.bounds, self.lanes, self.words):
-            rng = self.gen.reserve(e - s, 1, device=self.device, backend=self.codec, packed24=True)
+            rng = self.gen.reserve(e - s, 1, device=self.device, backend=self.codec)
             self.codec.qsgd_encode(x[s:e], self.norm, self.bits, rng, W, out=wd, lanes=ln)
             mark("encode_end", compute)
             work = self._reduce(wd)

@@ -46,7 +46,7 @@ def per_call(fn):
     return min(best)
 
 
-PACKED = os.environ.get("PACKED24", "1") == "1"  # the product's 24-bit packed draws (0: 32-bit draws)
+PACKED = os.environ.get("PACKED24", "0") == "1"  # 24-bit packed draws (the product: 32-bit)
 
 
 def enc():
@@ -57,6 +57,16 @@ def step():
     codec.absmax(x, out=nm)
     enc()
 
+
+if os.environ.get("AB") == "1":  # interleaved A/B of the packed and plain draws, the product's G and depth
+    codec.mt_release()
+    for rep in range(4):
+        for packed in (True, False):
+            PACKED = packed
+            codec.mt_release()
+            print(f"AB rep {rep} packed24={packed}: encode {per_call(enc):.3f} ms, absmax + encode "
+                  f"{per_call(step):.3f} ms per call", flush=True)
+    sys.exit(0)
 
 for G in GS:
     for D in DS:
