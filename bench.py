@@ -778,6 +778,8 @@ def packers_leg(torch, gcodec, codec, dev, gen, rank) -> dict:
         c = comp.compress(x)
     torch.cuda.synchronize()
     t_c = (time.perf_counter() - t0) / 10 * 1e3
+    comp.decompress(c[0], c[1], c[2], n)  # warm: the unpack buffers' first allocation
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(10):
         comp.decompress(c[0], c[1], c[2], n)
@@ -786,7 +788,8 @@ def packers_leg(torch, gcodec, codec, dev, gen, rank) -> dict:
     res["qsgdbp_compress_ms"] = t_c
     res["qsgdbp_decompress_ms"] = t_d
     res["qsgdbp_note"] = ("compress = absmax + quantize_split + 2 device greedy4 packs + 3 host syncs (norm, word "
-                          "counts); the reference packs on the host at 0.56 M elem/s (BASELINE.md)")
+                          "counts); decompress = 2 device greedy4 unpacks (2 host syncs: value counts) + the fused "
+                          "combine (gc_qsgdbp_decode); the reference packs on the host at 0.56 M elem/s (BASELINE.md)")
     del x, xi, sg, q8, bw, pk
     return res
 

@@ -207,11 +207,46 @@ __global__ __launch_bounds__(kBlock) void k_byteunpack8_v(const int64_t *__restr
     }
 }
 
+// QSGDBP decompress (compressors.py:375-376): out = (c * sgn) * float(xi),
+// sgn = -1 where the unpacked sign bit is 1, else +1 — c * (+-1) is exact, so
+// one rounding, as the reference's fp32 tensor ops give (a negative x that
+// rounded to 0 decodes to -0.0).  Four elements per thread, 16-byte accesses.
+__global__ __launch_bounds__(kBlock) void k_qsgdbp_decode(const int32_t *__restrict__ sign, const int32_t *__restrict__ xi,
+                                                          uint64_t n, const float *__restrict__ cp, float *__restrict__ out)
+{
+    const float c = *cp, nc = -c;
+    const uint64_t quads = n >> 2;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t <= quads; t += (uint64_t)gridDim.x * kBlock) {
+        if (t == quads) {  // the n % 4 tail
+            for (uint64_t i = 4 * quads; i < n; ++i)
+                out[i] = (sign[i] == 1 ? nc : c) * (float)xi[i];
+            continue;
+        }
+        const int4 s = *reinterpret_cast<const int4 *>(sign + 4 * t);
+        const int4 q = *reinterpret_cast<const int4 *>(xi + 4 * t);
+        *reinterpret_cast<float4 *>(out + 4 * t) =
+            make_float4((s.x == 1 ? nc : c) * (float)q.x, (s.y == 1 ? nc : c) * (float)q.y,
+                        (s.z == 1 ? nc : c) * (float)q.z, (s.w == 1 ? nc : c) * (float)q.w);
+    }
+}
+
 }  // namespace gc
 
 using namespace gc;
 
 extern "C" {
+
+int gc_qsgdbp_decode(const int32_t *sign, const int32_t *xi, uint64_t n, const float *c, float *out,
+                     gc_stream_t stream)
+{
+    GC_REQUIRE(n == 0 || (sign && xi && c && out), "gc_qsgdbp_decode: null pointer");
+    GC_REQUIRE(aligned16(sign) && aligned16(xi) && aligned16(out), "gc_qsgdbp_decode: buffers must be 16-byte aligned");
+    if (n == 0)
+        return GC_OK;
+    hipLaunchKernelGGL(k_qsgdbp_decode, dim3(grid_for((n >> 2) + 1)), dim3(kBlock), 0, as_stream(stream), sign, xi, n, c,
+                       out);
+    return launch_status("gc_qsgdbp_decode");
+}
 
 int gc_mt19937_seed(uint64_t seed, uint32_t *state)
 {

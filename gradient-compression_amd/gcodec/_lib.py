@@ -135,6 +135,7 @@ SIGNATURES = {
     "gc_mt19937_generate_phase_j": (C.c_int, [P, P, u64, u64, P, u64, P, C.c_int, P]),
     "gc_mt19937_generate_split_j": (C.c_int, [P, P, u64, u64, P, u64, P, u64, P, C.c_int, P]),
     "gc_mt19937_generate_split24_j": (C.c_int, [P, P, u64, u64, P, u64, P, u64, u64, P, C.c_int, P]),
+    "gc_qsgdbp_decode": (C.c_int, [P, P, u64, P, P, P]),
     "gc_randk_workspace_size": (C.c_size_t, []),
     "gc_randk_gather_absmax": (C.c_int, [P, P, u64, P, P, P, P]),
     "gc_randk_encode_w1": (C.c_int, [P, P, u64, P, P, u32, LANESP, RNGP, P, P, P]),

@@ -948,11 +948,13 @@ MT_WAIT_NEXT_JUMPS = False  # consumers also wait for the speculative run's jump
 
 
 def mt_pipe_generators(count: int) -> int:
-    """Generators of one pipelined torch-mode run: about one per 780k draws
-    (128 for 1e8), at least the latency rule's count for small calls."""
+    """Generators of one pipelined torch-mode run: about one per 390k draws
+    (256 for 1e8).  Swept on MI355X at 1e8, back to back (tools/time_torch_mode.py):
+    128 generators 0.39-0.43 ms per encode, 192 0.31-0.39, 256 0.31-0.37
+    (profiles/r04d_torch_mode_sweep.log, r04o_torch_mode_32bit.log)."""
     if MT_PIPE_GENERATORS:
         return int(MT_PIPE_GENERATORS)
-    return max(1, min(MT_MAX_GENERATORS, -(-count // 781_250)))
+    return max(1, min(MT_MAX_GENERATORS, -(-count // 390_625)))
 
 
 def mt_pipe_generator_draws(count: int) -> int:
@@ -1199,6 +1201,20 @@ def byteunpack8(words: torch.Tensor) -> torch.Tensor:
     words = words.contiguous().view(-1).to(torch.int64)
     out = torch.empty(8 * words.numel(), dtype=torch.int8, device=dev)
     check(_lib.load().gc_byteunpack8(_p(words), words.numel(), _p(out), _stream(dev)), "gc_byteunpack8")
+    return out
+
+
+def qsgdbp_decode(sign: torch.Tensor, xi: torch.Tensor, c: torch.Tensor, n: int) -> torch.Tensor:
+    """QSGDBPCompressor.decompress's combine (compressors.py:375-376) in one
+    kernel: (c * (+-1)) * float(xi) over the first n unpacked values."""
+    dev = _dev(xi)
+    sign = sign.contiguous().view(-1).to(torch.int32)
+    xi = xi.contiguous().view(-1).to(torch.int32)
+    if sign.numel() < n or xi.numel() < n:
+        raise _lib.GCodecError(_lib.GC_EINVAL, "qsgdbp_decode: fewer unpacked values than n")
+    ct = c.reshape(1).to(device=dev, dtype=torch.float32)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    check(_lib.load().gc_qsgdbp_decode(_p(sign), _p(xi), n, _p(ct), _p(out), _stream(dev)), "gc_qsgdbp_decode")
     return out
 
 

@@ -142,8 +142,12 @@ class QSGDBPCompressor(_Base):
 
     def decompress(self, norm, sign_packed, xi_packed, tensor_size):
         n = int(tensor_size)
-        sign = self.backend.greedy4_unpack(sign_packed)[:n]
-        xi = self.backend.greedy4_unpack(xi_packed)[:n]
+        sign = self.backend.greedy4_unpack(sign_packed)
+        xi = self.backend.greedy4_unpack(xi_packed)
+        fused = getattr(self.backend, "qsgdbp_decode", None)
+        if fused is not None and xi.is_cuda:
+            return fused(sign, xi, norm, n)  # one kernel (gc_qsgdbp_decode)
+        sign, xi = sign[:n], xi[:n]
         # norm * sign * xi in the reference's order, fp32: (c * (+-1)) is exact, then one
         # rounding; a negative x that rounded to 0 decodes to -0.0 as in the reference
         sgn = torch.where(sign == 1, -1.0, 1.0).to(torch.float32)

@@ -410,6 +410,11 @@ int64_t gc_greedy4_unpack(const int32_t *src, uint64_t nwords, int32_t *out, uin
 /* 8 x (v & 0xFF) per int64, MSB-first (extensions/Extension CPU BP), device */
 int gc_bytepack8(const void *src, uint32_t src_dtype, uint64_t n, int64_t *out, gc_stream_t stream);
 int gc_byteunpack8(const int64_t *src, uint64_t nwords, int8_t *out, gc_stream_t stream);
+/* QSGDBPCompressor.decompress (compressors.py:375-376) after the two greedy4
+ * unpacks: out[i] = (*c * (sign[i] == 1 ? -1 : 1)) * (float)xi[i], device
+ * buffers, 16-byte aligned (c = RN(norm / s) as compress returns it) */
+int gc_qsgdbp_decode(const int32_t *sign, const int32_t *xi, uint64_t n, const float *c, float *out,
+                     gc_stream_t stream);
 /* host-buffer forms (the reference's byte packer is a CPU extension) */
 int gc_bytepack8_host(const int64_t *src, uint64_t n, int64_t *out);
 int gc_byteunpack8_host(const int64_t *src, uint64_t nwords, int8_t *out);

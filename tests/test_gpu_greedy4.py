@@ -110,3 +110,20 @@ def test_device_packer_unaligned_source():
     assert d.data_ptr() % 16 != 0
     host = codec.greedy4_pack(torch.from_numpy(a[1:].copy()))
     assert np.array_equal(codec.greedy4_pack(d).cpu().numpy(), host.numpy())
+
+
+@pytest.mark.parametrize("n", [1, 7, 4099, 23_520_842])
+def test_qsgdbp_fused_decode_equals_reference_ops(n):
+    """gc_qsgdbp_decode == the reference's fp32 ops (c * sgn) * float(xi)
+    (compressors.py:375-376) bit for bit, -0.0 for a negative x rounded to 0,
+    any n % 4 tail, on oversized unpack buffers (whole words)."""
+    g = torch.Generator(device=DEV).manual_seed(n)
+    m = n + 13
+    sign = torch.randint(0, 2, (m,), device=DEV, generator=g, dtype=torch.int32)
+    xi = torch.randint(0, 16, (m,), device=DEV, generator=g, dtype=torch.int32)
+    c = torch.tensor([0.0123], device=DEV)
+    got = codec.qsgdbp_decode(sign, xi, c, n)
+    sgn = torch.where(sign[:n] == 1, -1.0, 1.0).to(torch.float32)
+    ref = (c * sgn) * xi[:n].to(torch.float32)
+    assert got.shape == (n,)
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), ref.cpu().numpy().view(np.uint32))
