@@ -1,4 +1,6 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-PYTEST_K="greedy4 or qsgdbp or packer or torch_mode" bash tools/gpu.sh r04q tests || exit $?
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 --legs packers,torch --cpu-seconds 0 > gpurun_out/bench_legs_r04q.log 2>&1
+for q in 4 8 16; do
+  echo "== GPU_MAX_HW_QUEUES=$q" >> gpurun_out/torch_hwq_r04r.log
+  GPU_MAX_HW_QUEUES=$q timeout -k 10 250 python tools/time_torch_mode.py 128,256 2,3 >> gpurun_out/torch_hwq_r04r.log 2>&1 || exit $?
+done
