@@ -1,7 +1,6 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-PYTEST_K="greedy4 or qsgdbp or packer" bash tools/gpu.sh r04z tests || exit $?
-for L in 1 0 1 0; do
-  GC_G4_LOOP=$L timeout -k 10 300 python bench.py --steps 5 --warmup 2 --legs packers --cpu-seconds 0 > gpurun_out/packers_loop${L}_r04z.log 2>&1 || exit $?
-  grep -o '"greedy4_pack_[a-z]*": {"us": [0-9.]*' gpurun_out/packers_loop${L}_r04z.log | sed "s/^/loop=$L /" >> gpurun_out/packers_ab_r04z.log
+for b in lab_ms lab_ms_wpe6 lab_ms_wpe7 lab_ms; do
+  echo "== $b" >> gpurun_out/lab_ms_wpe_r04zb.log
+  timeout -k 10 200 tools/$b 2>&1 | grep "^product one\|^lab one-pass octet PREFETCH\|^lab mask + cache octet ROLL\|^lab select octet ROLL\|^product mask + cache\|^product select encode" >> gpurun_out/lab_ms_wpe_r04zb.log || exit $?
 done

@@ -370,6 +370,11 @@ int main(int argc, char **argv)
     vs.push_back({"mask + cache per-quad KIND0 (r03)", mask4(k_ms_mask_fast<32, 0, 2, 0, 1>, mw2, cache2), xb + mb + cbytes, {}});
     vs.push_back({"product select from cache", p_selc, cbytes + mb + qb, {}});
     vs.push_back({"product one-pass W=1 (octet)", p_w1, xb + mb + qb, {}});
+    // the product's octet configurations compiled into the lab (GC_MS_WPE builds pin their occupancy)
+    vs.push_back({"lab one-pass octet PREFETCH", w1(k_ms_fused_w1_o2<MSV_PREFETCH>, g8(Mm)), xb + mb + qb, {}});
+    vs.push_back({"lab mask + cache octet ROLL", mask8(k_ms_mask_fast_o2<32, MSV_ROLL, 1>, mw2, cache2),
+                  xb + mb + cbytes, {}});
+    vs.push_back({"lab select octet ROLL", sel(k_ms_select_fast_o2<10, MSV_ROLL>, g8(Mq), wq2), xb + mb + qb, {}});
     vs.push_back({"one-pass octet no prefetch", w1(k_ms_fused_w1_o2<0>, g8(Mm)), xb + mb + qb, {}});
     vs.push_back({"one-pass per-quad dense EAGER0 U2", w1(k_ms_fused_w1<2, 2, MSV_EAGER0, 2>, g4(Mm)), xb + mb + qb, {}});
     vs.push_back({"one-pass per-quad KIND0 EAGER0 U2 (r03)", w1(k_ms_fused_w1<0, 2, MSV_EAGER0, 2>, g4(Mm)), xb + mb + qb, {}});
