@@ -807,6 +807,110 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
     }
 }
 
+// the same with two adjacent word quads per lane (8 elements of a plane: one
+// 8- / 16-byte cell load, twice the bytes in flight per wave; Mq % 8 == 0)
+template <int LQ, int NL, int CBY>
+__global__ __launch_bounds__(kBlock) void k_ms_select_cache_o2(const void *__restrict__ cache, uint32_t n, MaskArg mk,
+                                                               FastDiv fd, uint32_t Mq, uint32_t wq, uint32_t cb,
+                                                               uint32_t *__restrict__ words)
+{
+    const uint32_t cm = (1u << cb) - 1u;
+    const uint32_t octs = Mq >> 3;
+    constexpr int PW = (LQ + 3) / 4;
+    __shared__ uint4 part[3][2][kMsQuadsPerBlock];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    typedef typename CacheCell<CBY>::T T;
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < octs; tb += gridDim.x * kMsQuadsPerBlock) {
+        const uint32_t t = tb + lane;
+        uint4 acc[2] = {};
+        if (t < octs) {
+            // every plane's cells and mask words are loaded before any is used
+            uint2 c[PW][2];
+            uint4 mw[PW][2][NL - 1];
+            uint32_t shm[PW][2];
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                const uint32_t p = wave + 4u * j;
+                const uint32_t i0 = p * Mq + 8u * t;
+#pragma unroll
+                for (int hq = 0; hq < 2; ++hq) {
+                    c[j][hq] = make_uint2(0u, 0u);
+                    shm[j][hq] = 0;
+#pragma unroll
+                    for (int f = 0; f < NL - 1; ++f)
+                        mw[j][hq][f] = make_uint4(0u, 0u, 0u, 0u);
+                }
+                if (p < (uint32_t)LQ && i0 < n) {
+                    if (i0 + 8 <= n) {  // 8 cells in one load (i0 % 8 == 0: 8 CBY-byte aligned)
+                        const T *cp = reinterpret_cast<const T *>(cache) + i0;
+                        if constexpr (CBY == 1) {
+                            const uint2 u = *reinterpret_cast<const uint2 *>(cp);
+                            c[j][0] = make_uint2(u.x, 0u);
+                            c[j][1] = make_uint2(u.y, 0u);
+                        } else {
+                            const uint4 u = *reinterpret_cast<const uint4 *>(cp);
+                            c[j][0] = make_uint2(u.x, u.y);
+                            c[j][1] = make_uint2(u.z, u.w);
+                        }
+                    } else {
+                        c[j][0] = cache_load<CBY>(cache, i0, n);
+                        if (i0 + 4 < n)
+                            c[j][1] = cache_load<CBY>(cache, i0 + 4, n);
+                    }
+#pragma unroll
+                    for (int hq = 0; hq < 2; ++hq) {
+                        const uint32_t iq = i0 + 4u * hq;
+                        if (hq == 1 && iq >= n)
+                            break;
+                        const uint32_t plane = fdiv(iq, fd);
+                        const uint32_t pos = iq - plane * fd.d;
+                        shm[j][hq] = plane * mk.w;
+#pragma unroll
+                        for (int f = 0; f < NL - 1; ++f)
+                            mw[j][hq][f] = *reinterpret_cast<const uint4 *>(mk.words + (uint64_t)f * mk.M + pos);
+                    }
+                }
+            }
+            const uint32_t msk = (1u << mk.w) - 1u;
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                const uint32_t p = wave + 4u * j;  // planes past LQ / n contribute c = 0
+                const uint32_t sh = p < (uint32_t)LQ ? p * wq : 0u;
+#pragma unroll
+                for (int hq = 0; hq < 2; ++hq) {
+                    const uint4 cj = cache_cells<CBY>(c[j][hq]);
+                    uint4 m = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+                    for (int f = 0; f < NL - 1; ++f) {
+                        m.x += ((mw[j][hq][f].x >> shm[j][hq]) & msk) == mk.world;
+                        m.y += ((mw[j][hq][f].y >> shm[j][hq]) & msk) == mk.world;
+                        m.z += ((mw[j][hq][f].z >> shm[j][hq]) & msk) == mk.world;
+                        m.w += ((mw[j][hq][f].w >> shm[j][hq]) & msk) == mk.world;
+                    }
+                    acc[hq].x += ((cj.x >> (m.x * cb)) & cm) << sh;
+                    acc[hq].y += ((cj.y >> (m.y * cb)) & cm) << sh;
+                    acc[hq].z += ((cj.z >> (m.z * cb)) & cm) << sh;
+                    acc[hq].w += ((cj.w >> (m.w * cb)) & cm) << sh;
+                }
+            }
+        }
+        if (wave) {
+            part[wave - 1][0][lane] = acc[0];
+            part[wave - 1][1][lane] = acc[1];
+        }
+        __syncthreads();
+        if (wave == 0 && t < octs) {
+#pragma unroll
+            for (int hq = 0; hq < 2; ++hq) {
+                const uint4 a = part[0][hq][lane], b = part[1][hq][lane], c = part[2][hq][lane];
+                st_nt4u(words + 8u * t + 4u * hq, make_uint4(acc[hq].x + a.x + b.x + c.x, acc[hq].y + a.y + b.y + c.y,
+                                                             acc[hq].z + a.z + b.z + c.z, acc[hq].w + a.w + b.w + c.w));
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // W = 1: mask + select in ONE pass (compressors.py:778-817 with the MIN
 // all-reduce of reducer.py:1680 over a single rank, the identity: the common

@@ -364,6 +364,17 @@ static uint64_t ms_tiles()
 // the ResNet50 bucket, 73 against 57 VGPRs; U = 3 the same as 2:
 // profiles/r03s_ms_sweep_u*.log).  GC_MS_FUSED_U=1 selects the one-plane loop
 // (measurement only)
+// the select from the q cache with two word quads per lane (k_ms_select_cache_o2);
+// GC_MS_SELECT_CACHE_OCTETS=0 keeps one quad per lane (A/B)
+static bool ms_select_cache_octets()
+{
+    static const bool on = [] {
+        const char *e = getenv("GC_MS_SELECT_CACHE_OCTETS");
+        return !(e && atol(e) == 0);
+    }();
+    return on;
+}
+
 static int ms_fused_u()
 {
     static const int u = [] {
@@ -692,11 +703,23 @@ int gc_ms_select_cached(const void *cache, uint64_t n, const gc_levels *levels, 
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_cache<LL, NL_, CBY_>), dim3(g), dim3(kBlock), 0, \
                                                          st, cache, (uint32_t)n, mk, fd, Mq, q_lanes->bits, cg.cb,    \
                                                          words))
-    if (levels->count == 2) {
+#define GC_SC8(NL_, CBY_)                                                                                           \
+    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_cache_o2<LL, NL_, CBY_>), dim3(g8), dim3(kBlock), \
+                                                         0, st, cache, (uint32_t)n, mk, fd, Mq, q_lanes->bits, cg.cb, \
+                                                         words))
+    if (Mq % 8 == 0 && ms_select_cache_octets()) {  // two quads per lane
+        const unsigned g8 = (unsigned)std::max<uint64_t>(1, (ms_grid(Mq >> 3) + ms_tiles() - 1) / ms_tiles());
+        if (levels->count == 2) {
+            if (cg.bytes == 1) { GC_SC8(2, 1); } else { GC_SC8(2, 2); }
+        } else {
+            if (cg.bytes == 1) { GC_SC8(3, 1); } else { GC_SC8(3, 2); }
+        }
+    } else if (levels->count == 2) {
         if (cg.bytes == 1) { GC_SC(2, 1); } else { GC_SC(2, 2); }
     } else {
         if (cg.bytes == 1) { GC_SC(3, 1); } else { GC_SC(3, 2); }
     }
+#undef GC_SC8
 #undef GC_SC
     return launch_status(what);
 }
