@@ -627,6 +627,10 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_sums(const int32_t *__restri
 }
 
 constexpr unsigned G4U_SCAN_THREADS = 1024;
+// up to this many unpack blocks (4 M words) each emit block sums the block
+// totals itself (k_g4u_emit_nb: <= 16 loads per thread from L2) instead of a
+// one-block scan launch
+constexpr uint64_t G4U_NB_DIRECT = 4096;
 
 __global__ __launch_bounds__(G4U_SCAN_THREADS) void k_g4u_scan(const uint32_t *__restrict__ bsum, uint64_t nb,
                                                                uint64_t *__restrict__ bbase,
@@ -686,6 +690,79 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit(const int32_t *__restri
     __syncthreads();
     const uint64_t base = bbase[blockIdx.x];
     for (uint32_t k = threadIdx.x; k < tot; k += G4_THREADS)
+        out[base + k] = (int32_t)obuf[k];
+}
+
+// the emit without a scan launch: each block sums the block totals before it
+// (its base) and all of them (the count and the capacity check) from the
+// L2-resident bsum, so no block writes past cap and nothing is written on
+// NOSPC; block 0 writes *count and *status (the workspace and result need no
+// initialisation launch)
+__device__ __forceinline__ uint64_t g4u_wave_sum(uint64_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(G4_THREADS) void k_g4u_emit_nb(const int32_t *__restrict__ words, uint64_t nw,
+                                                            const uint32_t *__restrict__ bsum, uint64_t nb,
+                                                            int32_t *__restrict__ out, uint64_t cap,
+                                                            uint64_t *__restrict__ count, uint32_t *__restrict__ status)
+{
+    __shared__ uint8_t obuf[G4U_BLOCK_WORDS * 15];
+    __shared__ uint64_t red[2][G4_THREADS / 64];
+    const unsigned t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint64_t b = blockIdx.x;
+    uint64_t pre = 0, all = 0;
+    for (uint64_t k = t; k < nb; k += G4_THREADS) {
+        const uint32_t v = bsum[k];
+        all += v;
+        pre += k < b ? v : 0u;
+    }
+    pre = g4u_wave_sum(pre);
+    all = g4u_wave_sum(all);
+    if (lane == 0) {
+        red[0][wv] = pre;
+        red[1][wv] = all;
+    }
+    const uint64_t w0 = b * G4U_BLOCK_WORDS + (uint64_t)t * G4U_PER_THREAD;
+    const int4 w4 = g4u_words(words, nw, w0);
+    uint32_t tot;
+    uint32_t o = block_excl_scan<G4_THREADS>(g4u_cnt4(w4, nw, w0), &tot);  // its barriers publish red
+    uint64_t base = 0, total = 0;
+#pragma unroll
+    for (unsigned i = 0; i < G4_THREADS / 64; ++i) {
+        base += red[0][i];
+        total += red[1][i];
+    }
+    if (b == 0 && t == 0) {
+        *count = total;
+        *status = total > cap ? G4_STATUS_NOSPC : 0u;
+    }
+    if (total > cap)
+        return;
+    const int32_t wv4[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+    for (uint32_t i = 0; i < G4U_PER_THREAD; ++i) {
+        if (w0 + i >= nw)
+            break;
+        const uint32_t code = (uint32_t)wv4[i];
+        const int mode = (int)(code >> 30);
+        const uint32_t cnt = g4_cnt(mode), top = g4_top(mode), bb = g4_bits(mode);
+        const uint32_t mask = (1u << bb) - 1u;
+#pragma unroll
+        for (uint32_t j = 0; j < 15; ++j)
+            if (j < cnt)
+                obuf[o + j] = (uint8_t)((code >> (top - j * bb)) & mask);
+        o += cnt;
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < tot; k += G4_THREADS)
         out[base + k] = (int32_t)obuf[k];
 }
 
@@ -797,11 +874,17 @@ int gc_greedy4_unpack_device(const int32_t *words, uint64_t nwords, int32_t *out
     hipStream_t st = as_stream(stream);
     G4Ws w;
     g4u_ws(nwords, reinterpret_cast<char *>(workspace), &w);
+    const uint64_t nb = (nwords + G4U_BLOCK_WORDS - 1) / G4U_BLOCK_WORDS;
+    if (nwords > 0 && nb <= G4U_NB_DIRECT) {  // every block sums the block totals itself: two launches
+        hipLaunchKernelGGL(k_g4u_sums, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bsum);
+        hipLaunchKernelGGL(k_g4u_emit_nb, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bsum, nb, out,
+                           cap, count, status);
+        return launch_status("gc_greedy4_unpack_device");
+    }
     hipLaunchKernelGGL(k_g4_init, dim3(1), dim3(256), 0, st, count, status, nullptr, (uint64_t)0, nullptr,
                        (uint64_t)0);
     if (nwords == 0)
         return launch_status("gc_greedy4_unpack_device");
-    const uint64_t nb = (nwords + G4U_BLOCK_WORDS - 1) / G4U_BLOCK_WORDS;
     hipLaunchKernelGGL(k_g4u_sums, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bsum);
     hipLaunchKernelGGL(k_g4u_scan, dim3(1), dim3(G4U_SCAN_THREADS), 0, st, w.bsum, nb, w.bbase, count, cap, status);
     hipLaunchKernelGGL(k_g4u_emit, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bbase, out, status);

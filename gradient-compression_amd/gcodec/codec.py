@@ -1266,7 +1266,7 @@ class Greedy4Device:
 
 def greedy4_pack(src: torch.Tensor) -> torch.Tensor:
     """The reference's greedy 4-mode format (extensions/Extension CPU/bitpacking.cpp:5-124).
-    Device tensors: HIP list-ranking packer (gc_greedy4_pack_device); host
+    Device tensors: HIP segment-table scan packer (gc_greedy4_pack_device); host
     tensors: the host packer, like the reference's CPU extension."""
     lib = _lib.load()
     if src.is_cuda:

@@ -6,6 +6,7 @@ host packer on inputs that stress the boundaries (32-position segments,
 8192-position tiles, 128-tile groups, the top walk past 64 groups):
 all-mode-0 runs, all-mode-3 runs, mixes, ragged ends, and the QSGDBP call
 site's ResNet50 bucket (23,520,842 sign bits and 4-bit magnitudes)."""
+import ctypes as C
 import os
 
 import numpy as np
@@ -127,3 +128,35 @@ def test_qsgdbp_fused_decode_equals_reference_ops(n):
     ref = (c * sgn) * xi[:n].to(torch.float32)
     assert got.shape == (n,)
     assert np.array_equal(got.cpu().numpy().view(np.uint32), ref.cpu().numpy().view(np.uint32))
+
+
+@pytest.mark.parametrize("nwords", [1, 1000, 5000, 5_000_000])
+def test_device_unpack_capacity_writes_nothing(nwords):
+    """gc_greedy4_unpack_device with too small a cap: status 2, the count is
+    still reported, and not one output element is written (both the
+    two-launch form, where every block checks the total itself, and the scan
+    form above 4 M words); with enough cap the values come back."""
+    from gcodec import _lib
+
+    lib = _lib.load()
+    rng = np.random.default_rng(nwords)
+    vals = rng.integers(128, 256, 3 * nwords).astype(np.int32)  # 3 values per word (mode 3)
+    vals[rng.integers(0, vals.size, vals.size // 50)] = 1      # and some shorter runs
+    w = codec.greedy4_pack(torch.from_numpy(vals).to(DEV))
+    nw = w.numel()
+    need = int(codec.greedy4_unpack(w).numel())
+    ws = torch.empty(int(lib.gc_greedy4_unpack_workspace_size(nw)), dtype=torch.uint8, device=DEV)
+    for cap, ok in ((need - 1, False), (need, True)):
+        out = torch.full((need + 8,), -7, dtype=torch.int32, device=DEV)
+        res = torch.full((2,), 123, dtype=torch.int64, device=DEV)
+        assert lib.gc_greedy4_unpack_device(C.c_void_p(w.data_ptr()), nw, C.c_void_p(out.data_ptr()), cap,
+                                            C.c_void_p(res.data_ptr()), C.c_void_p(res.data_ptr() + 8),
+                                            C.c_void_p(ws.data_ptr()), None) == 0
+        torch.cuda.synchronize()
+        count, status = int(res[0].item()), int(res[1].item()) & 0xFFFFFFFF
+        assert count == need
+        if ok:
+            assert status == 0
+            assert torch.equal(out[:need], codec.greedy4_unpack(w))
+        else:
+            assert status == 2 and bool((out == -7).all())
