@@ -163,12 +163,17 @@ __global__ __launch_bounds__(kBlock) void k_decode_scatter1(const uint32_t *__re
 // unpacked quantize / dequantize (the literal compress()/decompress() drop-in)
 // ---------------------------------------------------------------------------
 // SPLIT (the QSGDBP call site, compressors.py:344-353): q = xi (>= 0) and
-// sgn = 1 iff x < 0 as two int32 arrays, the greedy packer's two inputs
+// sgn = 1 iff x < 0 as two int32 arrays, the greedy packer's two inputs.
+// vst: the outputs take one vector store per 4 elements (q, sgn 16-byte /
+// int8 q and le 4-byte aligned; host-checked) — per-element stores of 4
+// scattered lanes made the split 1.9x slower than its bytes (88 us at the
+// ResNet50 size)
 template <int KIND, int MODE, typename QT, bool SPLIT = false>
 __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float *__restrict__ x, uint64_t n,
                                                           const float *__restrict__ normp, float s, uint32_t level,
                                                           RngArgs rng, QT *__restrict__ q, int8_t *__restrict__ le,
-                                                          int32_t le_max, int32_t *__restrict__ sgn = nullptr)
+                                                          int32_t le_max, uint32_t vst,
+                                                          int32_t *__restrict__ sgn = nullptr)
 {
     const float norm = *normp;
     const uint64_t groups = (n + 3) >> 2;
@@ -176,6 +181,29 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float *__restric
         const uint64_t i0 = g << 2;
         const float4 v = load4<MODE>(x, nullptr, i0, n);
         const uint4 r = draws4<KIND>(rng, level, i0);
+        if (vst && i0 + 4 <= n) {
+            int32_t a[4], b[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const QElem qe = q_elem(pickf(v, e), norm, s, pick(r, e));
+                a[e] = SPLIT ? qe.xi : qe.sg * qe.xi;
+                b[e] = SPLIT ? (pickf(v, e) < 0.0f ? 1 : 0) : (qe.xi <= le_max ? 1 : 0);
+            }
+            if constexpr (sizeof(QT) == 4) {
+                *reinterpret_cast<int4 *>(q + i0) = make_int4(a[0], a[1], a[2], a[3]);
+            } else {
+                *reinterpret_cast<uint32_t *>(q + i0) = (uint32_t)(a[0] & 0xff) | (uint32_t)(a[1] & 0xff) << 8 |
+                                                        (uint32_t)(a[2] & 0xff) << 16 | (uint32_t)a[3] << 24;
+            }
+            if constexpr (SPLIT) {
+                *reinterpret_cast<int4 *>(sgn + i0) = make_int4(b[0], b[1], b[2], b[3]);
+            } else {
+                if (le)
+                    *reinterpret_cast<uint32_t *>(le + i0) =
+                        (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24;
+            }
+            continue;
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             if (i0 + e < n) {
@@ -565,9 +593,11 @@ int gc_qsgd_quantize_le(const float *x, uint64_t n, const float *norm, uint32_t 
     const int32_t le_max = le_mask ? (int32_t)((1u << le_bits) - 1u) : 0;
     const unsigned grid = grid_for((n + 3) >> 2);
     const bool vec = aligned16(x);
+    const uint32_t vst = (q_dtype == GC_I8 ? (reinterpret_cast<uintptr_t>(q) & 3u) == 0 : aligned16(q)) &&
+                         (!le_mask || (reinterpret_cast<uintptr_t>(le_mask) & 3u) == 0);
 #define GC_Q(KIND_, MODE_, QT_)                                                                                  \
     hipLaunchKernelGGL((k_qsgd_quantize<KIND_, MODE_, QT_>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, sf, level, \
-                       ra, reinterpret_cast<QT_ *>(q), le_mask, le_max)
+                       ra, reinterpret_cast<QT_ *>(q), le_mask, le_max, vst)
     if (rng->kind == GC_RNG_PHILOX) {
         if (q_dtype == GC_I8) {
             if (vec) GC_Q(0, 0, int8_t); else GC_Q(0, 1, int8_t);
@@ -599,9 +629,10 @@ int gc_qsgd_quantize_split(const float *x, uint64_t n, const float *norm, uint32
     const float sf = (float)((1u << bits) - 1u);
     const unsigned grid = grid_for((n + 3) >> 2);
     const bool vec = aligned16(x);
+    const uint32_t vst = aligned16(xi) && aligned16(sign);
 #define GC_QS(KIND_, MODE_)                                                                                         \
     hipLaunchKernelGGL((k_qsgd_quantize<KIND_, MODE_, int32_t, true>), dim3(grid), dim3(kBlock), 0, st, x, n, norm, \
-                       sf, 0u, ra, xi, nullptr, 0, sign)
+                       sf, 0u, ra, xi, nullptr, 0, vst, sign)
     if (rng->kind == GC_RNG_PHILOX) {
         if (vec) GC_QS(0, 0); else GC_QS(0, 1);
     } else {
