@@ -760,7 +760,7 @@ def packers_leg(torch, gcodec, codec, dev, gen, rank) -> dict:
         w = pk.words[:nw].clone()
         us_p = _events(torch, lambda: pk.pack(src), 20) * 1e3
         pk.unpack(w)
-        cnt = pk.result()
+        cnt = pk.unpack_result()
         ok = bool(torch.equal(pk.values[:n], src))
         us_u = _events(torch, lambda: pk.unpack(w), 20) * 1e3
         res[f"greedy4_pack_{name}"] = row(us_p, 4 * n + 4 * nw, words=nw)

@@ -9,46 +9,49 @@
 // [0, 255] (the reference corrupts negatives and loops forever on >= 256).
 //
 // The word starts form a chain next(i) = i + CNT[mode(i)] from i = 0: a scan
-// whose elements are FUNCTIONS.  Cut the positions into segments of 32; a
-// word that starts in one segment ends at most 14 positions into the next, so
-// a segment maps the offset its first word starts at (0..14, or 15 = past n)
-// to the offset its chain leaves at and the words it emitted: a 16-entry
-// table, and tables compose associatively.
-//   k_g4_init      zero the result pair and the per-group tickets
-//   k_g4p_tile     per 8192-element tile (256 threads x one segment): window
-//                  masks by SWAR byte tests and OR-doubling, the segment table
-//                  by a backward recurrence held in registers (static indices
-//                  only), a reduction tree of the 256 tables in LDS -> the
-//                  tile's table; the bytes go to the workspace for phase 2.
-//                  The last tile of each 128-tile group to finish (a ticket;
-//                  ready bits, no fence) builds and stores the group's tree.
-//   k_g4p_top      only for > 64 groups: one block walks the group roots ->
-//                  group entry offsets and word bases, the total
-//   k_g4p_emit     per tile: its entry = walk of the group roots (<= 64
-//                  groups) + the left siblings down the group tree; the tile
-//                  tree again from the bytes, a down-sweep -> every segment's
-//                  entry and word base; each thread packs its segment's words
-//                  into LDS, the block stores the tile's words coalesced.
-// HBM: src read once (4n), the bytes written and read (2n), the words written.
-// Unpack: per-word element counts -> block sums -> one-block scan -> decode
-// into LDS -> coalesced stores.
+// whose elements are FUNCTIONS.  A range of positions maps the offset its
+// first word starts at (0..14, or 15 = the chain has passed n) to the offset
+// its chain leaves at and the words it emitted: a 16-entry table (exit |
+// words << 4), and tables compose associatively.
+//
+// Pack: ONE persistent launch, one 1024-thread workgroup per CU (k_g4p_one).
+// Round r, block b owns tile r*G + b (C positions, <= 98,304):
+//   1. the tile's values -> LDS as bytes (+ a 16-byte halo), range check;
+//   2. per thread 96 positions: window classes (SWAR byte tests + OR
+//      doubling), the table by a backward recurrence chained over three
+//      32-position blocks (registers only, static indices);
+//   3. per wave a tree of its 64 tables in LDS (u16 entries, 16 lanes per
+//      node pair; only LEFT children are kept — the walk down needs nothing
+//      else), then a 16-leaf tree of the wave roots -> the tile's table;
+//   4. the table goes out as 16 {entry, tag} granules (8-byte sc1 stores),
+//      one arrival add per block; every block waits for the round's G
+//      arrivals, reads all G tables (sc1) and composes them (bpermute, then a
+//      4-ary tree in LDS) -> its entry state and word base, the round's exit
+//      state and total, and whether any tile held a value outside [0, 255];
+//   5. walking down the trees gives every thread its entry and word base;
+//      it packs its words from the LDS bytes straight to `out`.
+// HBM: src read once (4n), the words written once — the algorithmic bytes.
+// The workspace (header + granules, 64 KB) must be zero before its first use;
+// every call leaves it so (the last block re-arms it).
+//
+// Unpack: per-word element counts -> block sums -> decode into LDS ->
+// coalesced stores.
 #include "gc_device.h"
 #include "gc_host.h"
 
 #include <algorithm>
+#include <atomic>
+
+#ifndef GC_G4_STRICT  // 1: the release/acquire form of the table hand-off (see g1_store_granule)
+#define GC_G4_STRICT 0
+#endif
 
 namespace gc {
 
-constexpr unsigned G4_THREADS = 256;
-constexpr uint32_t G4_SEG = 32;                         // positions per segment (one thread)
-constexpr uint32_t G4_TILE = G4_SEG * G4_THREADS;       // 8192 positions per tile
-constexpr uint32_t G4_GROUP = 128;                      // tiles per group
-constexpr uint32_t G4_GDEPTH = 7;                       // log2(G4_GROUP)
+constexpr unsigned G4_THREADS = 256;                    // unpack blocks
+constexpr uint32_t G4_SEG = 32;                         // positions per table block
 constexpr uint32_t G4_DEAD = 15;                        // table state: the chain has passed n
-constexpr uint32_t G4_TOP_CHUNK = 128;                  // group tables staged in LDS per top step
-constexpr uint32_t G4_WALK_MAX = 64;                    // groups the emit blocks walk themselves (else k_g4p_top)
-constexpr uint32_t G4_STATUS_RANGE = 1u, G4_STATUS_NOSPC = 2u;
-constexpr uint32_t G4_READY = 0x80000000u;              // agg entry written (tile tables need < 2^16)
+constexpr uint32_t G4_STATUS_RANGE = 1u, G4_STATUS_NOSPC = 2u, G4_STATUS_TIMEOUT = 4u;
 
 // per-mode constants as nibble / byte tables in an immediate (a per-lane mode
 // index into __constant__ arrays became vector memory loads in the emit loops)
@@ -65,36 +68,20 @@ __device__ __forceinline__ uint32_t byte_flags(uint32_t w, uint32_t hi)
     return ((y & 0x80808080u) * 0x00204081u) >> 28;           // gather the 4 top bits
 }
 
-// table entries: exit offset (4 bits) | words << 4
-
-struct G4Tile {
-    uint32_t v[(G4_TILE + 32) / 4];  // values as bytes (0 past n), 32-byte halo
-    uint16_t node[2 * G4_THREADS][16];  // reduction tree: leaves 256..511, root 1
-};
-
-// a group's tree of tile tables (u32 entries: words up to 256 x 2731)
-struct G4GroupTree {
-    uint32_t node[2 * G4_GROUP][16];
-};
-
-// the mode classes of this thread's segment (bit p = position seg0 + p), from
-// the window masks W15 = some value >= 4 in [p, p+15), W7 = some value >= 16
-// in [p, p+7), W4 = some value >= 128 in [p, p+4).  W4 ⊆ W7 ⊆ W15, so the
-// mode at p is W15[p] + W7[p] + W4[p] = 2 hi[p] + lo[p] with hi = W7 and
+// the mode classes of a 32-position block (bit p = position p), from the
+// window masks W15 = some value >= 4 in [p, p+15), W7 = some value >= 16 in
+// [p, p+7), W4 = some value >= 128 in [p, p+4).  W4 ⊆ W7 ⊆ W15, so the mode at
+// p is W15[p] + W7[p] + W4[p] = 2 hi[p] + lo[p] with hi = W7 and
 // lo = W15 ^ W7 ^ W4 (0: 15 x 2 bits, 1: 7 x 4, 2: 4 x 7, 3: 3 x 8).
 struct G4Cls {
     uint32_t lo, hi;
 };
 
-__device__ __forceinline__ G4Cls g4_classes(const G4Tile &sm)
+// w: the block's 8 dwords of bytes + the next 4 (windows reach +14)
+__device__ __forceinline__ G4Cls g4_classes(const uint32_t *w)
 {
-    constexpr int DW = G4_SEG / 4 + 4;  // the segment's dwords + 16 bytes of the next (windows reach +14)
-    const unsigned t = threadIdx.x;
-    uint32_t w[DW];
-#pragma unroll
-    for (int k = 0; k < DW; k += 4)
-        *reinterpret_cast<uint4 *>(&w[k]) = *reinterpret_cast<const uint4 *>(&sm.v[(G4_SEG / 4) * t + k]);
-    uint64_t ge4 = 0, ge16 = 0, ge128 = 0;  // bit j: byte j (position seg0 + j)
+    constexpr int DW = G4_SEG / 4 + 4;
+    uint64_t ge4 = 0, ge16 = 0, ge128 = 0;  // bit j: byte j
 #pragma unroll
     for (int k = 0; k < DW; ++k) {
         ge4 |= (uint64_t)byte_flags(w[k], 0xfcfcfcfcu) << (4 * k);
@@ -117,21 +104,22 @@ __device__ __forceinline__ uint32_t g4_mode(const G4Cls &c, uint32_t p)
 // bit p of m as a lane mask (0 or ~0): one v_bfe_i32
 __device__ __forceinline__ uint32_t bitmask(uint32_t m, int p) { return (uint32_t)__builtin_amdgcn_sbfe((int)m, p, 1); }
 
-// the segment table (entries 0..14, exit | words << 4) by the backward
-// recurrence f[p] = 1 word + f[p + cnt(p)], where a successor past the
-// segment is its offset there, p + cnt - G4_SEG (0..14).  All indices are
-// static (the recurrence is unrolled), so f stays in registers; the
-// successor is picked with three bitfield selects on the class bits.
-// TAIL: the tile holds position n (positions >= live are past the chain's end).
+// one 32-position block's table by the backward recurrence
+// f[p] = 1 word + f[p + cnt(p)]; a successor past the block is entry
+// p + cnt - 32 of the NEXT block's table fn (identity for a thread's last
+// block: the offset into the next thread's range).  All indices are static
+// (the recurrence is unrolled), so f stays in registers; the successor is
+// picked with three bitfield selects on the class bits.  TAIL: positions >=
+// live are past n (the chain has ended there).
 template <bool TAIL>
-__device__ __forceinline__ void g4_dp(const G4Cls &c, uint32_t live, uint32_t f[G4_SEG])
+__device__ __forceinline__ void g4_dp(const G4Cls &c, uint32_t live, const uint32_t fn[15], uint32_t f[G4_SEG])
 {
 #pragma unroll
     for (int p = G4_SEG - 1; p >= 0; --p) {
-        const uint32_t s3 = p + 3 < (int)G4_SEG ? f[(p + 3) % G4_SEG] : (uint32_t)(p + 3 - (int)G4_SEG);
-        const uint32_t s4 = p + 4 < (int)G4_SEG ? f[(p + 4) % G4_SEG] : (uint32_t)(p + 4 - (int)G4_SEG);
-        const uint32_t s7 = p + 7 < (int)G4_SEG ? f[(p + 7) % G4_SEG] : (uint32_t)(p + 7 - (int)G4_SEG);
-        const uint32_t s15 = p + 15 < (int)G4_SEG ? f[(p + 15) % G4_SEG] : (uint32_t)(p + 15 - (int)G4_SEG);
+        const uint32_t s3 = p + 3 < (int)G4_SEG ? f[(p + 3) % G4_SEG] : fn[(p + 3 - (int)G4_SEG) % 15];
+        const uint32_t s4 = p + 4 < (int)G4_SEG ? f[(p + 4) % G4_SEG] : fn[(p + 4 - (int)G4_SEG) % 15];
+        const uint32_t s7 = p + 7 < (int)G4_SEG ? f[(p + 7) % G4_SEG] : fn[(p + 7 - (int)G4_SEG) % 15];
+        const uint32_t s15 = p + 15 < (int)G4_SEG ? f[(p + 15) % G4_SEG] : fn[(p + 15 - (int)G4_SEG) % 15];
         const uint32_t mlo = bitmask(c.lo, p), mhi = bitmask(c.hi, p);
         // mode 3: s3, 2: s4, 1: s7, 0: s15
         const uint32_t nx = (mhi & ((mlo & s3) | (~mlo & s4))) | (~mhi & ((mlo & s7) | (~mlo & s15)));
@@ -142,405 +130,448 @@ __device__ __forceinline__ void g4_dp(const G4Cls &c, uint32_t live, uint32_t f[
     }
 }
 
-// reduction tree over the NLEAF leaves node[NLEAF + i] -> node[1] (u16 tile
-// tree of 256 segments, u32 group tree of G4_GROUP tiles).  Level by level (unrolled: every level's trip count
-// is a constant); node i = left child then right child, a thread per (node,
-// entry) pair: entry e = t & 15 of nodes lvl + (t >> 4) + 16 r, so 16
-// consecutive lanes read one row (conflict-free) at immediate LDS offsets.
-// Composition: exit from the right child's entry at the left's exit, words
-// added — (x & ~15) + y.  A level's lookups are all issued before its stores
-// (the rows written are never read on the same level).
-template <typename T, uint32_t NLEAF>
-__device__ __forceinline__ void g4_tree_up(T (*node)[16])
+// ---- one-pass pack ----------------------------------------------------------
+constexpr unsigned G1_THREADS = 1024;
+constexpr unsigned G1_WAVES = G1_THREADS / 64;            // 16
+constexpr uint32_t G1_BLK = 3;                            // 32-position blocks per thread
+constexpr uint32_t G1_RANGE = G4_SEG * G1_BLK;            // 96 positions per thread
+constexpr uint32_t G1_TILE_MAX = G1_THREADS * G1_RANGE;   // 98,304 positions per block and round
+constexpr uint32_t G1_GMAX = 256;                         // blocks of the persistent grid (<= one per CU)
+constexpr uint32_t G1_LB = 12;                            // 16-byte loads in flight per thread (tile load)
+constexpr uint32_t G1_MIN_TILE = 16384;                   // small buckets: fewer, larger tiles
+constexpr uint64_t G1_TIMEOUT_TICKS = 1ull << 27;         // s_memrealtime (100 MHz): ~1.3 s, then status 4
+static_assert(G1_TILE_MAX / 4 <= 2 * G1_LB * G1_THREADS, "two load batches cover a tile");
+
+// workspace: the header's words on lines of their own, then the granules
+// (two round parities x G1_GMAX tiles x 16 entries x {entry, tag})
+struct G1Hdr {
+    uint64_t arrive;        // +1 per block per round, never reset
+    uint64_t pad0[15];
+    uint64_t abase;         // arrive at the start of the next launch
+    uint32_t done;          // blocks finished (the last one re-arms)
+    uint32_t tmo;           // a block gave up waiting
+    uint64_t pad1[14];
+};
+static_assert(sizeof(G1Hdr) == 256, "header size");
+constexpr uint64_t G1_WS_BYTES = sizeof(G1Hdr) + 2ull * G1_GMAX * 16 * 8;
+
+struct G1Smem {
+    alignas(16) uint32_t v[G1_TILE_MAX / 4 + 4];            // the tile's values as bytes + 16-byte halo (96 KB)
+    uint32_t pl[G1_WAVES][63][8];               // per wave: the left children of its tree (u16 x 16 a row)
+    union {
+        uint32_t tr[G1_WAVES][32][8];           // per wave: right children of the level in flight
+        uint32_t t0[G1_GMAX][16];               // the round's tile tables
+    } u;
+    uint32_t g4[G1_GMAX / 4][16];               // compositions of 4 / 16 / 64 tiles
+    uint32_t g16[G1_GMAX / 16][16];
+    uint32_t g64[G1_GMAX / 64][16];
+    uint32_t x[32][16];                         // the tree of the 16 wave roots (nodes 1..31)
+    uint64_t base_b;                            // the block's word base within the round
+    uint32_t s_b, s_end, tw, flag;
+};
+
+// the waves of a workgroup run one LDS tree each: order a wave's LDS stores
+// before its later loads of other lanes' rows (LDS executes a wave's
+// instructions in order; this keeps the compiler from moving them)
+__device__ __forceinline__ void wave_lds_sync()
 {
-    static_assert(NLEAF <= 256 && (NLEAF & (NLEAF - 1)) == 0, "tree width");
-    const uint32_t t = threadIdx.x, e = t & 15u, i0 = t >> 4;
-#pragma unroll
-    for (int L = 7; L >= 0; --L) {
-        if ((1u << L) >= NLEAF)
-            continue;
-        const uint32_t lvl = 1u << L;
-        __syncthreads();
-        if (lvl >= 16) {
-            constexpr uint32_t RMAX = 8;
-            const uint32_t R = lvl / 16;
-            uint32_t res[RMAX];
-#pragma unroll
-            for (uint32_t r = 0; r < RMAX; ++r) {
-                if (r < R) {
-                    const uint32_t i = lvl + i0 + 16 * r;
-                    const uint32_t x = node[2 * i][e], y = node[2 * i + 1][x & 15u];
-                    res[r] = (x & ~15u) + y;
-                }
-            }
-#pragma unroll
-            for (uint32_t r = 0; r < RMAX; ++r)
-                if (r < R)
-                    node[lvl + i0 + 16 * r][e] = (T)res[r];
-        } else if (i0 < lvl) {
-            const uint32_t i = lvl + i0;
-            const uint32_t x = node[2 * i][e], y = node[2 * i + 1][x & 15u];
-            node[i][e] = (T)((x & ~15u) + y);
-        }
-    }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
 }
 
-// load tile `tile` of the values into LDS as bytes (0 past n) + halo.
-// From int32 src (range-checked; the bytes also go to vb) or from vb.  A tile
-// whose halo lies before n (every tile but the last one or two) issues all its
-// loads before using any (the guarded form made each wait for the previous).
-template <bool FROM_SRC, bool ALIGNED>
-__device__ __forceinline__ void g4_load(G4Tile &sm, const int32_t *__restrict__ src, uint8_t *__restrict__ vb,
-                                        uint64_t n, uint64_t start, uint32_t *__restrict__ status)
+__device__ __forceinline__ uint32_t g1_apply(uint32_t x, uint32_t &s)  // table entry -> words, new state
 {
-    constexpr uint32_t QT = G4_TILE / 4, QH = (G4_TILE + 32) / 4;  // dwords of the tile / with the halo
-    constexpr uint32_t J = QT / G4_THREADS;                          // full rounds (8)
-    const unsigned t = threadIdx.x;
-    if (start + 4ull * QH <= n && (!FROM_SRC || ALIGNED)) {
-        if (FROM_SRC) {
-            typedef int i4v __attribute__((ext_vector_type(4)));
-            int4 v[J + 1];
+    s = x & 15u;
+    return x >> 4;
+}
+
+// the hand-off of the round's tile tables (MI355X_MICROARCH.md, row 1 of the
+// sc1 table): 8-byte sc1 granule stores, drained, then one agent-scope add per
+// block; readers poll the count with sc1 loads and read the granules with sc1
+// loads.  GC_G4_STRICT: plain stores + an agent release fence before the add,
+// an agent acquire fence after the poll, plain loads — the memory model's own
+// form (slower; kept so the hardware-observed form can be switched off).
+__device__ __forceinline__ void g1_store_granule(uint64_t *p, uint64_t v)
+{
+#if GC_G4_STRICT
+    *p = v;
+#else
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
+__device__ __forceinline__ uint64_t g1_load_granule(const uint64_t *p)
+{
+#if GC_G4_STRICT
+    return *(const volatile uint64_t *)p;
+#else
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ uint32_t g1_load_tile(G1Smem &sm, const int32_t *__restrict__ src, uint64_t n,
+                                                 uint64_t start, uint32_t C, unsigned t)
+{
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    const uint32_t QT = C / 4;  // dwords of the tile (C is a multiple of 96)
+    uint32_t bad = 0;
+    for (uint32_t q0 = 0; q0 < QT + 4; q0 += G1_LB * G1_THREADS) {
+        int4 v[G1_LB];
+        const bool full = ALIGNED && q0 + G1_LB * G1_THREADS <= QT && start + 4ull * (q0 + G1_LB * G1_THREADS) <= n;
+        if (full) {  // uniform: every load in bounds, all issued before any is used
 #pragma unroll
-            for (uint32_t j = 0; j < J; ++j) {  // src is streamed once: nontemporal
-                const i4v r = __builtin_nontemporal_load(reinterpret_cast<const i4v *>(src + start) + j * G4_THREADS + t);
+            for (uint32_t j = 0; j < G1_LB; ++j) {
+                const i4v r = __builtin_nontemporal_load(reinterpret_cast<const i4v *>(src + start) + q0 +
+                                                         j * G1_THREADS + t);
                 v[j] = make_int4(r.x, r.y, r.z, r.w);
             }
-            if (t < QH - QT)
-                v[J] = *(reinterpret_cast<const int4 *>(src + start) + QT + t);
-            uint32_t bad = 0;
-#pragma unroll
-            for (uint32_t j = 0; j <= J; ++j) {
-                if (j == J && t >= QH - QT)
-                    break;
-                const uint32_t q = j * G4_THREADS + t;
-                bad |= (uint32_t)v[j].x | (uint32_t)v[j].y | (uint32_t)v[j].z | (uint32_t)v[j].w;
-                const uint32_t packed = __builtin_amdgcn_perm(__builtin_amdgcn_perm(v[j].w, v[j].z, 0x0c0c0400u),
-                                                              __builtin_amdgcn_perm(v[j].y, v[j].x, 0x0c0c0400u),
-                                                              0x05040100u);
-                if (j < J)
-                    reinterpret_cast<uint32_t *>(vb + start)[q] = packed;
-                sm.v[q] = packed;
-            }
-            if (bad > 255u)
-                atomicOr(status, G4_STATUS_RANGE);
         } else {
-            uint32_t v[J + 1];
 #pragma unroll
-            for (uint32_t j = 0; j < J; ++j)
-                v[j] = reinterpret_cast<const uint32_t *>(vb + start)[j * G4_THREADS + t];
-            if (t < QH - QT)
-                v[J] = reinterpret_cast<const uint32_t *>(vb + start)[QT + t];
-#pragma unroll
-            for (uint32_t j = 0; j < J; ++j)
-                sm.v[j * G4_THREADS + t] = v[j];
-            if (t < QH - QT)
-                sm.v[QT + t] = v[J];
-        }
-        __syncthreads();
-        return;
-    }
-    bool bad = false;
-    for (uint32_t q = t; q < QH; q += G4_THREADS) {  // the tail: guarded element loads
-        const uint64_t g = start + 4ull * q;
-        uint32_t packed = 0;
-        if (FROM_SRC) {
-            int4 v = make_int4(0, 0, 0, 0);
-            if (g + 4 <= n) {
-                if (ALIGNED)
-                    v = *reinterpret_cast<const int4 *>(src + g);
-                else
-                    v = make_int4(src[g], src[g + 1], src[g + 2], src[g + 3]);
-            } else if (g < n) {
-                v.x = src[g];
-                v.y = g + 1 < n ? src[g + 1] : 0;
-                v.z = g + 2 < n ? src[g + 2] : 0;
-            }
-            bad |= ((uint32_t)v.x | (uint32_t)v.y | (uint32_t)v.z | (uint32_t)v.w) > 255u;
-            packed = __builtin_amdgcn_perm(__builtin_amdgcn_perm(v.w, v.z, 0x0c0c0400u),
-                                           __builtin_amdgcn_perm(v.y, v.x, 0x0c0c0400u), 0x05040100u);
-            if (q < QT && g < n)
-                *reinterpret_cast<uint32_t *>(vb + g) = packed;  // vb is padded to whole tiles
-        } else if (g < n) {
-            packed = *reinterpret_cast<const uint32_t *>(vb + g);  // zero past n (written so by k_g4p_tile)
-        }
-        sm.v[q] = packed;
-    }
-    if (FROM_SRC && bad)
-        atomicOr(status, G4_STATUS_RANGE);
-    __syncthreads();
-}
-
-// this thread's segment table (leaves) from the tile's LDS bytes; written to
-// node[256 + t] (and returned packed, 8 u32)
-__device__ __forceinline__ G4Cls g4_leaf(G4Tile &sm, uint64_t start, uint64_t n, uint4 &l0, uint4 &l1)
-{
-    const unsigned t = threadIdx.x;
-    const G4Cls c = g4_classes(sm);
-    uint32_t f[G4_SEG];
-    const uint64_t seg0 = start + G4_SEG * t;
-    if (start + G4_TILE <= n) {  // uniform: a full tile has no position past n
-        g4_dp<false>(c, G4_SEG, f);
-    } else {
-        const uint32_t live = seg0 >= n ? 0u : (uint32_t)std::min<uint64_t>(G4_SEG, n - seg0);
-        g4_dp<true>(c, live, f);
-    }
-    uint32_t h[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-        h[e] = f[2 * e] | ((2 * e + 1 == 15 ? G4_DEAD : f[2 * e + 1]) << 16);
-    l0 = make_uint4(h[0], h[1], h[2], h[3]);
-    l1 = make_uint4(h[4], h[5], h[6], h[7]);
-    uint4 *leaf = reinterpret_cast<uint4 *>(sm.node[G4_THREADS + t]);
-    leaf[0] = l0;
-    leaf[1] = l1;
-    return c;
-}
-
-// Phase 1 per tile: its table -> agg.  The last tile block of a group to
-// finish (a relaxed agent-scope ticket) builds the group's tree of tile
-// tables and stores all of it (gtree: 511 nodes x 16 u32).  No fence: every
-// agg entry is a single agent-scope atomic store carrying a ready bit (bit 31,
-// cleared by k_g4_init), and the winner reads each entry with agent-scope
-// atomic loads until its bit is set — coherence of single locations is all it
-// needs.  (A release fence per block writes back the whole L2 on gfx950:
-// measured 102 against 40 us for the kernel.)
-template <bool ALIGNED>
-__global__ __launch_bounds__(G4_THREADS) void k_g4p_tile(const int32_t *__restrict__ src, uint64_t n,
-                                                         uint64_t tiles, uint8_t *__restrict__ vb,
-                                                         uint4 *__restrict__ leaves, uint2 *__restrict__ cls,
-                                                         uint32_t *__restrict__ agg, uint32_t *__restrict__ gtree,
-                                                         uint32_t *__restrict__ gcount, uint32_t *__restrict__ status)
-{
-    __shared__ union {
-        G4Tile tile;
-        G4GroupTree grp;
-    } sm;
-    __shared__ uint32_t is_last;
-    const unsigned t = threadIdx.x;
-    const uint64_t tile = blockIdx.x, start = tile * G4_TILE;
-    g4_load<true, ALIGNED>(sm.tile, src, vb, n, start, status);
-    uint4 l0, l1;
-    const G4Cls c = g4_leaf(sm.tile, start, n, l0, l1);
-    const uint64_t seg = tile * G4_THREADS + t;  // the emit reads these instead of recomputing them
-    leaves[2 * seg] = l0;
-    leaves[2 * seg + 1] = l1;
-    cls[seg] = make_uint2(c.lo, c.hi);
-    g4_tree_up<uint16_t, G4_THREADS>(sm.tile.node);
-    if (t < 16)
-        __hip_atomic_store(&agg[tile * 16 + t], (uint32_t)sm.tile.node[1][t] | G4_READY, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t g = tile / G4_GROUP, first = g * G4_GROUP;
-    const uint32_t cnt = (uint32_t)std::min<uint64_t>(G4_GROUP, tiles - first);
-    __syncthreads();
-    if (t == 0)
-        is_last = __hip_atomic_fetch_add(&gcount[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == cnt - 1;
-    __syncthreads();
-    if (!is_last)
-        return;
-    // leaves of the group tree; past the group's end: identity.  All loads are
-    // issued first; an entry whose ready bit is not visible yet is re-read
-    constexpr uint32_t R = G4_GROUP * 16 / G4_THREADS;
-    static_assert(R * G4_THREADS == G4_GROUP * 16, "leaf loads per thread");
-    uint32_t x[R];
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r) {
-        const uint32_t k = t + r * G4_THREADS, i = k >> 4;
-        x[r] = i < cnt ? __hip_atomic_load(&agg[(first + i) * 16 + (k & 15u)], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)
-                       : (k & 15u) | G4_READY;
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r) {
-        const uint32_t k = t + r * G4_THREADS, i = k >> 4;
-        while (!(x[r] & G4_READY))  // its block took a ticket, so the store is done; visibility may lag
-            x[r] = __hip_atomic_load(&agg[(first + i) * 16 + (k & 15u)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sm.grp.node[G4_GROUP + i][k & 15u] = x[r] & ~G4_READY;
-    }
-    g4_tree_up<uint32_t, G4_GROUP>(sm.grp.node);
-    uint4 *dst = reinterpret_cast<uint4 *>(gtree + g * (2 * G4_GROUP * 16));
-    const uint4 *srcn = reinterpret_cast<const uint4 *>(sm.grp.node);
-    for (uint32_t k = t; k < 2 * G4_GROUP * 4; k += G4_THREADS)
-        dst[k] = srcn[k];
-}
-
-// groups > G4_WALK_MAX: one block walks the group roots from offset 0 ->
-// each group's entry offset and word base, the total and the capacity check
-__global__ __launch_bounds__(G4_THREADS) void k_g4p_top(const uint32_t *__restrict__ gtree, uint64_t groups,
-                                                        uint32_t *__restrict__ gentry, uint64_t *__restrict__ gbase,
-                                                        uint64_t *__restrict__ nwords, uint64_t cap,
-                                                        uint32_t *__restrict__ status)
-{
-    __shared__ uint32_t t16[G4_TOP_CHUNK * 16];
-    uint32_t state = 0;
-    uint64_t base = 0;
-    for (uint64_t g0 = 0; g0 < groups; g0 += G4_TOP_CHUNK) {
-        const uint32_t cnt = (uint32_t)std::min<uint64_t>(G4_TOP_CHUNK, groups - g0);
-        __syncthreads();
-        for (uint32_t k = threadIdx.x; k < cnt * 16; k += G4_THREADS)
-            t16[k] = gtree[(g0 + (k >> 4)) * (2 * G4_GROUP * 16) + 16 + (k & 15u)];  // node 1 of group g0 + k/16
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (uint32_t j = 0; j < cnt; ++j) {
-                gentry[g0 + j] = state;
-                gbase[g0 + j] = base;
-                const uint32_t x = t16[j * 16 + state];
-                base += x >> 4;
-                state = x & 15u;
-            }
-        }
-    }
-    if (threadIdx.x == 0) {
-        *nwords = base;
-        if (base > cap)
-            atomicOr(status, G4_STATUS_NOSPC);
-    }
-}
-
-// Phase 2 per tile: its entry offset and word base (the group's, from a walk
-// of the group roots or from k_g4p_top, then down the group tree: the left
-// siblings on the path to the tile's leaf), the tile's tree again from the
-// bytes, a down-sweep from the entry -> every segment's entry and base; each
-// thread packs its segment's words into LDS, the block stores them coalesced.
-// WALK (groups <= G4_WALK_MAX): every block walks all group roots, so it
-// also knows the total and checks the capacity itself (block 0 reports it).
-template <bool WALK>
-__global__ __launch_bounds__(G4_THREADS) void k_g4p_emit(const uint8_t *__restrict__ vb,
-                                                         const uint4 *__restrict__ leaves,
-                                                         const uint2 *__restrict__ cls, uint64_t n, uint64_t groups,
-                                                         const uint32_t *__restrict__ gtree,
-                                                         const uint32_t *__restrict__ gentry,
-                                                         const uint64_t *__restrict__ gbase,
-                                                         int32_t *__restrict__ out, uint64_t cap,
-                                                         uint64_t *__restrict__ nwords, uint32_t *__restrict__ status)
-{
-    __shared__ G4Tile sm;
-    __shared__ uint8_t st[2 * G4_THREADS];
-    __shared__ uint16_t bs[2 * G4_THREADS];
-    __shared__ uint32_t roots[WALK ? G4_WALK_MAX * 16 : 1];
-    __shared__ uint32_t path[G4_GDEPTH][16];
-    __shared__ uint32_t e_state, e_ok;
-    __shared__ uint64_t e_base;
-    if (*status != 0)  // an out-of-domain value: write nothing
-        return;
-    const unsigned t = threadIdx.x;
-    const uint64_t tile = blockIdx.x, start = tile * G4_TILE;
-    const uint64_t g = tile / G4_GROUP;
-    const uint32_t j = (uint32_t)(tile - g * G4_GROUP);
-    const uint32_t *gt = gtree + g * (2 * G4_GROUP * 16);
-    if (t < 16 * G4_GDEPTH) {  // the left siblings of the path root -> leaf G4_GROUP + j
-        const uint32_t lvl = t >> 4;
-        path[lvl][t & 15u] = gt[((((uint32_t)G4_GROUP + j) >> (G4_GDEPTH - 1 - lvl)) ^ 1u) * 16 + (t & 15u)];
-    }
-    if (WALK)
-        for (uint32_t k = t; k < groups * 16; k += G4_THREADS)
-            roots[k] = gtree[(k >> 4) * (2 * G4_GROUP * 16) + 16 + (k & 15u)];
-    const uint64_t seg = tile * G4_THREADS + t;  // this thread's segment table and classes (phase 1)
-    {
-        uint4 *leaf = reinterpret_cast<uint4 *>(sm.node[G4_THREADS + t]);
-        leaf[0] = leaves[2 * seg];
-        leaf[1] = leaves[2 * seg + 1];
-    }
-    const uint2 cl = cls[seg];
-    const G4Cls c{cl.x, cl.y};
-    g4_load<false, true>(sm, nullptr, const_cast<uint8_t *>(vb), n, start, nullptr);  // ends with a barrier
-    if (t == 0) {
-        uint32_t state = 0;
-        uint64_t base = 0, total = 0;
-        if (WALK) {
-            for (uint32_t q = 0; q < groups; ++q) {
-                if (q == g) {
-                    e_state = state;
-                    e_base = base;
+            for (uint32_t j = 0; j < G1_LB; ++j) {
+                const uint32_t q = q0 + j * G1_THREADS + t;
+                const uint64_t g = start + 4ull * q;
+                int4 r = make_int4(0, 0, 0, 0);
+                if (q < QT + 4) {  // the tile and its 16-position halo (the next tile's head)
+                    if (ALIGNED && g + 4 <= n)
+                        r = *reinterpret_cast<const int4 *>(src + g);
+                    else if (g < n) {
+                        r.x = src[g];
+                        r.y = g + 1 < n ? src[g + 1] : 0;
+                        r.z = g + 2 < n ? src[g + 2] : 0;
+                        r.w = g + 3 < n ? src[g + 3] : 0;
+                    }
                 }
-                const uint32_t x = roots[q * 16 + state];
-                base += x >> 4;
-                state = x & 15u;
-            }
-            total = base;
-            state = e_state;
-            base = e_base;
-        } else {
-            state = gentry[g];
-            base = gbase[g];
-        }
-        for (uint32_t lvl = 0; lvl < G4_GDEPTH; ++lvl) {
-            if ((j >> (G4_GDEPTH - 1 - lvl)) & 1u) {  // the path goes right: the left sibling's words come first
-                const uint32_t x = path[lvl][state];
-                base += x >> 4;
-                state = x & 15u;
+                v[j] = r;
             }
         }
-        e_state = state;
-        e_base = base;
-        e_ok = 1;
-        if (WALK) {
-            e_ok = total <= cap;
-            if (tile == 0) {
-                *nwords = total;
-                if (!e_ok)
-                    atomicOr(status, G4_STATUS_NOSPC);
-            }
-        }
-    }
-    g4_tree_up<uint16_t, G4_THREADS>(sm.node);  // starts with a barrier (e_* visible after)
-    if (!e_ok)
-        return;
-    const uint32_t s0 = e_state;
-    const uint32_t tile_words = sm.node[1][s0] >> 4;
-    if (t == 0) {
-        st[1] = (uint8_t)s0;
-        bs[1] = 0;
-    }
-#pragma unroll 1
-    for (uint32_t lvl = 1; lvl < G4_THREADS; lvl <<= 1) {
-        __syncthreads();
-        if (t < lvl) {
-            const uint32_t i = lvl + t, s = st[i];
-            const uint32_t e = sm.node[2 * i][s];
-            st[2 * i] = (uint8_t)s;
-            bs[2 * i] = bs[i];
-            st[2 * i + 1] = (uint8_t)(e & 15u);
-            bs[2 * i + 1] = (uint16_t)(bs[i] + (e >> 4));
-        }
-    }
-    __syncthreads();
-    // the tree is done with: its 16 KB hold the tile's word list, one u16 per
-    // word = start position in the tile | mode << 14 (<= 8192 / 3 + 1 words)
-    static_assert(sizeof(sm.node) >= (G4_TILE / 3 + 2) * 2 && G4_TILE <= (1u << 14), "word list");
-    uint16_t *wl = reinterpret_cast<uint16_t *>(sm.node);
-    {  // this segment's word starts: from its entry offset while inside the segment and < n
-        uint32_t pos = st[G4_THREADS + t], jw = bs[G4_THREADS + t];
-        const uint64_t seg0 = start + G4_SEG * t;
-        const uint32_t live = seg0 >= n ? 0u : (uint32_t)std::min<uint64_t>(G4_SEG, n - seg0);
-        while (pos < live) {
-            const uint32_t mode = g4_mode(c, pos);
-            wl[jw++] = (uint16_t)((G4_SEG * t + pos) | (mode << 14));
-            pos += g4_cnt(mode);
-        }
-    }
-    __syncthreads();
-    // one word per lane: consecutive lanes pack consecutive words and store them coalesced
-    const uint64_t base = e_base;
-    const uint8_t *vbytes = reinterpret_cast<const uint8_t *>(sm.v);
-    for (uint32_t k = t; k < tile_words; k += G4_THREADS) {
-        const uint32_t s16 = wl[k], p = s16 & 0x3fffu, mode = s16 >> 14;
-        // bytes p .. p+15 of the tile (zero past n): 5 aligned dwords, byte-aligned
-        const uint32_t *d = &sm.v[p >> 2];
-        const uint32_t sh = p & 3u;
-        const uint32_t u0 = d[0], u1 = d[1], u2 = d[2], u3 = d[3], u4 = d[4];
-        const uint32_t x[4] = {__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
-                               __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
-        const uint32_t b = g4_bits(mode), top = g4_top(mode), cnt = g4_cnt(mode);
-        uint32_t code = mode << 30;
 #pragma unroll
-        for (uint32_t q = 0; q < 15; ++q)  // values past cnt belong to the next word: left out
-            if (q < cnt)
-                code |= ((x[q >> 2] >> (8 * (q & 3))) & 0xffu) << (top - q * b);
-        if (base + k < cap)
-            out[base + k] = (int32_t)code;
+        for (uint32_t j = 0; j < G1_LB; ++j) {
+            const uint32_t q = q0 + j * G1_THREADS + t;
+            if (q < QT + 4) {
+                bad |= (uint32_t)v[j].x | (uint32_t)v[j].y | (uint32_t)v[j].z | (uint32_t)v[j].w;
+                sm.v[q] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(v[j].w, v[j].z, 0x0c0c0400u),
+                                                __builtin_amdgcn_perm(v[j].y, v[j].x, 0x0c0c0400u), 0x05040100u);
+            }
+        }
     }
-    (void)vbytes;
+    return __syncthreads_or(bad > 255u);
+}
+
+// Persistent pack.  Grid: G <= one block per CU (the LDS image admits one);
+// every block runs all R rounds.  Deadlock-free without co-residency
+// guarantees only in the sense that a block waits for blocks of its own
+// launch: a block not yet resident gets a CU once another kernel's blocks
+// leave; a wait longer than G1_TIMEOUT_TICKS ends the call with status 4.
+template <bool ALIGNED>
+__global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restrict__ src, uint64_t n, uint32_t C,
+                                                        uint32_t R, int32_t *__restrict__ out, uint64_t cap,
+                                                        uint64_t *__restrict__ nwords, uint32_t *__restrict__ status,
+                                                        G1Hdr *__restrict__ hdr, uint64_t *__restrict__ gran)
+{
+    __shared__ G1Smem sm;
+    const unsigned tid = threadIdx.x;
+    const uint32_t b = blockIdx.x, G = gridDim.x;
+    const uint64_t abase = __hip_atomic_load(&hdr->abase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t carry_s = 0, bad_all = 0, nospc = 0, tmo = 0;
+    uint64_t carry_base = 0;
+    for (uint32_t r = 0; r < R; ++r) {
+        // the thread index re-made opaque each round, so the many per-thread
+        // LDS and global offsets are not hoisted out of the round loop (they
+        // would hold ~60 VGPRs across the whole body)
+        unsigned t;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
+        const unsigned lane = t & 63u, w = t >> 6;
+        const uint64_t tile_start = ((uint64_t)r * G + b) * C;
+        // 1. the tile's bytes
+        const uint32_t bad = g1_load_tile<ALIGNED>(sm, src, n, tile_start, C, t);
+        // 2. this thread's table over its 96 positions (identity past the tile)
+        const bool in_tile = G1_RANGE * t < C;
+        const uint64_t r0 = tile_start + G1_RANGE * t;
+        const uint32_t live = r0 >= n ? 0u : (uint32_t)std::min<uint64_t>(G1_RANGE, n - r0);
+        G4Cls cls[G1_BLK];
+        uint32_t h[8];
+        if (in_tile) {
+            uint32_t fn[15];
+#pragma unroll
+            for (uint32_t q = 0; q < 15; ++q)
+                fn[q] = q;
+#pragma unroll
+            for (int k = G1_BLK - 1; k >= 0; --k) {  // the blocks back to front, each one's table chained on
+                uint32_t wv[G4_SEG / 4 + 4];
+#pragma unroll
+                for (uint32_t j = 0; j < G4_SEG / 4 + 4; j += 4)
+                    *reinterpret_cast<uint4 *>(&wv[j]) =
+                        *reinterpret_cast<const uint4 *>(&sm.v[G1_RANGE / 4 * t + G4_SEG / 4 * k + j]);
+                cls[k] = g4_classes(wv);
+                uint32_t f[G4_SEG];
+                // one body for every thread: with a second, tail-free body beside it the
+                // register allocation of the whole kernel grew past 128 VGPRs
+                g4_dp<true>(cls[k], live > G4_SEG * k ? live - G4_SEG * k : 0u, fn, f);
+#pragma unroll
+                for (uint32_t q = 0; q < 15; ++q)
+                    fn[q] = f[q];
+            }
+#pragma unroll
+            for (uint32_t e = 0; e < 7; ++e)
+                h[e] = fn[2 * e] | (fn[2 * e + 1] << 16);
+            h[7] = fn[14] | (G4_DEAD << 16);
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < G1_BLK; ++k)
+                cls[k] = G4Cls{0, 0};
+#pragma unroll
+            for (uint32_t e = 0; e < 8; ++e)
+                h[e] = (2 * e) | ((2 * e + 1) << 16);
+        }
+        // 3. the wave's tree: node 64 + lane = this thread's table; even
+        // nodes (left children) kept in pl[w][node / 2 - 1], odd ones only
+        // while their level is composed (tr[w][index among the level's odd])
+        {
+            uint32_t *row = (lane & 1u) ? sm.u.tr[w][lane >> 1] : sm.pl[w][31 + (lane >> 1)];
+            reinterpret_cast<uint4 *>(row)[0] = make_uint4(h[0], h[1], h[2], h[3]);
+            reinterpret_cast<uint4 *>(row)[1] = make_uint4(h[4], h[5], h[6], h[7]);
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (uint32_t m = 32; m >= 1; m >>= 1) {  // parents [m, 2m); a task = (parent, entry pair)
+            constexpr uint32_t RMAX = 4;
+            uint32_t res[RMAX];
+#pragma unroll
+            for (uint32_t rr = 0; rr < RMAX; ++rr) {
+                const uint32_t task = lane + 64 * rr;
+                if (task < 8 * m) {
+                    const uint32_t p = m + (task >> 3), pr = task & 7u;
+                    const uint32_t xx = sm.pl[w][p - 1][pr];
+                    const uint16_t *rt = reinterpret_cast<const uint16_t *>(sm.u.tr[w][p - m]);
+                    const uint32_t x0 = xx & 0xffffu, x1 = xx >> 16;
+                    res[rr] = ((x0 & ~15u) + rt[x0 & 15u]) | (((x1 & ~15u) + rt[x1 & 15u]) << 16);
+                }
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (uint32_t rr = 0; rr < RMAX; ++rr) {
+                const uint32_t task = lane + 64 * rr;
+                if (task < 8 * m) {
+                    const uint32_t p = m + (task >> 3), pr = task & 7u;
+                    if (m == 1) {  // the wave root -> leaf 16 + w of the block's tree (u32 entries)
+                        sm.x[16 + w][2 * pr] = res[rr] & 0xffffu;
+                        sm.x[16 + w][2 * pr + 1] = res[rr] >> 16;
+                    } else if ((p & 1u) == 0) {
+                        sm.pl[w][p / 2 - 1][pr] = res[rr];
+                    } else {
+                        sm.u.tr[w][(p - 1) / 2 - m / 2][pr] = res[rr];
+                    }
+                }
+            }
+            wave_lds_sync();
+        }
+        __syncthreads();
+        // 4. the block's tree over the wave roots (wave 0) -> x[1], published
+        if (w == 0) {
+#pragma unroll
+            for (uint32_t m = 8; m >= 1; m >>= 1) {
+                uint32_t res[2];
+#pragma unroll
+                for (uint32_t rr = 0; rr < 2; ++rr) {
+                    const uint32_t task = lane + 64 * rr;
+                    if (task < 16 * m) {
+                        const uint32_t p = m + (task >> 4), e = task & 15u;
+                        const uint32_t xv = sm.x[2 * p][e];
+                        res[rr] = (xv & ~15u) + sm.x[2 * p + 1][xv & 15u];
+                    }
+                }
+                wave_lds_sync();
+#pragma unroll
+                for (uint32_t rr = 0; rr < 2; ++rr) {
+                    const uint32_t task = lane + 64 * rr;
+                    if (task < 16 * m)
+                        sm.x[m + (task >> 4)][task & 15u] = res[rr];
+                }
+                wave_lds_sync();
+            }
+            const uint32_t tag = (uint32_t)(abase + (uint64_t)G * (r + 1));
+            uint64_t *gr = gran + ((uint64_t)(r & 1u) * G1_GMAX + b) * 16;
+            if (lane < 16)
+                g1_store_granule(&gr[lane], (uint64_t)(sm.x[1][lane] | (bad << 31)) | ((uint64_t)tag << 32));
+#if GC_G4_STRICT
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                __hip_atomic_fetch_add(&hdr->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // wait for the round's G arrivals
+                const uint64_t target = abase + (uint64_t)G * (r + 1);
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                uint32_t ok = 1;
+                while (__hip_atomic_load(&hdr->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > G1_TIMEOUT_TICKS) {
+                        ok = 0;
+                        break;
+                    }
+                }
+#if GC_G4_STRICT
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+                sm.flag = ok;
+            }
+        }
+        __syncthreads();
+        if (!sm.flag)
+            tmo = 1;
+        // 5. the round's tables: thread (k, e) reads tiles 4k..4k+3 and composes them
+        uint32_t rbad = 0;
+        {
+            const uint32_t k = t >> 4, e = t & 15u;
+            const uint32_t tag = (uint32_t)(abase + (uint64_t)G * (r + 1));
+            const uint64_t *gr = gran + (uint64_t)(r & 1u) * G1_GMAX * 16;
+            uint32_t a[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t i = 4 * k + j;
+                a[j] = e;  // identity past the grid
+                if (i < G && !tmo) {
+                    uint64_t g = g1_load_granule(&gr[i * 16 + e]);
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    while ((uint32_t)(g >> 32) != tag) {  // the count says it is there; visibility may lag
+                        __builtin_amdgcn_s_sleep(1);
+                        g = g1_load_granule(&gr[i * 16 + e]);
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > G1_TIMEOUT_TICKS) {
+                            tmo = 1;
+                            break;
+                        }
+                    }
+                    rbad |= (uint32_t)g >> 31;
+                    a[j] = (uint32_t)g & 0x7fffffffu;
+                }
+                sm.u.t0[i][e] = a[j];
+            }
+            uint32_t c = a[0];
+#pragma unroll
+            for (uint32_t j = 1; j < 4; ++j) {
+                const int src_lane = (int)((lane & ~15u) | (c & 15u));
+                c = (c & ~15u) + (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane * 4, (int)a[j]);
+            }
+            sm.g4[k][e] = c;
+        }
+        rbad = __syncthreads_or(rbad);
+        tmo = __syncthreads_or(tmo);
+        if (t < 256) {
+            const uint32_t k = t >> 4, e = t & 15u;
+            uint32_t c = sm.g4[4 * k][e];
+#pragma unroll
+            for (uint32_t j = 1; j < 4; ++j)
+                c = (c & ~15u) + sm.g4[4 * k + j][c & 15u];
+            sm.g16[k][e] = c;
+        }
+        __syncthreads();
+        if (t < 64) {
+            const uint32_t k = t >> 4, e = t & 15u;
+            uint32_t c = sm.g16[4 * k][e];
+#pragma unroll
+            for (uint32_t j = 1; j < 4; ++j)
+                c = (c & ~15u) + sm.g16[4 * k + j][c & 15u];
+            sm.g64[k][e] = c;
+        }
+        __syncthreads();
+        if (t == 0) {  // the block's entry and word base; the round's exit and total
+            uint32_t s = carry_s, base = 0;
+            const uint32_t i3 = b >> 6, i2 = (b >> 4) & 3u, i1 = (b >> 2) & 3u, i0 = b & 3u;
+            for (uint32_t j = 0; j < i3; ++j)
+                base += g1_apply(sm.g64[j][s], s);
+            for (uint32_t j = 0; j < i2; ++j)
+                base += g1_apply(sm.g16[4 * i3 + j][s], s);
+            for (uint32_t j = 0; j < i1; ++j)
+                base += g1_apply(sm.g4[16 * i3 + 4 * i2 + j][s], s);
+            for (uint32_t j = 0; j < i0; ++j)
+                base += g1_apply(sm.u.t0[64 * i3 + 16 * i2 + 4 * i1 + j][s], s);
+            sm.s_b = s;
+            sm.base_b = base;
+            uint32_t se = carry_s, tw = 0;
+            for (uint32_t j = 0; j < G1_GMAX / 64; ++j)
+                tw += g1_apply(sm.g64[j][se], se);
+            sm.s_end = se;
+            sm.tw = tw;
+        }
+        __syncthreads();
+        bad_all |= rbad;
+        const uint64_t round_end = carry_base + sm.tw;
+        if (round_end > cap)
+            nospc = 1;
+        // 6. this thread's entry and word base: down the block's tree, then the wave's
+        if (!bad_all && !nospc && !tmo && in_tile) {
+            uint32_t s = sm.s_b;
+            uint64_t base = carry_base + sm.base_b;
+            uint32_t node = 1;
+#pragma unroll
+            for (int d = 3; d >= 0; --d) {
+                const uint32_t bit = (w >> d) & 1u;
+                if (bit)
+                    base += g1_apply(sm.x[2 * node][s], s);
+                node = 2 * node + bit;
+            }
+            node = 1;
+#pragma unroll
+            for (int d = 5; d >= 0; --d) {
+                const uint32_t bit = (lane >> d) & 1u;
+                if (bit)
+                    base += g1_apply(reinterpret_cast<const uint16_t *>(sm.pl[w][node - 1])[s], s);
+                node = 2 * node + bit;
+            }
+            // 7. the words: modes from the class bits, values from the LDS bytes
+            uint32_t pos = s;  // G4_DEAD (15) when the chain ended before this range
+#pragma unroll
+            for (uint32_t k = 0; k < G1_BLK; ++k) {  // block by block: the class bits indexed statically
+                const uint32_t end = std::min<uint32_t>(live, G4_SEG * (k + 1));
+                while (pos < end) {
+                    const uint32_t mode = g4_mode(cls[k], pos & 31u);
+                    const uint32_t a = G1_RANGE * t + pos;
+                    const uint32_t *d = &sm.v[a >> 2];
+                    const uint32_t sh = a & 3u;
+                    const uint32_t u0 = d[0], u1 = d[1], u2 = d[2], u3 = d[3], u4 = d[4];
+                    const uint32_t x[4] = {__builtin_amdgcn_alignbyte(u1, u0, sh),
+                                           __builtin_amdgcn_alignbyte(u2, u1, sh),
+                                           __builtin_amdgcn_alignbyte(u3, u2, sh),
+                                           __builtin_amdgcn_alignbyte(u4, u3, sh)};
+                    const uint32_t bb = g4_bits(mode), top = g4_top(mode), cnt = g4_cnt(mode);
+                    uint32_t code = mode << 30;
+#pragma unroll
+                    for (uint32_t q = 0; q < 15; ++q)  // values past cnt belong to the next word: left out
+                        if (q < cnt)
+                            code |= ((x[q >> 2] >> (8 * (q & 3))) & 0xffu) << (top - q * bb);
+                    out[base++] = (int32_t)code;
+                    pos += cnt;
+                }
+            }
+        }
+        carry_s = sm.s_end;
+        carry_base = round_end;
+        __syncthreads();  // the next round rewrites the LDS image and the trees
+    }
+    if (tid == 0) {
+        if (tmo)
+            __hip_atomic_fetch_or(&hdr->tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t old = __hip_atomic_fetch_add(&hdr->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == G - 1) {  // the last block: results, then re-arm the header for the next call
+            const uint32_t any_tmo = __hip_atomic_load(&hdr->tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *nwords = carry_base;
+            *status = (bad_all ? G4_STATUS_RANGE : 0u) | (nospc ? G4_STATUS_NOSPC : 0u) |
+                      (any_tmo ? G4_STATUS_TIMEOUT : 0u);
+            const uint64_t arrived = __hip_atomic_load(&hdr->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&hdr->abase, any_tmo ? arrived : abase + (uint64_t)G * R, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&hdr->tmo, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&hdr->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// n == 0: the result pair only
+__global__ void k_g4p_empty(uint64_t *nwords, uint32_t *status)
+{
+    *nwords = 0;
+    *status = 0;
 }
 
 // ---- unpack ---------------------------------------------------------------
@@ -573,22 +604,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *total)
     __syncthreads();
     *total = tot;
     return off + inc - v;
-}
-
-// the result pair, the per-group tickets and the ready bits of k_g4p_tile's
-// table rows (the workspace needs no initialisation by the caller)
-__global__ void k_g4_init(uint64_t *count, uint32_t *status, uint32_t *__restrict__ gcount, uint64_t groups,
-                          uint32_t *__restrict__ agg, uint64_t agg_words)
-{
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) {
-        *count = 0;
-        *status = 0;
-    }
-    for (uint64_t k = i; k < groups; k += (uint64_t)gridDim.x * blockDim.x)
-        gcount[k] = 0;
-    for (uint64_t k = i; k < agg_words; k += (uint64_t)gridDim.x * blockDim.x)
-        agg[k] = 0;
 }
 
 // this thread's 4 words (0 past nw: counted as 15 values of mode 0, so only
@@ -766,40 +781,13 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit_nb(const int32_t *__res
         out[base + k] = (int32_t)obuf[k];
 }
 
-// workspace layout (bytes, 256-aligned pieces)
+// unpack workspace layout (bytes, 256-aligned pieces)
 struct G4Ws {
-    uint32_t *agg, *gtree, *gcount, *gentry, *bsum;
-    uint64_t *gbase, *bbase;
-    uint8_t *vb;
-    uint4 *leaves;  // per segment: its table, 16 x u16
-    uint2 *cls;     // per segment: the mode classes (lo, hi)
+    uint32_t *bsum;
+    uint64_t *bbase;
 };
 
 static inline uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
-
-static uint64_t g4_ws(uint64_t n, char *base, G4Ws *w)
-{
-    const uint64_t tiles = (n + G4_TILE - 1) / G4_TILE;
-    const uint64_t groups = (tiles + G4_GROUP - 1) / G4_GROUP;
-    uint64_t off = 0;
-    auto take = [&](uint64_t bytes) {
-        char *p = base ? base + off : nullptr;
-        off += al256(bytes);
-        return p;
-    };
-    G4Ws t{};
-    t.agg = (uint32_t *)take(tiles * 64);
-    t.gtree = (uint32_t *)take(groups * (2 * G4_GROUP * 16 * 4));  // 16 KB per group
-    t.gcount = (uint32_t *)take(groups * 4);
-    t.gentry = (uint32_t *)take(groups * 4);
-    t.gbase = (uint64_t *)take(groups * 8);
-    t.vb = (uint8_t *)take(tiles * G4_TILE);  // whole tiles: the dword stores past n stay inside
-    t.leaves = (uint4 *)take(tiles * G4_THREADS * 32);
-    t.cls = (uint2 *)take(tiles * G4_THREADS * 8);
-    if (w)
-        *w = t;
-    return off;
-}
 
 static uint64_t g4u_ws(uint64_t nw, char *base, G4Ws *w)
 {
@@ -818,13 +806,54 @@ static uint64_t g4u_ws(uint64_t nw, char *base, G4Ws *w)
     return off;
 }
 
+// compute units of the stream's device (cached per device): the persistent
+// pack's grid is at most one block per CU
+static uint32_t g1_cus(hipStream_t st)
+{
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess)
+        dev = 0;
+    if (dev < 0 || dev >= 64)
+        dev = 0;
+    int c = cache[dev].load(std::memory_order_relaxed);
+    if (c <= 0) {
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 1;
+        cache[dev].store(c, std::memory_order_relaxed);
+    }
+    return (uint32_t)c;
+}
+
+// the pack's geometry for n positions on `cus` CUs: G blocks, R rounds, C
+// positions per tile (a multiple of 96, <= G1_TILE_MAX), G * R * C >= n
+struct G1Geom {
+    uint32_t G, R, C;
+};
+
+static G1Geom g1_geom(uint64_t n, uint32_t cus)
+{
+    G1Geom g{};
+    const uint64_t gmax = std::min<uint64_t>(std::min<uint32_t>(cus, G1_GMAX), (n + G1_MIN_TILE - 1) / G1_MIN_TILE);
+    g.G = (uint32_t)std::max<uint64_t>(1, gmax);
+    const uint64_t per_round = (uint64_t)g.G * G1_TILE_MAX;
+    g.R = (uint32_t)std::max<uint64_t>(1, (n + per_round - 1) / per_round);
+    const uint64_t per_tile = (n + (uint64_t)g.G * g.R - 1) / ((uint64_t)g.G * g.R);
+    g.C = (uint32_t)std::max<uint64_t>(G1_RANGE, (per_tile + G1_RANGE - 1) / G1_RANGE * G1_RANGE);
+    return g;
+}
+
 }  // namespace gc
 
 using namespace gc;
 
 extern "C" {
 
-size_t gc_greedy4_workspace_size(uint64_t n) { return (size_t)std::max<uint64_t>(g4_ws(n, nullptr, nullptr), 256); }
+size_t gc_greedy4_workspace_size(uint64_t n)
+{
+    (void)n;
+    return (size_t)G1_WS_BYTES;
+}
 
 size_t gc_greedy4_unpack_workspace_size(uint64_t nwords)
 {
@@ -839,29 +868,19 @@ int gc_greedy4_pack_device(const int32_t *src, uint64_t n, int32_t *out, uint64_
     GC_REQUIRE(n < (1ull << 40), "gc_greedy4_pack_device: n too large");
     GC_REQUIRE(aligned16(workspace), "gc_greedy4_pack_device: workspace must be 16-byte aligned");
     hipStream_t st = as_stream(stream);
-    G4Ws w;
-    g4_ws(n, reinterpret_cast<char *>(workspace), &w);
-    const uint64_t tiles = (n + G4_TILE - 1) / G4_TILE;
-    const uint64_t groups = (tiles + G4_GROUP - 1) / G4_GROUP;
-    hipLaunchKernelGGL(k_g4_init, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, tiles / 16))),
-                       dim3(256), 0, st, nwords, status, w.gcount, groups, w.agg, tiles * 16);
-    if (n == 0)
+    if (n == 0) {
+        hipLaunchKernelGGL(k_g4p_empty, dim3(1), dim3(1), 0, st, nwords, status);
         return launch_status("gc_greedy4_pack_device");
-    if (aligned16(src))
-        hipLaunchKernelGGL(k_g4p_tile<true>, dim3((unsigned)tiles), dim3(G4_THREADS), 0, st, src, n, tiles, w.vb,
-                           w.leaves, w.cls, w.agg, w.gtree, w.gcount, status);
-    else
-        hipLaunchKernelGGL(k_g4p_tile<false>, dim3((unsigned)tiles), dim3(G4_THREADS), 0, st, src, n, tiles, w.vb,
-                           w.leaves, w.cls, w.agg, w.gtree, w.gcount, status);
-    if (groups <= G4_WALK_MAX) {
-        hipLaunchKernelGGL(k_g4p_emit<true>, dim3((unsigned)tiles), dim3(G4_THREADS), 0, st, w.vb, w.leaves, w.cls, n,
-                           groups, w.gtree, w.gentry, w.gbase, out, cap, nwords, status);
-    } else {
-        hipLaunchKernelGGL(k_g4p_top, dim3(1), dim3(G4_THREADS), 0, st, w.gtree, groups, w.gentry, w.gbase, nwords,
-                           cap, status);
-        hipLaunchKernelGGL(k_g4p_emit<false>, dim3((unsigned)tiles), dim3(G4_THREADS), 0, st, w.vb, w.leaves, w.cls,
-                           n, groups, w.gtree, w.gentry, w.gbase, out, cap, nwords, status);
     }
+    const G1Geom g = g1_geom(n, g1_cus(st));
+    G1Hdr *hdr = reinterpret_cast<G1Hdr *>(workspace);
+    uint64_t *gran = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(workspace) + sizeof(G1Hdr));
+    if (aligned16(src))
+        hipLaunchKernelGGL(k_g4p_one<true>, dim3(g.G), dim3(G1_THREADS), 0, st, src, n, g.C, g.R, out, cap, nwords,
+                           status, hdr, gran);
+    else
+        hipLaunchKernelGGL(k_g4p_one<false>, dim3(g.G), dim3(G1_THREADS), 0, st, src, n, g.C, g.R, out, cap, nwords,
+                           status, hdr, gran);
     return launch_status("gc_greedy4_pack_device");
 }
 
@@ -881,8 +900,7 @@ int gc_greedy4_unpack_device(const int32_t *words, uint64_t nwords, int32_t *out
                            cap, count, status);
         return launch_status("gc_greedy4_unpack_device");
     }
-    hipLaunchKernelGGL(k_g4_init, dim3(1), dim3(256), 0, st, count, status, nullptr, (uint64_t)0, nullptr,
-                       (uint64_t)0);
+    hipLaunchKernelGGL(k_g4p_empty, dim3(1), dim3(1), 0, st, count, status);
     if (nwords == 0)
         return launch_status("gc_greedy4_unpack_device");
     hipLaunchKernelGGL(k_g4u_sums, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bsum);

@@ -1225,13 +1225,19 @@ def _g4_result(res: torch.Tensor, what: str) -> int:
         raise _lib.GCodecError(_lib.GC_ERANGE, f"{what}: a value outside [0, 255] (the greedy format's domain)")
     if status & 2:
         raise _lib.GCodecError(_lib.GC_ENOSPC, f"{what}: output capacity too small")
+    if status & 4:
+        raise _lib.GCodecError(_lib.GC_EHIP, f"{what}: a block of the persistent pack waited too long "
+                                             "(the workspace must be zeroed again before its next use)")
     return count
 
 
 class Greedy4Device:
     """Device greedy-4 packing of buckets of one size with the buffers
     allocated once: pack() / unpack() only enqueue (no allocation, no host
-    sync); result() reads the (count, status) pair back (one 16-byte D2H)."""
+    sync); result() / unpack_result() read the (count, status) pair back (one
+    16-byte D2H each).  Pack and unpack keep separate result pairs and
+    workspaces, so a pack's word count survives an unpack enqueued before it
+    is read.  The pack workspace starts zeroed; every pack leaves it so."""
 
     def __init__(self, n: int, device, unpack_words: int | None = None):
         lib = _lib.load()
@@ -1242,9 +1248,10 @@ class Greedy4Device:
         nw = self.cap if unpack_words is None else int(unpack_words)
         self.ucap = max(15 * nw, 1)
         self.values = torch.empty(self.ucap, dtype=torch.int32, device=self.device)
-        ws = max(int(lib.gc_greedy4_workspace_size(self.n)), int(lib.gc_greedy4_unpack_workspace_size(nw)))
-        self.ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
+        self.ws = torch.zeros(int(lib.gc_greedy4_workspace_size(self.n)), dtype=torch.uint8, device=self.device)
+        self.uws = torch.empty(int(lib.gc_greedy4_unpack_workspace_size(nw)), dtype=torch.uint8, device=self.device)
         self.res = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self.ures = torch.zeros(2, dtype=torch.int64, device=self.device)
 
     def pack(self, a: torch.Tensor):
         """a: int32 [n] on the device -> self.words (count via result())."""
@@ -1254,14 +1261,19 @@ class Greedy4Device:
                                                  _stream(self.device)), "gc_greedy4_pack_device")
 
     def unpack(self, w: torch.Tensor):
-        """w: int32 words on the device -> self.values (count via result())."""
+        """w: int32 words on the device -> self.values (count via unpack_result())."""
         assert w.dtype == torch.int32 and w.is_contiguous() and 15 * w.numel() <= self.ucap
-        check(_lib.load().gc_greedy4_unpack_device(_p(w), w.numel(), _p(self.values), self.ucap, _p(self.res),
-                                                   C.c_void_p(self.res.data_ptr() + 8), _p(self.ws),
+        check(_lib.load().gc_greedy4_unpack_device(_p(w), w.numel(), _p(self.values), self.ucap, _p(self.ures),
+                                                   C.c_void_p(self.ures.data_ptr() + 8), _p(self.uws),
                                                    _stream(self.device)), "gc_greedy4_unpack_device")
 
-    def result(self, what: str = "greedy4") -> int:
+    def result(self, what: str = "greedy4_pack") -> int:
+        """The last pack's word count."""
         return _g4_result(self.res, what)
+
+    def unpack_result(self, what: str = "greedy4_unpack") -> int:
+        """The last unpack's value count."""
+        return _g4_result(self.ures, what)
 
 
 def greedy4_pack(src: torch.Tensor) -> torch.Tensor:

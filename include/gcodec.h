@@ -211,10 +211,16 @@ int gc_randk_encode_w1_segments(const gc_segments *segs, const int64_t *idx, uin
  * a parallel scan over 16-entry segment tables.
  * Results are asynchronous: *nwords / *count (device uint64) receive the
  * number of words / values, *status (device uint32) 0 or a bit set: 1 = a
- * value outside [0, 255] (nothing written), 2 = more than cap outputs
- * (nothing written).  workspace: gc_greedy4[_unpack]_workspace_size bytes,
- * device, no initialisation needed.  unpack emits whole words (the caller
- * truncates, as compressors.py:371 does). */
+ * value outside [0, 255], 2 = more than cap outputs, 4 = (pack) a block of the
+ * persistent launch gave up waiting for the others (about a second).  With 1
+ * or 2 set nothing is written when the pack runs in one round (n up to about
+ * 25 M on 256 CUs); a longer pack has written the words of the rounds before
+ * the one that found it.  The unpack writes nothing on 2.
+ * workspace: gc_greedy4[_unpack]_workspace_size bytes, device.  The PACK
+ * workspace must be zero-filled before its first use and is left that way by
+ * every call (after status 4: zero it again); the unpack workspace needs no
+ * initialisation.  One pack at a time per pack workspace.  unpack emits whole
+ * words (the caller truncates, as compressors.py:371 does). */
 size_t gc_greedy4_workspace_size(uint64_t n);
 int gc_greedy4_pack_device(const int32_t *src, uint64_t n, int32_t *out, uint64_t cap, uint64_t *nwords,
                            uint32_t *status, void *workspace, gc_stream_t stream);

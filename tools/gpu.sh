@@ -14,6 +14,7 @@
 #   scale     plain `bench.py --gpus 2` and `--gpus 4` over gloo (the SCALE form; ranks share cuda:0)
 #   pmc       FETCH_SIZE / WRITE_SIZE passes over the headline kernels
 #   kprof     tools/prof_kernels.py: trace, FETCH, WRITE, SQ, LDS passes
+#   g4prof    the same five passes over tools/prof_packers.py (the drop-in packers)
 #   cmd       the command after "--" (e.g. a lab sweep), with a 600 s limit
 #
 # Every GPU step has its own time limit.  A timeout, signal, abort or fault
@@ -92,6 +93,18 @@ if has kprof; then
   prof k_sq 240 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
     SQ_ACTIVE_INST_SCA SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d "$D/sq" -o run -- python3 $K || exit $?
   prof k_lds 240 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES \
+    SQ_WAVES --output-format csv -d "$D/lds" -o run -- python3 $K || exit $?
+fi
+if has g4prof; then
+  K="$ROOT/tools/prof_packers.py"
+  D="$OUT/prof_${TAG}_g4"
+  export PACK_SRC=xi
+  prof g4_trace 240 --kernel-trace --stats --output-format csv -d "$D/trace" -o run -- python3 $K || exit $?
+  prof g4_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$D/fetch" -o run -- python3 $K || exit $?
+  prof g4_write 240 --pmc WRITE_SIZE --output-format csv -d "$D/write" -o run -- python3 $K || exit $?
+  prof g4_sq 240 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
+    SQ_ACTIVE_INST_SCA SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d "$D/sq" -o run -- python3 $K || exit $?
+  prof g4_lds 240 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES \
     SQ_WAVES --output-format csv -d "$D/lds" -o run -- python3 $K || exit $?
 fi
 if has cmd && [ ${#EXTRA[@]} -gt 0 ]; then

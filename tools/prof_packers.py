@@ -15,6 +15,7 @@ import gcodec  # noqa: E402
 from gcodec import codec  # noqa: E402
 
 REPS = int(os.environ.get("REPS", "20"))
+SRCS = os.environ.get("PACK_SRC", "both")  # xi | sign | both
 dev = torch.device("cuda", 0)
 n = 23_520_842
 g = torch.Generator(device=dev).manual_seed(21)
@@ -28,9 +29,10 @@ t0 = time.perf_counter()
 while time.perf_counter() - t0 < 0.3:  # clock settle
     pk.pack(xi)
     torch.cuda.synchronize()
-for src in (xi, sg):
+for src in {"xi": (xi,), "sign": (sg,)}.get(SRCS, (xi, sg)):
     pk.pack(src)
     w = pk.words[:pk.result()].clone()
+    print("words", w.numel())
     for _ in range(REPS):
         pk.pack(src)
     for _ in range(REPS):
