@@ -23,16 +23,17 @@
 //   3. per wave a tree of its 64 tables in LDS (u16 entries, 16 lanes per
 //      node pair; only LEFT children are kept — the walk down needs nothing
 //      else), then a 16-leaf tree of the wave roots -> the tile's table;
-//   4. the table goes out as 16 {entry, tag} granules (8-byte sc1 stores),
-//      one arrival add per block; every block waits for the round's G
-//      arrivals, reads all G tables (sc1) and composes them (bpermute, then a
-//      4-ary tree in LDS) -> its entry state and word base, the round's exit
-//      state and total, and whether any tile held a value outside [0, 255];
+//   4. the table goes out as 16 {entry, tag} granules (8-byte sc1 stores);
+//      every block re-reads all G tiles' granules (sc1) until the tags match
+//      and composes them (a 4-ary tree in LDS) -> its entry state and word
+//      base, the round's exit state and total, and whether any tile held a
+//      value outside [0, 255];
 //   5. walking down the trees gives every thread its entry and word base;
-//      it packs its words from the LDS bytes straight to `out`.
+//      the threads list their word starts, then consecutive lanes pack
+//      consecutive words from the LDS bytes (coalesced stores).
 // HBM: src read once (4n), the words written once — the algorithmic bytes.
-// The workspace (header + granules, 64 KB) must be zero before its first use;
-// every call leaves it so (the last block re-arms it).
+// The workspace (header + granules, 64 KB) is zeroed once before its first
+// use; tags are unique per launch and round, so nothing is re-armed.
 //
 // Unpack: per-word element counts -> block sums -> decode into LDS ->
 // coalesced stores.
@@ -44,6 +45,9 @@
 
 #ifndef GC_G4_STRICT  // 1: the release/acquire form of the table hand-off (see g1_store_granule)
 #define GC_G4_STRICT 0
+#endif
+#ifndef GC_G4_STAMPS  // lab builds: per-block phase timestamps of round 0 behind the workspace's granules
+#define GC_G4_STAMPS 0
 #endif
 
 namespace gc {
@@ -142,32 +146,44 @@ constexpr uint32_t G1_MIN_TILE = 16384;                   // small buckets: fewe
 constexpr uint64_t G1_TIMEOUT_TICKS = 1ull << 27;         // s_memrealtime (100 MHz): ~1.3 s, then status 4
 static_assert(G1_TILE_MAX / 4 <= 2 * G1_LB * G1_THREADS, "two load batches cover a tile");
 
-// workspace: the header's words on lines of their own, then the granules
-// (two round parities x G1_GMAX tiles x 16 entries x {entry, tag})
+// workspace: the header on a line of its own, then the granules (two round
+// parities x G1_GMAX tiles x 16 entries x {entry, tag}), then (lab builds)
+// the phase stamps
 struct G1Hdr {
-    uint64_t arrive;        // +1 per block per round, never reset
-    uint64_t pad0[15];
-    uint64_t abase;         // arrive at the start of the next launch
-    uint32_t done;          // blocks finished (the last one re-arms)
-    uint32_t tmo;           // a block gave up waiting
-    uint64_t pad1[14];
+    uint64_t seq;           // tags used so far: round r of a launch tags seq + r + 1
+    uint64_t pad[31];
 };
 static_assert(sizeof(G1Hdr) == 256, "header size");
-constexpr uint64_t G1_WS_BYTES = sizeof(G1Hdr) + 2ull * G1_GMAX * 16 * 8;
+constexpr uint32_t G1_NSTAMP = 8;
+constexpr uint64_t G1_WS_BYTES = sizeof(G1Hdr) + 2ull * G1_GMAX * 16 * 8 + (GC_G4_STAMPS ? G1_GMAX * G1_NSTAMP * 8 : 0);
+
+// lab builds only: s_memrealtime (100 MHz) at a block's phase boundaries
+#define G1_STAMP(i)                                                                                      \
+    do {                                                                                                 \
+        if (GC_G4_STAMPS && r == 0 && t == 0)                                                            \
+            gran[2ull * G1_GMAX * 16 + (uint64_t)b * G1_NSTAMP + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 
 struct G1Smem {
-    alignas(16) uint32_t v[G1_TILE_MAX / 4 + 4];            // the tile's values as bytes + 16-byte halo (96 KB)
-    uint32_t pl[G1_WAVES][63][8];               // per wave: the left children of its tree (u16 x 16 a row)
+    alignas(16) uint32_t v[G1_TILE_MAX / 4 + 4];  // the tile's values as bytes + 16-byte halo (96 KB)
     union {
-        uint32_t tr[G1_WAVES][32][8];           // per wave: right children of the level in flight
-        uint32_t t0[G1_GMAX][16];               // the round's tile tables
-    } u;
-    uint32_t g4[G1_GMAX / 4][16];               // compositions of 4 / 16 / 64 tiles
-    uint32_t g16[G1_GMAX / 16][16];
-    uint32_t g64[G1_GMAX / 64][16];
-    uint32_t x[32][16];                         // the tree of the 16 wave roots (nodes 1..31)
-    uint64_t base_b;                            // the block's word base within the round
-    uint32_t s_b, s_end, tw, flag;
+        struct {
+            uint32_t pl[G1_WAVES][63][8];         // per wave: the left children of its tree (u16 x 16 a row)
+            union {
+                uint32_t tr[G1_WAVES][32][8];     // per wave: right children of the level in flight
+                uint32_t t0[G1_GMAX][16];         // the round's tile tables
+            } u;
+            uint32_t g4[G1_GMAX / 4][16];         // compositions of 4 / 16 / 64 tiles
+            uint32_t g16[G1_GMAX / 16][16];
+            uint32_t g64[G1_GMAX / 64][16];
+            uint32_t x[32][16];                   // the tree of the 16 wave roots (nodes 1..31)
+        } k;
+        uint16_t wl[G1_WAVES / 2][64 * G1_RANGE / 3 + 4];  // emission: half the waves' word lists at a time
+    };
+    uint64_t wbase[G1_WAVES];                     // each wave's first word (absolute)
+    uint32_t wcnt[G1_WAVES];                      // each wave's words
+    uint64_t base_b;                              // the block's word base within the round
+    uint32_t s_b, s_end, tw;
 };
 
 // the waves of a workgroup run one LDS tree each: order a wave's LDS stores
@@ -185,16 +201,18 @@ __device__ __forceinline__ uint32_t g1_apply(uint32_t x, uint32_t &s)  // table 
     return x >> 4;
 }
 
-// the hand-off of the round's tile tables (MI355X_MICROARCH.md, row 1 of the
-// sc1 table): 8-byte sc1 granule stores, drained, then one agent-scope add per
-// block; readers poll the count with sc1 loads and read the granules with sc1
-// loads.  GC_G4_STRICT: plain stores + an agent release fence before the add,
-// an agent acquire fence after the poll, plain loads — the memory model's own
-// form (slower; kept so the hardware-observed form can be switched off).
+// The hand-off of the round's tile tables: MI355X_MICROARCH.md's data-tagged
+// granules (cdna_hip_programming.md Guideline 16, R2): every table entry is
+// one 8-byte {entry, tag} granule written by ONE sc1 store; readers re-read
+// with sc1 loads until every tag matches.  No flag, no counter, no fence.
+// Tags are unique per (launch, round) (G1Hdr::seq), so nothing is re-armed.
+// GC_G4_STRICT: the memory model's own message passing instead — the entry
+// and tag as a release store of the whole granule, acquire loads — for builds
+// that must not rely on the observed untorn sc1 granule.
 __device__ __forceinline__ void g1_store_granule(uint64_t *p, uint64_t v)
 {
 #if GC_G4_STRICT
-    *p = v;
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 #else
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
@@ -203,7 +221,7 @@ __device__ __forceinline__ void g1_store_granule(uint64_t *p, uint64_t v)
 __device__ __forceinline__ uint64_t g1_load_granule(const uint64_t *p)
 {
 #if GC_G4_STRICT
-    return *(const volatile uint64_t *)p;
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
 #else
     return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
@@ -258,11 +276,27 @@ __device__ __forceinline__ uint32_t g1_load_tile(G1Smem &sm, const int32_t *__re
     return __syncthreads_or(bad > 255u);
 }
 
+// pack one word of mode `mode` from the bytes at tile offset a (zero past n)
+__device__ __forceinline__ uint32_t g1_word(const G1Smem &sm, uint32_t a, uint32_t mode)
+{
+    const uint32_t *d = &sm.v[a >> 2];
+    const uint32_t sh = a & 3u;
+    const uint32_t u0 = d[0], u1 = d[1], u2 = d[2], u3 = d[3], u4 = d[4];
+    const uint32_t x[4] = {__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
+                           __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
+    const uint32_t bb = g4_bits(mode), top = g4_top(mode), cnt = g4_cnt(mode);
+    uint32_t code = mode << 30;
+#pragma unroll
+    for (uint32_t q = 0; q < 15; ++q)  // values past cnt belong to the next word: left out
+        if (q < cnt)
+            code |= ((x[q >> 2] >> (8 * (q & 3))) & 0xffu) << (top - q * bb);
+    return code;
+}
+
 // Persistent pack.  Grid: G <= one block per CU (the LDS image admits one);
-// every block runs all R rounds.  Deadlock-free without co-residency
-// guarantees only in the sense that a block waits for blocks of its own
-// launch: a block not yet resident gets a CU once another kernel's blocks
-// leave; a wait longer than G1_TIMEOUT_TICKS ends the call with status 4.
+// every block runs all R rounds.  A block waits only for blocks of its own
+// launch; one not yet resident gets a CU once another kernel's blocks leave.
+// A wait longer than G1_TIMEOUT_TICKS ends the call with status 4.
 template <bool ALIGNED>
 __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restrict__ src, uint64_t n, uint32_t C,
                                                         uint32_t R, int32_t *__restrict__ out, uint64_t cap,
@@ -272,7 +306,9 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
     __shared__ G1Smem sm;
     const unsigned tid = threadIdx.x;
     const uint32_t b = blockIdx.x, G = gridDim.x;
-    const uint64_t abase = __hip_atomic_load(&hdr->abase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every block reads seq before its round-0 granules exist; block 0 moves
+    // it on only after it has read every block's round-0 granules
+    const uint64_t seq = __hip_atomic_load(&hdr->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t carry_s = 0, bad_all = 0, nospc = 0, tmo = 0;
     uint64_t carry_base = 0;
     for (uint32_t r = 0; r < R; ++r) {
@@ -283,8 +319,11 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
         const unsigned lane = t & 63u, w = t >> 6;
         const uint64_t tile_start = ((uint64_t)r * G + b) * C;
+        const uint32_t tag = (uint32_t)(seq + r + 1);
+        G1_STAMP(0);
         // 1. the tile's bytes
         const uint32_t bad = g1_load_tile<ALIGNED>(sm, src, n, tile_start, C, t);
+        G1_STAMP(1);
         // 2. this thread's table over its 96 positions (identity past the tile)
         const bool in_tile = G1_RANGE * t < C;
         const uint64_t r0 = tile_start + G1_RANGE * t;
@@ -305,9 +344,7 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
                         *reinterpret_cast<const uint4 *>(&sm.v[G1_RANGE / 4 * t + G4_SEG / 4 * k + j]);
                 cls[k] = g4_classes(wv);
                 uint32_t f[G4_SEG];
-                // one body for every thread: with a second, tail-free body beside it the
-                // register allocation of the whole kernel grew past 128 VGPRs
-                g4_dp<true>(cls[k], live > G4_SEG * k ? live - G4_SEG * k : 0u, fn, f);
+                g4_dp<false>(cls[k], G4_SEG, fn, f);  // n is handled below, for the one thread that holds it
 #pragma unroll
                 for (uint32_t q = 0; q < 15; ++q)
                     fn[q] = f[q];
@@ -324,11 +361,53 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
             for (uint32_t e = 0; e < 8; ++e)
                 h[e] = (2 * e) | ((2 * e + 1) << 16);
         }
+        // the thread whose range holds position n: its chains end there, so
+        // every entry is DEAD with the words that start before n.  Entry e is
+        // walked by lane e of its wave (the class bits read from its lane);
+        // ranges past it keep their tables, which a DEAD state passes through.
+        if (n >= tile_start && n < tile_start + C) {  // block-uniform: the tile that holds n
+            const uint32_t ts = (uint32_t)((n - tile_start) / G1_RANGE), nlive = (uint32_t)(n - tile_start) - G1_RANGE * ts;
+            if (w == (ts >> 6)) {  // wave-uniform
+                const int sl = (int)(ts & 63u);
+                G4Cls sc[G1_BLK];
+#pragma unroll
+                for (uint32_t k = 0; k < G1_BLK; ++k)
+                    sc[k] = G4Cls{(uint32_t)__builtin_amdgcn_readlane((int)cls[k].lo, sl),
+                                  (uint32_t)__builtin_amdgcn_readlane((int)cls[k].hi, sl)};
+                uint32_t pos = lane, words = 0;
+                if (lane < 15) {
+                    while (pos < nlive) {
+                        const uint32_t k = pos >> 5;  // masks, not a select (that became a scratch array)
+                        const uint32_t m0 = 0u - (k == 0), m1 = 0u - (k == 1), m2 = 0u - (k == 2);
+                        const G4Cls c{(sc[0].lo & m0) | (sc[1].lo & m1) | (sc[2].lo & m2),
+                                      (sc[0].hi & m0) | (sc[1].hi & m1) | (sc[2].hi & m2)};
+                        pos += g4_cnt(g4_mode(c, pos & 31u));
+                        ++words;
+                    }
+                }
+                const uint32_t ent = G4_DEAD | (words << 4);
+                uint32_t hs[8];
+#pragma unroll
+                for (uint32_t e = 0; e < 7; ++e)
+                    hs[e] = (uint32_t)__builtin_amdgcn_readlane((int)ent, 2 * e) |
+                            ((uint32_t)__builtin_amdgcn_readlane((int)ent, 2 * e + 1) << 16);
+                hs[7] = (uint32_t)__builtin_amdgcn_readlane((int)ent, 14) | (G4_DEAD << 16);
+                if (lane == (unsigned)sl) {
+#pragma unroll
+                    for (uint32_t e = 0; e < 8; ++e)
+                        h[e] = hs[e];
+                }
+            }
+        }
+#if GC_G4_STAMPS
+        __syncthreads();
+        G1_STAMP(2);
+#endif
         // 3. the wave's tree: node 64 + lane = this thread's table; even
         // nodes (left children) kept in pl[w][node / 2 - 1], odd ones only
         // while their level is composed (tr[w][index among the level's odd])
         {
-            uint32_t *row = (lane & 1u) ? sm.u.tr[w][lane >> 1] : sm.pl[w][31 + (lane >> 1)];
+            uint32_t *row = (lane & 1u) ? sm.k.u.tr[w][lane >> 1] : sm.k.pl[w][31 + (lane >> 1)];
             reinterpret_cast<uint4 *>(row)[0] = make_uint4(h[0], h[1], h[2], h[3]);
             reinterpret_cast<uint4 *>(row)[1] = make_uint4(h[4], h[5], h[6], h[7]);
         }
@@ -342,8 +421,8 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
                 const uint32_t task = lane + 64 * rr;
                 if (task < 8 * m) {
                     const uint32_t p = m + (task >> 3), pr = task & 7u;
-                    const uint32_t xx = sm.pl[w][p - 1][pr];
-                    const uint16_t *rt = reinterpret_cast<const uint16_t *>(sm.u.tr[w][p - m]);
+                    const uint32_t xx = sm.k.pl[w][p - 1][pr];
+                    const uint16_t *rt = reinterpret_cast<const uint16_t *>(sm.k.u.tr[w][p - m]);
                     const uint32_t x0 = xx & 0xffffu, x1 = xx >> 16;
                     res[rr] = ((x0 & ~15u) + rt[x0 & 15u]) | (((x1 & ~15u) + rt[x1 & 15u]) << 16);
                 }
@@ -355,12 +434,12 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
                 if (task < 8 * m) {
                     const uint32_t p = m + (task >> 3), pr = task & 7u;
                     if (m == 1) {  // the wave root -> leaf 16 + w of the block's tree (u32 entries)
-                        sm.x[16 + w][2 * pr] = res[rr] & 0xffffu;
-                        sm.x[16 + w][2 * pr + 1] = res[rr] >> 16;
+                        sm.k.x[16 + w][2 * pr] = res[rr] & 0xffffu;
+                        sm.k.x[16 + w][2 * pr + 1] = res[rr] >> 16;
                     } else if ((p & 1u) == 0) {
-                        sm.pl[w][p / 2 - 1][pr] = res[rr];
+                        sm.k.pl[w][p / 2 - 1][pr] = res[rr];
                     } else {
-                        sm.u.tr[w][(p - 1) / 2 - m / 2][pr] = res[rr];
+                        sm.k.u.tr[w][(p - 1) / 2 - m / 2][pr] = res[rr];
                     }
                 }
             }
@@ -377,8 +456,8 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
                     const uint32_t task = lane + 64 * rr;
                     if (task < 16 * m) {
                         const uint32_t p = m + (task >> 4), e = task & 15u;
-                        const uint32_t xv = sm.x[2 * p][e];
-                        res[rr] = (xv & ~15u) + sm.x[2 * p + 1][xv & 15u];
+                        const uint32_t xv = sm.k.x[2 * p][e];
+                        res[rr] = (xv & ~15u) + sm.k.x[2 * p + 1][xv & 15u];
                     }
                 }
                 wave_lds_sync();
@@ -386,111 +465,100 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
                 for (uint32_t rr = 0; rr < 2; ++rr) {
                     const uint32_t task = lane + 64 * rr;
                     if (task < 16 * m)
-                        sm.x[m + (task >> 4)][task & 15u] = res[rr];
+                        sm.k.x[m + (task >> 4)][task & 15u] = res[rr];
                 }
                 wave_lds_sync();
             }
-            const uint32_t tag = (uint32_t)(abase + (uint64_t)G * (r + 1));
-            uint64_t *gr = gran + ((uint64_t)(r & 1u) * G1_GMAX + b) * 16;
-            if (lane < 16)
-                g1_store_granule(&gr[lane], (uint64_t)(sm.x[1][lane] | (bad << 31)) | ((uint64_t)tag << 32));
-#if GC_G4_STRICT
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) {
-                __hip_atomic_fetch_add(&hdr->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // wait for the round's G arrivals
-                const uint64_t target = abase + (uint64_t)G * (r + 1);
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                uint32_t ok = 1;
-                while (__hip_atomic_load(&hdr->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > G1_TIMEOUT_TICKS) {
-                        ok = 0;
-                        break;
-                    }
-                }
-#if GC_G4_STRICT
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-                sm.flag = ok;
-            }
+            if (lane < 16)  // bit 31 of each entry: this tile holds a value outside [0, 255]
+                g1_store_granule(&gran[((uint64_t)(r & 1u) * G1_GMAX + b) * 16 + lane],
+                                 (uint64_t)(sm.k.x[1][lane] | (bad << 31)) | ((uint64_t)tag << 32));
         }
-        __syncthreads();
-        if (!sm.flag)
-            tmo = 1;
-        // 5. the round's tables: thread (k, e) reads tiles 4k..4k+3 and composes them
+        G1_STAMP(3);
+        // 5. every tile's table: thread t re-reads granules t, t + 1024, ...
+        // (tile i, entry e = index / 16, index % 16) until every tag matches
         uint32_t rbad = 0;
         {
-            const uint32_t k = t >> 4, e = t & 15u;
-            const uint32_t tag = (uint32_t)(abase + (uint64_t)G * (r + 1));
             const uint64_t *gr = gran + (uint64_t)(r & 1u) * G1_GMAX * 16;
-            uint32_t a[4];
+            constexpr uint32_t NG = G1_GMAX * 16 / G1_THREADS;  // 4
+            uint64_t g[NG];
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                bool ok = true;
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint32_t i = 4 * k + j;
-                a[j] = e;  // identity past the grid
-                if (i < G && !tmo) {
-                    uint64_t g = g1_load_granule(&gr[i * 16 + e]);
-                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                    while ((uint32_t)(g >> 32) != tag) {  // the count says it is there; visibility may lag
-                        __builtin_amdgcn_s_sleep(1);
-                        g = g1_load_granule(&gr[i * 16 + e]);
-                        if (__builtin_amdgcn_s_memrealtime() - t0 > G1_TIMEOUT_TICKS) {
-                            tmo = 1;
-                            break;
-                        }
+                for (uint32_t j = 0; j < NG; ++j) {
+                    const uint32_t i = t + j * G1_THREADS;
+                    if (i < 16 * G && !tmo) {
+                        g[j] = g1_load_granule(&gr[i]);
+                        ok &= (uint32_t)(g[j] >> 32) == tag;
                     }
-                    rbad |= (uint32_t)g >> 31;
-                    a[j] = (uint32_t)g & 0x7fffffffu;
                 }
-                sm.u.t0[i][e] = a[j];
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0)  // wave-uniform exit
+                    break;
+                __builtin_amdgcn_s_sleep(2);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > G1_TIMEOUT_TICKS) {
+                    tmo = 1;
+                    break;
+                }
             }
-            uint32_t c = a[0];
 #pragma unroll
-            for (uint32_t j = 1; j < 4; ++j) {
-                const int src_lane = (int)((lane & ~15u) | (c & 15u));
-                c = (c & ~15u) + (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane * 4, (int)a[j]);
+            for (uint32_t j = 0; j < NG; ++j) {
+                const uint32_t i = t + j * G1_THREADS;
+                uint32_t a = i & 15u;  // identity past the grid
+                if (i < 16 * G && !tmo) {
+                    rbad |= (uint32_t)g[j] >> 31;
+                    a = (uint32_t)g[j] & 0x7fffffffu;
+                }
+                sm.k.u.t0[i >> 4][i & 15u] = a;
             }
-            sm.g4[k][e] = c;
         }
         rbad = __syncthreads_or(rbad);
         tmo = __syncthreads_or(tmo);
-        if (t < 256) {
+        G1_STAMP(4);
+        if (r == 0 && b == 0 && t == 0)  // every block has read seq: the next launch tags on from here
+            __hip_atomic_store(&hdr->seq, seq + R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        {  // compositions of 4 tiles (thread (k, e), k < 64)
             const uint32_t k = t >> 4, e = t & 15u;
-            uint32_t c = sm.g4[4 * k][e];
+            uint32_t c = sm.k.u.t0[4 * k][e];
 #pragma unroll
             for (uint32_t j = 1; j < 4; ++j)
-                c = (c & ~15u) + sm.g4[4 * k + j][c & 15u];
-            sm.g16[k][e] = c;
+                c = (c & ~15u) + sm.k.u.t0[4 * k + j][c & 15u];
+            sm.k.g4[k][e] = c;
+        }
+        __syncthreads();
+        if (t < 256) {
+            const uint32_t k = t >> 4, e = t & 15u;
+            uint32_t c = sm.k.g4[4 * k][e];
+#pragma unroll
+            for (uint32_t j = 1; j < 4; ++j)
+                c = (c & ~15u) + sm.k.g4[4 * k + j][c & 15u];
+            sm.k.g16[k][e] = c;
         }
         __syncthreads();
         if (t < 64) {
             const uint32_t k = t >> 4, e = t & 15u;
-            uint32_t c = sm.g16[4 * k][e];
+            uint32_t c = sm.k.g16[4 * k][e];
 #pragma unroll
             for (uint32_t j = 1; j < 4; ++j)
-                c = (c & ~15u) + sm.g16[4 * k + j][c & 15u];
-            sm.g64[k][e] = c;
+                c = (c & ~15u) + sm.k.g16[4 * k + j][c & 15u];
+            sm.k.g64[k][e] = c;
         }
         __syncthreads();
         if (t == 0) {  // the block's entry and word base; the round's exit and total
             uint32_t s = carry_s, base = 0;
             const uint32_t i3 = b >> 6, i2 = (b >> 4) & 3u, i1 = (b >> 2) & 3u, i0 = b & 3u;
             for (uint32_t j = 0; j < i3; ++j)
-                base += g1_apply(sm.g64[j][s], s);
+                base += g1_apply(sm.k.g64[j][s], s);
             for (uint32_t j = 0; j < i2; ++j)
-                base += g1_apply(sm.g16[4 * i3 + j][s], s);
+                base += g1_apply(sm.k.g16[4 * i3 + j][s], s);
             for (uint32_t j = 0; j < i1; ++j)
-                base += g1_apply(sm.g4[16 * i3 + 4 * i2 + j][s], s);
+                base += g1_apply(sm.k.g4[16 * i3 + 4 * i2 + j][s], s);
             for (uint32_t j = 0; j < i0; ++j)
-                base += g1_apply(sm.u.t0[64 * i3 + 16 * i2 + 4 * i1 + j][s], s);
+                base += g1_apply(sm.k.u.t0[64 * i3 + 16 * i2 + 4 * i1 + j][s], s);
             sm.s_b = s;
             sm.base_b = base;
             uint32_t se = carry_s, tw = 0;
             for (uint32_t j = 0; j < G1_GMAX / 64; ++j)
-                tw += g1_apply(sm.g64[j][se], se);
+                tw += g1_apply(sm.k.g64[j][se], se);
             sm.s_end = se;
             sm.tw = tw;
         }
@@ -499,71 +567,76 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
         const uint64_t round_end = carry_base + sm.tw;
         if (round_end > cap)
             nospc = 1;
+        const bool emit = !bad_all && !nospc && !tmo;
         // 6. this thread's entry and word base: down the block's tree, then the wave's
-        if (!bad_all && !nospc && !tmo && in_tile) {
-            uint32_t s = sm.s_b;
-            uint64_t base = carry_base + sm.base_b;
+        uint32_t s = sm.s_b;
+        uint64_t base = carry_base + sm.base_b;
+        if (emit) {
             uint32_t node = 1;
 #pragma unroll
             for (int d = 3; d >= 0; --d) {
                 const uint32_t bit = (w >> d) & 1u;
                 if (bit)
-                    base += g1_apply(sm.x[2 * node][s], s);
+                    base += g1_apply(sm.k.x[2 * node][s], s);
                 node = 2 * node + bit;
             }
+            if (lane == 0)
+                sm.wbase[w] = base;
+            const uint32_t xw = sm.k.x[16 + w][s];  // the wave's words from its entry
+            if (lane == 0)
+                sm.wcnt[w] = xw >> 4;
             node = 1;
 #pragma unroll
             for (int d = 5; d >= 0; --d) {
                 const uint32_t bit = (lane >> d) & 1u;
                 if (bit)
-                    base += g1_apply(reinterpret_cast<const uint16_t *>(sm.pl[w][node - 1])[s], s);
+                    base += g1_apply(reinterpret_cast<const uint16_t *>(sm.k.pl[w][node - 1])[s], s);
                 node = 2 * node + bit;
             }
-            // 7. the words: modes from the class bits, values from the LDS bytes
-            uint32_t pos = s;  // G4_DEAD (15) when the chain ended before this range
+        }
+        G1_STAMP(5);
+        // 7. the words, half the waves at a time: each thread lists its word
+        // starts (position in the wave's range | mode << 14) from its class
+        // bits, then every lane of the block packs listed words, consecutive
+        // lanes consecutive words, from the LDS bytes
+        if (emit) {
+#pragma unroll 1
+            for (uint32_t half = 0; half < 2; ++half) {
+                __syncthreads();  // the trees (or the previous half's lists) are no longer read
+                if ((w >> 3) == half && in_tile) {
+                    uint16_t *wl = sm.wl[w & 7u];
+                    uint32_t pos = s, j = (uint32_t)(base - sm.wbase[w]);  // DEAD (15) past n
 #pragma unroll
-            for (uint32_t k = 0; k < G1_BLK; ++k) {  // block by block: the class bits indexed statically
-                const uint32_t end = std::min<uint32_t>(live, G4_SEG * (k + 1));
-                while (pos < end) {
-                    const uint32_t mode = g4_mode(cls[k], pos & 31u);
-                    const uint32_t a = G1_RANGE * t + pos;
-                    const uint32_t *d = &sm.v[a >> 2];
-                    const uint32_t sh = a & 3u;
-                    const uint32_t u0 = d[0], u1 = d[1], u2 = d[2], u3 = d[3], u4 = d[4];
-                    const uint32_t x[4] = {__builtin_amdgcn_alignbyte(u1, u0, sh),
-                                           __builtin_amdgcn_alignbyte(u2, u1, sh),
-                                           __builtin_amdgcn_alignbyte(u3, u2, sh),
-                                           __builtin_amdgcn_alignbyte(u4, u3, sh)};
-                    const uint32_t bb = g4_bits(mode), top = g4_top(mode), cnt = g4_cnt(mode);
-                    uint32_t code = mode << 30;
-#pragma unroll
-                    for (uint32_t q = 0; q < 15; ++q)  // values past cnt belong to the next word: left out
-                        if (q < cnt)
-                            code |= ((x[q >> 2] >> (8 * (q & 3))) & 0xffu) << (top - q * bb);
-                    out[base++] = (int32_t)code;
-                    pos += cnt;
+                    for (uint32_t k = 0; k < G1_BLK; ++k) {  // block by block: the class bits indexed statically
+                        const uint32_t end = std::min<uint32_t>(live, G4_SEG * (k + 1));
+                        while (pos < end) {
+                            const uint32_t mode = g4_mode(cls[k], pos & 31u);
+                            wl[j++] = (uint16_t)((G1_RANGE * lane + pos) | (mode << 14));
+                            pos += g4_cnt(mode);
+                        }
+                    }
+                }
+                __syncthreads();
+                {
+                    const uint32_t L = w & 7u, wv = 8 * half + L;  // two waves per list
+                    const uint32_t cnt = sm.wcnt[wv];
+                    const uint64_t ob = sm.wbase[wv];
+                    const uint16_t *wl = sm.wl[L];
+                    for (uint32_t k = (w >> 3) * 64 + lane; k < cnt; k += 128) {
+                        const uint32_t ent = wl[k];
+                        out[ob + k] = (int32_t)g1_word(sm, 64 * G1_RANGE * wv + (ent & 0x3fffu), ent >> 14);
+                    }
                 }
             }
         }
         carry_s = sm.s_end;
         carry_base = round_end;
         __syncthreads();  // the next round rewrites the LDS image and the trees
+        G1_STAMP(6);
     }
-    if (tid == 0) {
-        if (tmo)
-            __hip_atomic_fetch_or(&hdr->tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t old = __hip_atomic_fetch_add(&hdr->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == G - 1) {  // the last block: results, then re-arm the header for the next call
-            const uint32_t any_tmo = __hip_atomic_load(&hdr->tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *nwords = carry_base;
-            *status = (bad_all ? G4_STATUS_RANGE : 0u) | (nospc ? G4_STATUS_NOSPC : 0u) |
-                      (any_tmo ? G4_STATUS_TIMEOUT : 0u);
-            const uint64_t arrived = __hip_atomic_load(&hdr->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&hdr->abase, any_tmo ? arrived : abase + (uint64_t)G * R, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&hdr->tmo, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&hdr->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    if (b == 0 && tid == 0) {
+        *nwords = carry_base;
+        *status = (bad_all ? G4_STATUS_RANGE : 0u) | (nospc ? G4_STATUS_NOSPC : 0u) | (tmo ? G4_STATUS_TIMEOUT : 0u);
     }
 }
 
