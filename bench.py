@@ -565,7 +565,32 @@ def _config5(torch, dist, gcodec, codec, dev, world, sync_ms, n5):
             tr = pipe.trace(x5, out5)
             r["overlap"] = tr
         res["config5_1b_8bit_chunked"] = r
-        del x5, out5, pipe
+        del pipe
+        if world == 1:
+            # config 5's own lane width on one GPU: lanes sized for W = 8 (12-bit, 2 per word),
+            # no collective; the full-bucket encode / decode kernels timed with HIP events
+            pipe8 = gcodec.ChunkedQSGDAllReduce(n5, 8, dev, chunks=8, generator=gen, world=8, collective=False)
+            t8 = sync_ms(lambda: pipe8(x5, out5), reps=3)
+            del pipe8
+            l8 = codec.qsgd_layout(n5, 8, 8)
+            w8 = torch.empty(l8.plane_words, dtype=torch.int32, device=dev)
+            nrm5 = codec.absmax(x5)
+            ms_e = _events(torch, lambda: codec.qsgd_encode(x5, nrm5, 8, gen.reserve(n5), 8, out=w8, lanes=l8), 5)
+            ms_d = _events(torch, lambda: codec.qsgd_decode(w8, n5, nrm5, 8, 8, 1.0 / 8, out=out5, lanes=l8), 5)
+            eb = 4 * n5 + 4 * l8.plane_words
+
+            def kr(ms):
+                gbs = eb / (ms * 1e-3) / 1e9
+                return {"us": ms * 1e3, "algorithmic_bytes": eb, "gbs": gbs, "frac_hbm_peak": gbs / HBM_PEAK_GBS}
+
+            res["config5_1b_8bit_w8_lanes"] = {
+                "n": n5, "chunks": 8, "world_lanes": 8, "lane_bits": l8.bits, "lanes_per_word": l8.per_word,
+                "packed_bytes_per_rank": 4 * l8.plane_words, "reference_wire_bytes_per_rank": 4 * n5,
+                "ms_per_step_chunked_no_collective": t8, "grad_floats_per_s": n5 / (t8 * 1e-3),
+                "k_qsgd_encode": kr(ms_e), "k_qsgd_decode": kr(ms_d),
+                "note": "the W = 8 layout of config 5 (compressors.py:294-297, reducer.py:498-554 at b = 8) on one "
+                        "GPU: the same kernels an 8-GPU rank runs, without the SUM"}
+            del w8
     except torch.cuda.OutOfMemoryError:
         res["config5_1b_8bit_chunked"] = {"skipped": "out of device memory"}
     torch.cuda.empty_cache()
@@ -594,6 +619,8 @@ def _timed_steps(torch, dist, fn, k, world, dev) -> float:
 
 
 def reduce_legs(torch, dist, codec, step, words, dec, norm, n, bits, world, lanes, K, dev) -> dict:
+    x_of = lambda f: f.x  # noqa: E731 — the headline bucket and encode, carried on step()
+    enc_of = lambda f: f.encode  # noqa: E731
     """The full DP path: absmax -> MAX -> encode -> all_reduce(SUM packed words)
     -> decode + 1/W; at N >= 4 (even) also through gcodec.NodeTopology as two
     'nodes' of N/2 ranks, with the flat and hierarchical sums compared."""
@@ -606,9 +633,60 @@ def reduce_legs(torch, dist, codec, step, words, dec, norm, n, bits, world, lane
         codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
 
     pel = _timed_steps(torch, dist, path, K, world, dev)
-    res["reduce_path"] = {"grad_floats_per_s": world * n * K / pel, "ms_per_step": pel / K * 1e3,
-                          "packed_bytes_per_rank": 4 * lanes.plane_words,
-                          "steps": "absmax, all_reduce MAX, encode, all_reduce SUM (RCCL), decode + 1/W"}
+    rp = {"grad_floats_per_s": world * n * K / pel, "ms_per_step": pel / K * 1e3,
+          "packed_bytes_per_rank": 4 * lanes.plane_words,
+          "steps": "absmax, all_reduce MAX, encode, all_reduce SUM (RCCL), decode + 1/W"}
+    # per phase, from HIP events on the codec's (torch's current) stream: an
+    # event after each phase of one path() call; RCCL runs on its own stream and
+    # the current stream waits for it, so the event after a collective marks its
+    # completion as the next phase sees it.  Median of 5 traced calls, MAX over ranks.
+    names = ("absmax", "max", "encode", "sum", "decode")
+    traced = []
+    for _ in range(5):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ev[0].record()
+        codec.absmax(x_of(step), out=norm)
+        ev[1].record()
+        if world > 1:
+            dist.all_reduce(norm, op=dist.ReduceOp.MAX)
+        ev[2].record()
+        enc_of(step)()
+        ev[3].record()
+        if world > 1:
+            dist.all_reduce(words)
+        ev[4].record()
+        codec.qsgd_decode(words, n, norm, bits, world, 1.0 / world, out=dec, lanes=lanes)
+        ev[5].record()
+        torch.cuda.synchronize()
+        traced.append([ev[i].elapsed_time(ev[i + 1]) for i in range(5)])
+    ph = torch.tensor([sorted(c)[2] for c in zip(*traced)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(ph, op=dist.ReduceOp.MAX)
+    rp["phase_ms"] = dict(zip(names, ph.tolist()))
+    rp["phase_method"] = ("HIP events between the phases of one call on the current stream (median of 5 calls, "
+                          "MAX over ranks); the untraced path above is what ms_per_step measures")
+    if world > 1:
+        # the packed SUM alone, and the reference's NoneAllReducer (reducer.py:140-170): an
+        # fp32 all_reduce of the same bucket, both timed as K barrier-bracketed calls, MAX over ranks
+        busf = 2.0 * (world - 1) / world
+        t_sum = _timed_steps(torch, dist, lambda: dist.all_reduce(words), K, world, dev) / K
+        pb = 4 * lanes.plane_words
+        xf = x_of(step).clone()
+        t_f32 = _timed_steps(torch, dist, lambda: dist.all_reduce(xf), K, world, dev) / K
+        del xf
+        rp["sum_packed"] = {"ms": t_sum * 1e3, "bytes_per_rank": pb, "algbw_gbs": pb / t_sum / 1e9,
+                            "busbw_gbs": busf * pb / t_sum / 1e9}
+        rp["sum_fp32_reference"] = {"ms": t_f32 * 1e3, "bytes_per_rank": 4 * n, "algbw_gbs": 4 * n / t_f32 / 1e9,
+                                    "busbw_gbs": busf * 4 * n / t_f32 / 1e9,
+                                    "reference": "NoneAllReducer, reducer.py:140-170 (fp32 all_reduce of the bucket)"}
+        rp["sum_fp32_over_packed"] = t_f32 / t_sum
+        rp["wire_bytes_fp32_over_packed"] = 4 * n / pb
+        rp["busbw_note"] = ("busbw = 2(N-1)/N x bytes / t (ring all-reduce); MI355X xGMI: 7 links x ~153 GB/s per "
+                            "GPU, one ring uses one link each way")
+    res["reduce_path"] = rp
     if world >= 4 and world % 2 == 0:
         # intra reduce-scatter, "inter-node" all-reduce of 1/L of the words, intra
         # all-gather: the multi-node code path on one node
@@ -883,6 +961,8 @@ def main():
     def step():
         norm_step()
         encode_step()
+
+    step.x, step.encode = x, encode_step  # for reduce_legs' per-phase trace
 
     norms = (norm, torch.empty_like(norm))
 

@@ -178,13 +178,17 @@ struct G1Smem {
             uint32_t g64[G1_GMAX / 64][16];
             uint32_t x[32][16];                   // the tree of the 16 wave roots (nodes 1..31)
         } k;
-        uint16_t wl[G1_WAVES / 2][64 * G1_RANGE / 3 + 4];  // emission: half the waves' word lists at a time
+        uint16_t wl[G1_WAVES / 2][64 * G1_RANGE / 3 + 4];  // emission, a big tile: half the waves' lists at a time
+        uint16_t wlb[1];                          // emission: the block's word list (G1_WLCAP entries)
     };
     uint64_t wbase[G1_WAVES];                     // each wave's first word (absolute)
     uint32_t wcnt[G1_WAVES];                      // each wave's words
+    uint32_t woff[G1_WAVES];                      // each wave's first word within the tile
     uint64_t base_b;                              // the block's word base within the round
-    uint32_t s_b, s_end, tw;
+    uint32_t s_b, s_end, tw, tile_words;
 };
+// entries of the block's word list: the tree storage, free by then
+constexpr uint32_t G1_WLCAP = (uint32_t)(sizeof(((G1Smem *)nullptr)->k) / 2);
 
 // the waves of a workgroup run one LDS tree each: order a wave's LDS stores
 // before its later loads of other lanes' rows (LDS executes a wave's
@@ -276,21 +280,62 @@ __device__ __forceinline__ uint32_t g1_load_tile(G1Smem &sm, const int32_t *__re
     return __syncthreads_or(bad > 255u);
 }
 
-// pack one word of mode `mode` from the bytes at tile offset a (zero past n)
-__device__ __forceinline__ uint32_t g1_word(const G1Smem &sm, uint32_t a, uint32_t mode)
+// pack one word of mode `mode` from the bytes at tile offset a (zero past n).
+// Per mode a SWAR form over the 16 bytes from a; `pres` (bit m: some lane of
+// the wave packs a mode-m word, wave-uniform) skips the forms no lane needs.
+//   mode 0 (15 x 2 bits): per dword (x * 0x40100401) >> 24 = b0 b1 b2 b3 as
+//          2-bit fields, b0 on top (no two product terms share a bit);
+//   mode 1 (7 x 4 bits):  per dword (x << 4 | x >> 8) holds b0b1 / b2b3 in
+//          bytes 0 / 2, one perm joins them;
+//   mode 2 (4 x 7 bits):  byte-swap, then 8 -> 7 -> 14-bit field merges;
+//   mode 3 (3 x 8 bits):  one perm.
+__device__ __forceinline__ uint32_t g1_word(const G1Smem &sm, uint32_t a, uint32_t mode, uint32_t pres)
 {
     const uint32_t *d = &sm.v[a >> 2];
     const uint32_t sh = a & 3u;
-    const uint32_t u0 = d[0], u1 = d[1], u2 = d[2], u3 = d[3], u4 = d[4];
-    const uint32_t x[4] = {__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
-                           __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
-    const uint32_t bb = g4_bits(mode), top = g4_top(mode), cnt = g4_cnt(mode);
-    uint32_t code = mode << 30;
-#pragma unroll
-    for (uint32_t q = 0; q < 15; ++q)  // values past cnt belong to the next word: left out
-        if (q < cnt)
-            code |= ((x[q >> 2] >> (8 * (q & 3))) & 0xffu) << (top - q * bb);
+    const uint32_t u0 = d[0], u1 = d[1];
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(u1, u0, sh);
+    uint32_t code = 0;
+    if (pres & 3u) {
+        const uint32_t u2 = d[2];
+        const uint32_t x1 = __builtin_amdgcn_alignbyte(u2, u1, sh);
+        if (pres & 1u) {
+            const uint32_t u3 = d[3], u4 = d[4];
+            const uint32_t x2 = __builtin_amdgcn_alignbyte(u3, u2, sh);
+            const uint32_t x3 = __builtin_amdgcn_alignbyte(u4, u3, sh) & 0x00ffffffu;  // b15 is not in the word
+            constexpr uint32_t M = 0x40100401u;
+            const uint32_t c0 = ((x0 * M) >> 24 << 22) | ((x1 * M) >> 24 << 14) | ((x2 * M) >> 24 << 6) |
+                                ((x3 * M) >> 26);
+            code = mode == 0 ? c0 : code;
+        }
+        if (pres & 2u) {
+            const uint32_t x1m = x1 & 0x00ffffffu;  // b7 is not in the word
+            const uint32_t y0 = (x0 << 4) | (x0 >> 8), y1 = (x1m << 4) | (x1m >> 8);
+            const uint32_t h0 = __builtin_amdgcn_perm(y0, y0, 0x0c0c0002u), h1 = __builtin_amdgcn_perm(y1, y1, 0x0c0c0002u);
+            const uint32_t c1 = 0x40000000u | (h0 << 14) | (h1 >> 2);
+            code = mode == 1 ? c1 : code;
+        }
+    }
+    if (pres & 4u) {
+        const uint32_t r = __builtin_amdgcn_perm(x0, x0, 0x00010203u);  // b0 << 24 | b1 << 16 | b2 << 8 | b3
+        const uint32_t uu = (r & 0x007f007fu) | ((r >> 1) & 0x3f803f80u);
+        const uint32_t v = (uu & 0x3fffu) | ((uu >> 2) & 0x0fffc000u);
+        const uint32_t c2 = 0x80000000u | (v << 2);
+        code = mode == 2 ? c2 : code;
+    }
+    if (pres & 8u) {
+        const uint32_t c3 = 0xc0000000u | (__builtin_amdgcn_perm(x0, x0, 0x0c000102u) << 6);
+        code = mode == 3 ? c3 : code;
+    }
     return code;
+}
+
+__device__ __forceinline__ uint32_t g1_modes_present(uint32_t mode, bool active)
+{
+    return (__builtin_amdgcn_ballot_w64(active && mode == 0) ? 1u : 0u) |
+           (__builtin_amdgcn_ballot_w64(active && mode == 1) ? 2u : 0u) |
+           (__builtin_amdgcn_ballot_w64(active && mode == 2) ? 4u : 0u) |
+           (__builtin_amdgcn_ballot_w64(active && mode == 3) ? 8u : 0u);
 }
 
 // Persistent pack.  Grid: G <= one block per CU (the LDS image admits one);
@@ -556,6 +601,7 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
                 base += g1_apply(sm.k.u.t0[64 * i3 + 16 * i2 + 4 * i1 + j][s], s);
             sm.s_b = s;
             sm.base_b = base;
+            sm.tile_words = sm.k.x[1][s] >> 4;
             uint32_t se = carry_s, tw = 0;
             for (uint32_t j = 0; j < G1_GMAX / 64; ++j)
                 tw += g1_apply(sm.k.g64[j][se], se);
@@ -580,8 +626,10 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
                     base += g1_apply(sm.k.x[2 * node][s], s);
                 node = 2 * node + bit;
             }
-            if (lane == 0)
+            if (lane == 0) {
                 sm.wbase[w] = base;
+                sm.woff[w] = (uint32_t)(base - carry_base - sm.base_b);
+            }
             const uint32_t xw = sm.k.x[16 + w][s];  // the wave's words from its entry
             if (lane == 0)
                 sm.wcnt[w] = xw >> 4;
@@ -595,36 +643,75 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
             }
         }
         G1_STAMP(5);
-        // 7. the words, half the waves at a time: each thread lists its word
-        // starts (position in the wave's range | mode << 14) from its class
-        // bits, then every lane of the block packs listed words, consecutive
-        // lanes consecutive words, from the LDS bytes
+        // 7. the words: each thread lists its word starts (position in its
+        // wave's range | mode << 14) from its class bits, then every lane of
+        // the block packs listed words, consecutive lanes consecutive words,
+        // from the LDS bytes.  A tile of more than G1_WLCAP words (values
+        // mostly >= 128) lists half its waves at a time.
         if (emit) {
-#pragma unroll 1
-            for (uint32_t half = 0; half < 2; ++half) {
-                __syncthreads();  // the trees (or the previous half's lists) are no longer read
-                if ((w >> 3) == half && in_tile) {
-                    uint16_t *wl = sm.wl[w & 7u];
-                    uint32_t pos = s, j = (uint32_t)(base - sm.wbase[w]);  // DEAD (15) past n
+            __syncthreads();  // the trees are no longer read
+            const uint32_t tw_tile = sm.tile_words;
+            if (tw_tile <= G1_WLCAP) {
+                if (in_tile) {
+                    uint32_t pos = s, j = sm.woff[w] + (uint32_t)(base - sm.wbase[w]);  // DEAD (15) past n
 #pragma unroll
                     for (uint32_t k = 0; k < G1_BLK; ++k) {  // block by block: the class bits indexed statically
                         const uint32_t end = std::min<uint32_t>(live, G4_SEG * (k + 1));
                         while (pos < end) {
                             const uint32_t mode = g4_mode(cls[k], pos & 31u);
-                            wl[j++] = (uint16_t)((G1_RANGE * lane + pos) | (mode << 14));
+                            sm.wlb[j++] = (uint16_t)((G1_RANGE * lane + pos) | (mode << 14));
                             pos += g4_cnt(mode);
                         }
                     }
                 }
                 __syncthreads();
-                {
+                const uint64_t ob = carry_base + sm.base_b;
+                for (uint32_t k0 = 0; k0 < tw_tile; k0 += G1_THREADS) {
+                    const uint32_t k = k0 + t;
+                    const bool act = k < tw_tile;
+                    const uint32_t ent = act ? sm.wlb[k] : 0u;
+                    uint32_t wv = 0;  // the last wave whose first word is <= k
+#pragma unroll
+                    for (uint32_t st = G1_WAVES / 2; st >= 1; st >>= 1)
+                        wv += sm.woff[wv + st] <= k ? st : 0u;
+                    const uint32_t mode = ent >> 14;
+                    const uint32_t code = g1_word(sm, 64 * G1_RANGE * wv + (ent & 0x3fffu), mode,
+                                                  g1_modes_present(mode, act));
+                    if (act)
+                        out[ob + k] = (int32_t)code;
+                }
+            } else {
+#pragma unroll 1
+                for (uint32_t half = 0; half < 2; ++half) {
+                    if (half)
+                        __syncthreads();  // the first half's lists are packed
+                    if ((w >> 3) == half && in_tile) {
+                        uint16_t *wl = sm.wl[w & 7u];
+                        uint32_t pos = s, j = (uint32_t)(base - sm.wbase[w]);
+#pragma unroll
+                        for (uint32_t k = 0; k < G1_BLK; ++k) {
+                            const uint32_t end = std::min<uint32_t>(live, G4_SEG * (k + 1));
+                            while (pos < end) {
+                                const uint32_t mode = g4_mode(cls[k], pos & 31u);
+                                wl[j++] = (uint16_t)((G1_RANGE * lane + pos) | (mode << 14));
+                                pos += g4_cnt(mode);
+                            }
+                        }
+                    }
+                    __syncthreads();
                     const uint32_t L = w & 7u, wv = 8 * half + L;  // two waves per list
                     const uint32_t cnt = sm.wcnt[wv];
                     const uint64_t ob = sm.wbase[wv];
                     const uint16_t *wl = sm.wl[L];
-                    for (uint32_t k = (w >> 3) * 64 + lane; k < cnt; k += 128) {
-                        const uint32_t ent = wl[k];
-                        out[ob + k] = (int32_t)g1_word(sm, 64 * G1_RANGE * wv + (ent & 0x3fffu), ent >> 14);
+                    for (uint32_t k0 = (w >> 3) * 64; k0 < cnt; k0 += 128) {
+                        const uint32_t k = k0 + lane;
+                        const bool act = k < cnt;
+                        const uint32_t ent = act ? wl[k] : 0u;
+                        const uint32_t mode = ent >> 14;
+                        const uint32_t code = g1_word(sm, 64 * G1_RANGE * wv + (ent & 0x3fffu), mode,
+                                                      g1_modes_present(mode, act));
+                        if (act)
+                            out[ob + k] = (int32_t)code;
                     }
                 }
             }

@@ -444,11 +444,15 @@ class Segments:
 
     @staticmethod
     def key_of(tensors):
-        """(data pointers, sizes) of a tensor list: what the table records.
-        Two attribute maps: a reducer step computes this for two lists of
-        ~50-160 tensors every step (the former key with dtype and device sets
-        cost ~4x as much host time)."""
-        return tuple(map(torch.Tensor.data_ptr, tensors)), tuple(map(torch.Tensor.numel, tensors))
+        """(data pointers, sizes, element sizes, contiguity) of a tensor list:
+        what the table records plus what makes it valid for the list.  A list
+        at recycled addresses with the same sizes but another dtype (a model
+        cast to fp16 / bf16) or a non-contiguous view of the same storage gets
+        another key, so it never hits an fp32 table.  Device and
+        the fp32 dtype itself are checked when a table is built
+        (eligible_list); four attribute maps, no per-tensor Python loop."""
+        return (tuple(map(torch.Tensor.data_ptr, tensors)), tuple(map(torch.Tensor.numel, tensors)),
+                tuple(map(torch.Tensor.element_size, tensors)), tuple(map(torch.Tensor.is_contiguous, tensors)))
 
     @staticmethod
     def eligible_list(tensors) -> bool:

@@ -34,15 +34,19 @@ class ChunkedQSGDAllReduce:
     """reduce(x) = decode(SUM over ranks of encode(x)) * 1/W, chunk-pipelined.
 
     world: the W the lanes are sized for; defaults to the group's size.
+    collective: run the MAX / SUM collectives (default: world > 1).  False
+    keeps the W-sized lanes without them (timing a rank's kernels on one GPU;
+    the decoded floats then assume a SUM that did not happen).
     """
 
     def __init__(self, n: int, bits: int, device, chunks: int = 4, group=None, generator=None, codec=None,
-                 world: int | None = None):
+                 world: int | None = None, collective: bool | None = None):
         self.n, self.bits, self.device = n, bits, torch.device(device)
         self.group = group
         if world is None:
             world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.world = int(world)
+        self.collective = self.world > 1 if collective is None else bool(collective)
         self.codec = codec or _hip_codec
         self.gen = generator or default_generator
         chunks = max(1, min(chunks, n))
@@ -59,13 +63,13 @@ class ChunkedQSGDAllReduce:
 
     def _max(self, norm: torch.Tensor):
         """MAX of the local norms (enqueued in line: every encode needs it)."""
-        if self.world > 1:
+        if self.collective:
             dist.all_reduce(norm, op=dist.ReduceOp.MAX, group=self.group)
 
     def _reduce(self, words: torch.Tensor):
         """Asynchronous SUM of one chunk's packed words; the work handle, or
         None when the words are final on the compute stream."""
-        if self.world > 1:
+        if self.collective:
             return dist.all_reduce(words, group=self.group, async_op=True)
         return None
 
@@ -89,6 +93,7 @@ class ChunkedQSGDAllReduce:
         self.dec_stream.wait_event(norm_ready)
         for (s, e), ln, wd in zip(self.bounds, self.lanes, self.words):
             rng = self.gen.reserve(e - s, 1, device=self.device, backend=self.codec)
+            mark("encode_start", compute)
             self.codec.qsgd_encode(x[s:e], self.norm, self.bits, rng, W, out=wd, lanes=ln)
             mark("encode_end", compute)
             work = self._reduce(wd)
@@ -119,18 +124,28 @@ class ChunkedQSGDAllReduce:
         """One call with HIP timing events on every stream it uses: per chunk
         the end of its encode, of its SUM (seen from a probe stream that waits
         for that chunk's collective only), and the start / end of its decode,
-        in ms from the call's start.  `decode_overlaps_next_sum` is the
-        evidence that the pipeline overlaps: decode(c) started before SUM(c+1)
-        ended, for every c."""
+        in ms from the call's start.  `decode_overlaps_next_sum`: decode(c)
+        started before SUM(c+1) ended, for every c; `encode_overlaps_previous_sum`:
+        encode(c+1) ran while SUM(c) was in flight, for every c (the overlap that
+        matters when the SUM is the long pole)."""
         torch.cuda.synchronize(self.device)
         tr = {"probe": torch.cuda.Stream(self.device)}
         self(x, out, _trace=tr)
         torch.cuda.synchronize(self.device)
         t0 = tr["start"][0]
         ms = {k: [t0.elapsed_time(e) for e in tr[k]]
-              for k in ("encode_end", "sum_end", "decode_start", "decode_end")}
+              for k in ("encode_start", "encode_end", "sum_end", "decode_start", "decode_end")}
         C = len(self.bounds)
         started = [ms["decode_start"][c] < ms["sum_end"][c + 1] for c in range(C - 1)]
         ended = [ms["decode_end"][c] < ms["sum_end"][c + 1] for c in range(C - 1)]
+        # encode(c+1) against SUM(c): the SUMs run in order on one communicator, so
+        # SUM(c) starts no earlier than max(encode_end(c), sum_end(c-1)); the overlap
+        # is that interval's intersection with encode(c+1)'s
+        ov = []
+        for c in range(C - 1):
+            s0 = max(ms["encode_end"][c], ms["sum_end"][c - 1] if c else 0.0)
+            ov.append(max(0.0, min(ms["encode_end"][c + 1], ms["sum_end"][c]) - max(ms["encode_start"][c + 1], s0)))
         return {"chunks": C, "ms": ms, "decode_overlaps_next_sum": bool(started) and all(started),
-                "decode_c_started_before_sum_c1_ended": started, "decode_c_ended_before_sum_c1_ended": ended}
+                "decode_c_started_before_sum_c1_ended": started, "decode_c_ended_before_sum_c1_ended": ended,
+                "encode_c1_overlap_sum_c_ms": ov,
+                "encode_overlaps_previous_sum": bool(ov) and all(v > 0 for v in ov)}

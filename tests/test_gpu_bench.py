@@ -75,9 +75,33 @@ def test_plain_bench_gpus_n_launches_ranks(world):
     pg = d["process_group"]
     assert pg["world_size"] == world and len(pg["ranks"]) == world and pg["backend"] == "gloo"
     assert sorted(x["rank"] for x in pg["ranks"]) == list(range(world))
-    assert d["reduce_path"]["ms_per_step"] > 0
+    rp = d["reduce_path"]
+    assert rp["ms_per_step"] > 0
+    # per-phase HIP-event times, the packed SUM's bandwidth, the fp32 all-reduce beside it
+    assert set(rp["phase_ms"]) == {"absmax", "max", "encode", "sum", "decode"}
+    assert all(v >= 0 for v in rp["phase_ms"].values())
+    sp, sf = rp["sum_packed"], rp["sum_fp32_reference"]
+    assert sp["ms"] > 0 and sp["algbw_gbs"] > 0 and sf["ms"] > 0 and sf["bytes_per_rank"] == 4 * 2_000_000
+    assert abs(sp["busbw_gbs"] - 2 * (world - 1) / world * sp["algbw_gbs"]) < 1e-6 * sp["algbw_gbs"]
+    assert rp["sum_fp32_over_packed"] > 0 and rp["wire_bytes_fp32_over_packed"] > 1
     if world >= 4:
         assert d["reduce_path_2x_nodes"]["bit_identical_to_flat"] is True
     ov = d["configs"]["config5_1b_8bit_chunked"]["overlap"]
     assert ov["chunks"] == 8 and len(ov["ms"]["sum_end"]) == 8
     assert all(a <= b for a, b in zip(ov["ms"]["decode_start"], ov["ms"]["decode_end"]))
+    assert len(ov["encode_c1_overlap_sum_c_ms"]) == 7 and all(v >= 0 for v in ov["encode_c1_overlap_sum_c_ms"])
+    assert isinstance(ov["encode_overlaps_previous_sum"], bool)
+    assert all(a <= b for a, b in zip(ov["ms"]["encode_start"], ov["ms"]["encode_end"]))
+
+
+def test_bench_config5_own_lane_width_one_gpu():
+    """Config 5 at its own lane width on one GPU (8-bit, lanes sized for W = 8:
+    12-bit, 2 per word), with per-kernel roofline fractions."""
+    args = ["--numel", "2000000", "--steps", "3", "--warmup", "1", "--settle", "0", "--cpu-seconds", "0",
+            "--legs", "config5", "--n5", "3000000"]
+    r = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    c = _line(r.stdout)["configs"]["config5_1b_8bit_w8_lanes"]
+    assert c["lane_bits"] == 12 and c["lanes_per_word"] == 2 and c["world_lanes"] == 8
+    for k in ("k_qsgd_encode", "k_qsgd_decode"):
+        assert c[k]["us"] > 0 and 0 < c[k]["frac_hbm_peak"] < 1.2

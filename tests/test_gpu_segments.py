@@ -255,3 +255,28 @@ def test_reducer_fresh_grad_out_every_step_pins_nothing():
     gc.collect()
     alive = [i for i, w in enumerate(dead) if w() is not None]
     assert not alive, f"{len(alive)} of {len(dead)} gradient tensors still referenced: {alive[:12]}"
+
+
+def test_segment_cache_rejects_recycled_addresses_of_another_dtype_or_layout():
+    """a cached fp32 segment table keyed by (pointers, sizes) alone
+    would be hit by a half-precision list living at the same addresses with
+    the same element counts (a model cast after the first step), or by a
+    non-contiguous view of the same storage: the kernels would then read and
+    write 4-byte elements through 2-byte tensors.  Such lists must miss the
+    cache and take the TensorBuffer path (no table)."""
+    sizes = [1000, 24, 4096, 7]
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]]).tolist()
+    store = torch.zeros(sum(sizes) + 64, dtype=torch.float32, device=DEV)
+    f32 = [store[s:s + z] for s, z in zip(starts, sizes)]
+    st = store.untyped_storage()
+    f16 = [torch.empty(0, dtype=torch.float16, device=DEV).set_(st, 2 * s, (z,)) for s, z in zip(starts, sizes)]
+    assert [t.data_ptr() for t in f16] == [t.data_ptr() for t in f32]
+    sq = store[:64 * 64].view(64, 64)
+    nc = [sq.t(), store[4096:4096 + 10]]  # the transpose shares the first tensor's pointer and size
+    red = gcodec.QSGDMaxNormReducer(DEV, quantization_level=4, generator=gcodec.Generator(1, "philox"))
+    assert red._segments(f32) is not None
+    assert codec.Segments.key_of(f16) != codec.Segments.key_of(f32)
+    assert red._segments(f16) is None
+    assert red._segments([sq.reshape(-1)[:4096].view(64, 64), store[4096:4106]]) is not None
+    assert red._segments(nc) is None
+    assert red._segments(f32) is not None  # the fp32 table is still served
