@@ -100,6 +100,30 @@ __device__ __forceinline__ G4Cls g4_classes(const uint32_t *w)
     return G4Cls{w15 ^ w7 ^ w4, w7};
 }
 
+// the classes of a thread's 3 blocks from its 24 dwords + the 4 after: each
+// dword's threshold flags computed once (the blocks' 16-byte windows overlap)
+__device__ __forceinline__ void g4_classes3(const uint32_t (&w)[28], G4Cls (&c)[3])
+{
+    uint32_t m4[4] = {0, 0, 0, 0}, m16[4] = {0, 0, 0, 0}, m128[4] = {0, 0, 0, 0};  // bit j: position 32i + j
+#pragma unroll
+    for (int k = 0; k < 28; ++k) {
+        m4[k >> 3] |= byte_flags(w[k], 0xfcfcfcfcu) << (4 * (k & 7));
+        m16[k >> 3] |= byte_flags(w[k], 0xf0f0f0f0u) << (4 * (k & 7));
+        m128[k >> 3] |= byte_flags(w[k], 0x80808080u) << (4 * (k & 7));
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // window ORs by doubling on (block i, block i + 1)
+        const uint64_t ge4 = m4[i] | ((uint64_t)m4[i + 1] << 32), ge16 = m16[i] | ((uint64_t)m16[i + 1] << 32),
+                       ge128 = m128[i] | ((uint64_t)m128[i + 1] << 32);
+        const uint64_t a1 = ge4 | (ge4 >> 1), a2 = a1 | (a1 >> 2), a3 = a2 | (a2 >> 4);
+        const uint64_t b1 = ge16 | (ge16 >> 1), b2 = b1 | (b1 >> 2);
+        const uint64_t c1 = ge128 | (ge128 >> 1);
+        const uint32_t w15 = (uint32_t)(a3 | (a3 >> 7)), w7 = (uint32_t)(b2 | (b2 >> 3)),
+                       w4 = (uint32_t)(c1 | (c1 >> 2));
+        c[i] = G4Cls{w15 ^ w7 ^ w4, w7};
+    }
+}
+
 __device__ __forceinline__ uint32_t g4_mode(const G4Cls &c, uint32_t p)
 {
     return (((c.hi >> p) & 1u) << 1) | ((c.lo >> p) & 1u);
@@ -165,7 +189,7 @@ constexpr uint64_t G1_WS_BYTES = sizeof(G1Hdr) + 2ull * G1_GMAX * 16 * 8 + (GC_G
     } while (0)
 
 struct G1Smem {
-    alignas(16) uint32_t v[G1_TILE_MAX / 4 + 4];  // the tile's values as bytes + 16-byte halo (96 KB)
+    alignas(16) uint32_t v[G1_TILE_MAX / 4 + 6];  // the tile's values as bytes + 16-byte halo (+ 8 bytes the word reads may touch)
     union {
         struct {
             uint32_t pl[G1_WAVES][63][8];         // per wave: the left children of its tree (u16 x 16 a row)
@@ -291,16 +315,21 @@ __device__ __forceinline__ uint32_t g1_load_tile(G1Smem &sm, const int32_t *__re
 //   mode 3 (3 x 8 bits):  one perm.
 __device__ __forceinline__ uint32_t g1_word(const G1Smem &sm, uint32_t a, uint32_t mode, uint32_t pres)
 {
-    const uint32_t *d = &sm.v[a >> 2];
+    // three aligned 8-byte reads cover bytes a .. a + 15 (64 banks for 8-byte
+    // reads: consecutive lanes' words stay conflict-free; 4-byte reads use 32)
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) const volatile u2v lds_u2v;  // whole ds_read_b64s
+    lds_u2v *d = (lds_u2v *)(&sm.v[(a >> 2) & ~1u]);
+    const u2v p0 = d[0], p1 = d[1], p2 = d[2];
+    const bool odd = (a >> 2) & 1u;
     const uint32_t sh = a & 3u;
-    const uint32_t u0 = d[0], u1 = d[1];
+    const uint32_t u0 = odd ? p0.y : p0.x, u1 = odd ? p1.x : p0.y, u2 = odd ? p1.y : p1.x, u3 = odd ? p2.x : p1.y,
+                   u4 = odd ? p2.y : p2.x;
     const uint32_t x0 = __builtin_amdgcn_alignbyte(u1, u0, sh);
     uint32_t code = 0;
     if (pres & 3u) {
-        const uint32_t u2 = d[2];
         const uint32_t x1 = __builtin_amdgcn_alignbyte(u2, u1, sh);
         if (pres & 1u) {
-            const uint32_t u3 = d[3], u4 = d[4];
             const uint32_t x2 = __builtin_amdgcn_alignbyte(u3, u2, sh);
             const uint32_t x3 = __builtin_amdgcn_alignbyte(u4, u3, sh) & 0x00ffffffu;  // b15 is not in the word
             constexpr uint32_t M = 0x40100401u;
@@ -376,18 +405,27 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
         G4Cls cls[G1_BLK];
         uint32_t h[8];
         if (in_tile) {
+            {  // 7 x 16-byte LDS reads (2-way bank conflicts at this 96-byte stride)
+                uint32_t wv[G1_RANGE / 4 + 4];
+#pragma unroll
+                for (uint32_t j = 0; j < G1_RANGE / 4 + 4; j += 4) {  // volatile: kept whole (split into
+                    // ds_read2_b32 pairs they were 8-way conflicts on 32 banks at this stride)
+                    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                    typedef __attribute__((address_space(3))) const volatile u4v lds_u4v;
+                    const u4v r = *(lds_u4v *)(&sm.v[G1_RANGE / 4 * t + j]);
+                    wv[j] = r.x;
+                    wv[j + 1] = r.y;
+                    wv[j + 2] = r.z;
+                    wv[j + 3] = r.w;
+                }
+                g4_classes3(wv, cls);
+            }
             uint32_t fn[15];
 #pragma unroll
             for (uint32_t q = 0; q < 15; ++q)
                 fn[q] = q;
 #pragma unroll
             for (int k = G1_BLK - 1; k >= 0; --k) {  // the blocks back to front, each one's table chained on
-                uint32_t wv[G4_SEG / 4 + 4];
-#pragma unroll
-                for (uint32_t j = 0; j < G4_SEG / 4 + 4; j += 4)
-                    *reinterpret_cast<uint4 *>(&wv[j]) =
-                        *reinterpret_cast<const uint4 *>(&sm.v[G1_RANGE / 4 * t + G4_SEG / 4 * k + j]);
-                cls[k] = g4_classes(wv);
                 uint32_t f[G4_SEG];
                 g4_dp<false>(cls[k], G4_SEG, fn, f);  // n is handled below, for the one thread that holds it
 #pragma unroll
