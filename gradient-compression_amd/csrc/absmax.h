@@ -18,7 +18,11 @@
 // architectural guarantee").  The release / acquire form the model asks for
 // costs a buffer_wbl2 per block (~1.7 us each, same guide) and a buffer_inv in
 // the last block; it measured 2x slower than the memset it removes
-// (include/gcodec.h states the assumption).  Same-address atomics serialise
+// (include/gcodec.h states the assumption).  GC_STRICT_HANDOFF=1 builds that
+// form instead (make strict -> lib/libgcodec_strict.so; plain partial stores,
+// an agent release fence before the ticket, an agent acquire in the last
+// block, plain loads), so the hardware assumption can be switched off;
+// tests/test_gpu_strict_handoff.py checks the two builds agree.  Same-address atomics serialise
 // (~88/us, MI355X_MICROARCH.md 'dequeue'), so launchers cap the grid at
 // kAbsmaxMaxBlocks = 256 tickets.
 #pragma once
@@ -27,6 +31,10 @@
 #include <stdint.h>
 
 #include "gc_device.h"
+
+#ifndef GC_STRICT_HANDOFF
+#define GC_STRICT_HANDOFF 0
+#endif
 
 namespace gc {
 
@@ -68,13 +76,32 @@ __device__ __forceinline__ uint32_t block_max(uint32_t m, uint32_t *part)
     return m;
 }
 
-// max over `count` sc1 partials by the whole block (valid in thread 0)
+// the block partials' hand-off: sc1 stores / loads, or (GC_STRICT_HANDOFF)
+// plain ones ordered by the release / acquire fences around the ticket
+__device__ __forceinline__ void part_store(uint32_t *p, uint32_t v)
+{
+#if GC_STRICT_HANDOFF
+    *p = v;
+#else
+    sc1_store(p, v);
+#endif
+}
+__device__ __forceinline__ uint32_t part_load(const uint32_t *p)
+{
+#if GC_STRICT_HANDOFF
+    return *p;
+#else
+    return sc1_load(p);
+#endif
+}
+
+// max over `count` handed-off partials by the whole block (valid in thread 0)
 template <unsigned BT>
 __device__ __forceinline__ uint32_t block_max_sc1(const uint32_t *p, uint32_t count, uint32_t *part)
 {
     uint32_t v = 0;
     for (uint32_t i = threadIdx.x; i < count; i += BT)
-        v = max(v, sc1_load(&p[i]));
+        v = max(v, part_load(&p[i]));
     return block_max<BT>(v, part);
 }
 
@@ -93,9 +120,18 @@ __device__ __forceinline__ void absmax_finish(uint32_t m, uint32_t *__restrict__
         if (threadIdx.x == 0) {
             // sc1 store, drained, then the agent-scope ticket: the fence-free
             // hand-off of MI355X_MICROARCH.md (row 1 of the sc1 table)
-            sc1_store(&ws[kWsPart + blockIdx.x], m);
+            part_store(&ws[kWsPart + blockIdx.x], m);
+#if GC_STRICT_HANDOFF
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             last = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+#if GC_STRICT_HANDOFF
+            if (last) {  // the acquire, then (barrier below) every wave's plain loads
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+#endif
         }
         __syncthreads();  // the other waves load only after the last add returned
         if (!last)

@@ -43,8 +43,11 @@
 #include <algorithm>
 #include <atomic>
 
+#ifndef GC_STRICT_HANDOFF
+#define GC_STRICT_HANDOFF 0
+#endif
 #ifndef GC_G4_STRICT  // 1: the release/acquire form of the table hand-off (see g1_store_granule)
-#define GC_G4_STRICT 0
+#define GC_G4_STRICT GC_STRICT_HANDOFF
 #endif
 #ifndef GC_G4_STAMPS  // lab builds: per-block phase timestamps of round 0 behind the workspace's granules
 #define GC_G4_STAMPS 0

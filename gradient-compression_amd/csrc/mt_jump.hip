@@ -143,7 +143,8 @@ static_assert((kMtJumpBits - 1) / 4 + kMtJumpThreads - 1 < kMtJumpQuads, "copy l
 constexpr uint64_t kWsPart = kWsWin + kMtN;
 
 __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__restrict__ table, uint32_t *__restrict__ ws,
-                                                           uint32_t jumps, const uint32_t *__restrict__ end_coef)
+                                                           uint32_t jumps, const uint32_t *__restrict__ end_coef,
+                                                           uint32_t nend)
 {
     __shared__ uint4 cp4[4 * kMtJumpQuads];  // copy r: word u = x_{k0 + u + r + 1}
     __shared__ alignas(16) uint32_t pos[kMtJumpBits + 8];  // byte offset of set bit kk in its copy: ((kk&3)*Q + (kk>>2)) * 16
@@ -151,9 +152,10 @@ __global__ __launch_bounds__(kMtJumpThreads) void k_mt_jump(const uint32_t *__re
     uint32_t *cp = reinterpret_cast<uint32_t *>(cp4);
     const uint32_t gi = blockIdx.x / kMtJumpSplit, sp = blockIdx.x % kMtJumpSplit;
     const uint32_t k0 = sp * kMtJumpBits, tid = threadIdx.x;
-    // slot jumps - 1 is the end window when end_coef is given (k_mt_end)
+    // the last nend slots are end windows (k_mt_end): coefficients end_coef[k]
     const uint32_t *__restrict__ coef =
-        (end_coef && gi == jumps - 1 ? end_coef : table + (uint64_t)gi * kMtN) + sp * kMtJumpWords;
+        (gi + nend >= jumps ? end_coef + (uint64_t)(gi + nend - jumps) * kMtN : table + (uint64_t)gi * kMtN) +
+        sp * kMtJumpWords;
     uint32_t c = 0;
     if (tid < kMtJumpWords) {
         c = coef[tid];
@@ -472,6 +474,38 @@ __global__ __launch_bounds__(256) void k_mt_end(uint32_t *__restrict__ ws, uint3
         state[kMtN] = (uint32_t)(ptr0 + count - kMtN * end_block);
 }
 
+// nend end states of one run (gc_mt19937_generate_multi_j): end k is the state
+// after (k + 1) * per_end draws, from the jump slot jumps - nend + k (raw
+// block B_k = floor((idx + (k + 1) per_end - 1) / 624) >= 1, read index
+// idx + (k + 1) per_end - 624 B_k), into ends[k * kMtEndStride ..]; the last
+// one also over the caller's state (the next run chains from it)
+constexpr uint32_t kMtEndStride = kMtN + 2;  // 624 words + read index, 8-byte rows
+__global__ __launch_bounds__(256) void k_mt_end_multi(const uint32_t *__restrict__ ws, uint32_t jumps, uint32_t nend,
+                                                      uint64_t per_end, uint32_t *__restrict__ state,
+                                                      uint32_t *__restrict__ ends)
+{
+    const uint32_t k = blockIdx.x;
+    const uint32_t ptr0 = ws[0];
+    const uint64_t pos = (uint64_t)ptr0 + (k + 1) * per_end;
+    const uint64_t block = (pos - 1) / kMtN;
+    const uint32_t slot = jumps - nend + k;
+    uint32_t *e = ends + (uint64_t)k * kMtEndStride;
+    for (uint32_t i = threadIdx.x; i < kMtN; i += 256) {
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t sp = 0; sp < kMtJumpSplit; ++sp)
+            v ^= ws[kWsPart + ((uint64_t)sp * jumps + slot) * kMtN + i];
+        e[i] = v;
+        if (k == nend - 1)
+            state[i] = v;
+    }
+    if (threadIdx.x == 0) {
+        e[kMtN] = (uint32_t)(pos - kMtN * block);
+        if (k == nend - 1)
+            state[kMtN] = (uint32_t)(pos - kMtN * block);
+    }
+}
+
 }  // namespace gc
 
 using namespace gc;
@@ -515,7 +549,7 @@ static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_
         hipLaunchKernelGGL(k_mt_seq, dim3(1), dim3(256), 0, st, state_dev, ws);
         if (jumps > 0)
             hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)(jumps * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st,
-                               table_dev, ws, jumps, has_end ? end_coef : nullptr);
+                               table_dev, ws, jumps, has_end ? end_coef : nullptr, has_end ? 1u : 0u);
         if (split)
             hipLaunchKernelGGL(k_mt_end, dim3(1), dim3(256), 0, st, ws, jumps, count, end_block, state_dev);
     }
@@ -574,6 +608,46 @@ int gc_mt19937_generate_split24_j(uint32_t *state_dev, const uint32_t *table_dev
     GC_REQUIRE(!out || ((uintptr_t)out & 3u) == 0, "%s: out must be 4-byte aligned", what);
     return mt_run(what, 3, state_dev, table_dev, table_gens, J, out, count, workspace, stream, nullptr, nullptr, 0.0f,
                   phase, true, end_coef, end_block);
+}
+
+size_t gc_mt19937_workspace_size_multi_j(uint64_t count, uint64_t J, uint32_t nend)
+{
+    const uint64_t gens = count && J ? (count + J - 1) / J : 1;
+    return 4 * (kWsPart + kMtJumpSplit * (gens - 1 + nend) * kMtN);
+}
+
+int gc_mt19937_generate_multi_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint32_t *ends_out,
+                                uint32_t *out, void *workspace, int phase, gc_stream_t stream)
+{
+    const char *what = "gc_mt19937_generate_multi_j";
+    GC_REQUIRE(phase >= 1 && phase <= 3, "%s: phase must be 1, 2 or 3", what);
+    GC_REQUIRE(state_dev && workspace && end_coefs && ends_out, "%s: null state / workspace / ends", what);
+    GC_REQUIRE(nend >= 1 && nend <= 64 && per_end >= kMtN, "%s: nend must be 1..64 and per_end >= 624", what);
+    GC_REQUIRE(J > 0 && J % kMtN == 0, "%s: J = %llu is not a positive multiple of 624", what, (unsigned long long)J);
+    const uint64_t count = per_end * nend;
+    GC_REQUIRE(count < (1ull << 40), "%s: count too large", what);
+    GC_REQUIRE(!(phase & 2) || out, "%s: null out", what);
+    const uint64_t gens = (count + J - 1) / J;
+    GC_REQUIRE(gens - 1 <= table_gens && (gens == 1 || table_dev),
+               "%s: jump table holds %llu generators, %llu draws need %llu", what, (unsigned long long)table_gens,
+               (unsigned long long)count, (unsigned long long)(gens - 1));
+    GC_REQUIRE(gens - 1 + nend <= 0x7fffffffull / kMtJumpSplit, "%s: count too large", what);
+    const uint32_t jumps = (uint32_t)(gens - 1 + nend);
+    hipStream_t st = as_stream(stream);
+    uint32_t *ws = reinterpret_cast<uint32_t *>(workspace);
+    if (phase & 1) {
+        hipLaunchKernelGGL(k_mt_seq, dim3(1), dim3(256), 0, st, state_dev, ws);
+        hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)(jumps * kMtJumpSplit)), dim3(kMtJumpThreads), 0, st, table_dev,
+                           ws, jumps, end_coefs, nend);
+        hipLaunchKernelGGL(k_mt_end_multi, dim3(nend), dim3(256), 0, st, ws, jumps, nend, per_end, state_dev,
+                           ends_out);
+    }
+    if (phase & 2)
+        hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
+                           J, count, (void *)out, (uint32_t *)nullptr, (const float *)nullptr, (const float *)nullptr,
+                           0.0f);
+    return launch_status(what);
 }
 
 int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,

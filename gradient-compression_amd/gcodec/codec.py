@@ -937,13 +937,18 @@ _MT_END = {}   # (device index, end block B) -> device coefficients of x^(624 B 
 _MT_WSS = {}   # (device index, slot) -> workspace of the runs in that slot
 _MT_BUSY = {}  # (device index, slot) -> event after the last generators that read the slot's workspace
 _MT_PREV = {}  # device index -> the count of the last mt19937_draws call
+_MT_NSLOT = {}  # device index -> the slot rotation the queued runs were enqueued with
 MT_SPECULATE = True  # generate the draws of the next same-size torch-mode calls ahead (mt19937_draws)
 # how many calls ahead: each speculative run holds 4 * count bytes of draws + one generator workspace
 # on the device until its call; runs start only after two calls in a row of the same count, and never
 # above MT_SPECULATE_MAX_DRAWS
-MT_SPECULATE_DEPTH = 2
-MT_SPECULATE_MAX_DRAWS = 1 << 30
-MT_MAX_SLOTS = 8  # workspace / pinned-state slots of the runs in flight (depth + 2 are used)
+MT_SPECULATE_DEPTH = 4  # calls' draws kept enqueued ahead of the current one
+MT_SPECULATE_MAX_DRAWS = 1 << 30  # per run (a run of MT_MULTI_CALLS calls holds that many times count)
+MT_MAX_SLOTS = 8  # workspace / pinned-state slots of the runs in flight
+# calls per run once a count repeats: one set of generators (and of generator
+# jumps, the LDS-bound part) makes the draws of this many consecutive calls,
+# each call taking its slice and its own end state (gc_mt19937_generate_multi_j)
+MT_MULTI_CALLS = 4
 # generators per pipelined run (mt19937_draws): None = mt_pipe_generators(count).  With the runs
 # made calls ahead, a generator's latency no longer bounds the call; fewer generators cut the
 # jump work, which shares the chip with the encodes
@@ -952,13 +957,14 @@ MT_WAIT_NEXT_JUMPS = False  # consumers also wait for the speculative run's jump
 
 
 def mt_pipe_generators(count: int) -> int:
-    """Generators of one pipelined torch-mode run: about one per 390k draws
-    (256 for 1e8).  Swept on MI355X at 1e8, back to back (tools/time_torch_mode.py):
-    128 generators 0.39-0.43 ms per encode, 192 0.31-0.39, 256 0.31-0.37
-    (profiles/r04d_torch_mode_sweep.log, r04o_torch_mode_32bit.log)."""
+    """Generators of one pipelined torch-mode run: about one per 781k draws
+    (128 for 1e8 draws).  Swept on MI355X at 1e8 per call (tools/time_torch_mode.py,
+    profiles/r05i_torch_mode_sweep.log): 128 generators at 4 calls ahead 0.291 ms
+    per encode back to back and 0.309 ms added to a 2.4 ms backward, against
+    0.314 / 0.340 ms at 256 and 0.349 / 0.359 ms at 64."""
     if MT_PIPE_GENERATORS:
         return int(MT_PIPE_GENERATORS)
-    return max(1, min(MT_MAX_GENERATORS, -(-count // 390_625)))
+    return max(1, min(MT_MAX_GENERATORS, -(-count // 781_250)))
 
 
 def mt_pipe_generator_draws(count: int) -> int:
@@ -1017,11 +1023,12 @@ def _mt_ws_slot(dev, slot: int, count: int, J: int, js) -> torch.Tensor:
 
 
 class _MtRun:
-    """One enqueued generation: its draws, the read index after it, the pinned
-    slot its end state goes to, and events after its jumps (p1), after that
-    state's copy to the host (state_ready) and after its generators (done)."""
+    """One enqueued generation of `calls` calls' draws: its draws, the read
+    index after it, the pinned slot its end states go to, the next call's
+    slice (k), and events after its jumps (p1), after the end states' copy to
+    the host (state_ready) and after its generators (done)."""
 
-    __slots__ = ("count", "packed", "out", "slot", "idx_end", "p1", "state_ready", "done")
+    __slots__ = ("count", "packed", "out", "slot", "idx_end", "p1", "state_ready", "done", "calls", "k", "ends")
 
 
 def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int, packed: bool = False) -> _MtRun:
@@ -1041,6 +1048,7 @@ def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int, packed: bool
     lib = _lib.load()
     run = _MtRun()
     run.count, run.packed, run.slot, run.idx_end = count, packed, slot, idx + count - 624 * block
+    run.calls, run.k, run.ends = 1, 0, None
     with torch.cuda.stream(js):
         if busy is not None:
             js.wait_event(busy)  # that slot's previous generators have read the workspace
@@ -1071,6 +1079,113 @@ def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int, packed: bool
         run.done = torch.cuda.Event()
         run.done.record()
     _MT_BUSY[(dev.index, slot)] = run.done
+    return run
+
+
+_MT_ENDS = {}   # (device index, slot) -> pinned (MT_MULTI_MAX, 626) int32 end states of that slot's run
+_MT_ENDCAT = {}  # (device index, end blocks) -> device (len, 624) coefficient tables of a multi-call run
+MT_MULTI_MAX = 64
+
+
+_MT_END_HOST = {}  # end block -> host coefficients of x^(624 block - 1) mod P (624 uint32)
+
+
+def _mt_end_coefs(dev, blocks: tuple) -> torch.Tensor:
+    """The end coefficient tables of a multi-call run, one per end block,
+    contiguous on the device (cached: a bucket size takes a few tuples).
+    Built on the host and uploaded synchronously, so the table is ready for
+    the side streams whatever the caller's stream is doing (a device-side
+    stack would run on the caller's stream: the table growth test holds that
+    stream busy)."""
+    key = (dev.index, blocks)
+    t = _MT_ENDCAT.get(key)
+    if t is None:
+        if len(_MT_ENDCAT) >= 256:
+            _MT_ENDCAT.clear()
+        host = np.empty((len(blocks), 624), dtype=np.uint32)
+        for i, b in enumerate(blocks):
+            h = _MT_END_HOST.get(b)
+            if h is None:
+                if len(_MT_END_HOST) >= 4096:
+                    _MT_END_HOST.clear()
+                h = _MT_END_HOST[b] = np.empty(624, dtype=np.uint32)
+                check(_lib.load().gc_mt19937_jump_table_j(624 * b, 1, 1, h.ctypes.data_as(C.c_void_p)),
+                      "gc_mt19937_jump_table_j")
+            host[i] = h
+        t = _MT_ENDCAT[key] = torch.from_numpy(host.view(np.int32)).to(dev)  # synchronous: ready on any stream
+    return t
+
+
+_MT_BUDGET = {}  # device index -> bytes the queued draws may hold
+
+
+def _mt_spec_budget(dev) -> int:
+    """Device bytes the speculative draws may hold: 1/32 of the device's memory
+    (9 GB on a 288 GB MI355X; ADVICE r04: the queued runs are invisible to the
+    caller)."""
+    b = _MT_BUDGET.get(dev.index)
+    if b is None:
+        b = _MT_BUDGET[dev.index] = int(torch.cuda.get_device_properties(dev).total_memory) // 32
+    return b
+
+
+def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int) -> _MtRun:
+    """Like _mt_enqueue for `calls` consecutive calls of `count` draws: one
+    generation of calls * count draws, the end state after each call's slice
+    (gc_mt19937_generate_multi_j).  count >= 624."""
+    total = count * calls
+    J = mt_pipe_generator_draws(total)
+    gens = -(-total // J)
+    js, gss = _mt_side(dev)
+    gs = gss[slot]
+    table, tgens = _mt_jump_table(dev, gens - 1, J, stream=js) if gens > 1 else (None, 0)
+    blocks = tuple((idx + (k + 1) * count - 1) // 624 for k in range(calls))
+    ends = _mt_end_coefs(dev, blocks)
+    lib = _lib.load()
+    need = int(lib.gc_mt19937_workspace_size_multi_j(total, J, calls))
+    key = (dev.index, slot)
+    ws = _MT_WSS.get(key)
+    busy = _MT_BUSY.get(key)
+    if ws is None or ws.numel() < need:
+        if busy is not None:
+            busy.synchronize()  # the old buffer may still be read by queued generators
+        _MT_WSS.pop(key, None)
+        with torch.cuda.stream(js):
+            ws = _MT_WSS[key] = torch.empty(need, dtype=torch.uint8, device=dev)
+        ws.record_stream(gs)
+    pin = _MT_ENDS.get(key)
+    if pin is None:
+        pin = _MT_ENDS[key] = torch.empty((MT_MULTI_MAX, 626), dtype=torch.int32).pin_memory()
+    dev_ends = _MT_ENDS.get(("dev",) + key)
+    if dev_ends is None:
+        with torch.cuda.stream(js):
+            dev_ends = _MT_ENDS[("dev",) + key] = torch.empty((MT_MULTI_MAX, 626), dtype=torch.int32, device=dev)
+    run = _MtRun()
+    run.count, run.packed, run.slot, run.calls, run.k = count, False, slot, calls, 0
+    run.idx_end = idx + total - 624 * blocks[-1]
+    with torch.cuda.stream(js):
+        if busy is not None:
+            js.wait_event(busy)  # that slot's previous generators have read the workspace
+        check(lib.gc_mt19937_generate_multi_j(_p(st_dev), _p(table), tgens, J, _p(ends), calls, count, _p(dev_ends),
+                                              None, _p(ws), 1, _stream(dev)), "gc_mt19937_generate_multi_j")
+        run.p1 = torch.cuda.Event()
+        run.p1.record()
+        pin[:calls].copy_(dev_ends[:calls], non_blocking=True)
+        run.state_ready = torch.cuda.Event()
+        run.state_ready.record()
+    run.ends = pin
+    for t in (table, ends):
+        if t is not None:
+            t.record_stream(js)
+            t.record_stream(gs)
+    with torch.cuda.stream(gs):
+        gs.wait_event(run.p1)
+        run.out = torch.empty(total, dtype=torch.int32, device=dev)
+        check(lib.gc_mt19937_generate_multi_j(_p(st_dev), _p(table), tgens, J, _p(ends), calls, count, _p(dev_ends),
+                                              _p(run.out), _p(ws), 2, _stream(dev)), "gc_mt19937_generate_multi_j")
+        run.done = torch.cuda.Event()
+        run.done.record()
+    _MT_BUSY[key] = run.done
     return run
 
 
@@ -1119,9 +1234,18 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     _MT_PREV[d] = count
     last = _MT_LAST.get(d)
     untouched = last is not None and last[1] == idx and np.array_equal(last[0], words)
+    depth = max(0, int(MT_SPECULATE_DEPTH))
+    calls = max(1, min(int(MT_MULTI_CALLS), MT_MULTI_MAX))
+    # slots in rotation: the runs in flight (the current one, those holding the
+    # next `depth` calls) + one; a change of depth or calls drops the queue
+    # (its runs' slots were counted for the old rotation)
+    nslot = min(MT_MAX_SLOTS, -(-depth // calls) + 3)
     queue = _MT_SPEC.pop(d, [])
-    depth = max(0, min(int(MT_SPECULATE_DEPTH), MT_MAX_SLOTS - 2))
-    nslot = depth + 2
+    if _MT_NSLOT.get(d) != nslot:
+        for r in queue:
+            r.done.synchronize()
+        queue = []
+        _MT_NSLOT[d] = nslot
 
     def next_slot():
         k = _MT_SLOT.get(d, 0)
@@ -1133,8 +1257,16 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
             _MT_LAST.pop(d, None)
         return torch.empty(0, dtype=torch.int32, device=device)
     packed = bool(packed24) and mt19937_packable(count, int(idx))
+    multi = not packed and count >= 624  # multi-call runs (gc_mt19937_generate_multi_j)
+
+    def enqueue(st_idx, ncalls):
+        if multi:
+            return _mt_enqueue_multi(device, dst, count, ncalls, st_idx, next_slot())
+        return _mt_enqueue(device, dst, count, st_idx, hout, next_slot(),
+                           packed and mt19937_packable(count, st_idx))
+
     if queue and untouched and queue[0].count == count and queue[0].packed == packed:
-        run = queue.pop(0)
+        run = queue[0]
     else:
         if queue or not untouched:  # dst is not torch's state: send it
             with torch.cuda.stream(js):
@@ -1142,28 +1274,37 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
                 h[:624] = words
                 h[624] = idx
                 dst.copy_(hin, non_blocking=True)
-        queue = []
-        run = _mt_enqueue(device, dst, count, int(idx), hout, next_slot(), packed)
-    if MT_SPECULATE and repeat and count <= MT_SPECULATE_MAX_DRAWS:
-        tail = queue[-1] if queue else run
-        while len(queue) < depth:
-            tail = _mt_enqueue(device, dst, count, tail.idx_end, hout, next_slot(),
-                               packed and mt19937_packable(count, tail.idx_end))
-            queue.append(tail)
-    else:
+        queue = [enqueue(int(idx), 1)]
+        run = queue[0]
+    k = run.k if run.calls > 1 or multi else 0
+    run.k = k + 1
+    if run.k >= run.calls:
+        queue.pop(0)
+    if MT_SPECULATE and repeat and count * calls <= MT_SPECULATE_MAX_DRAWS and \
+            4 * count * (depth + calls) <= _mt_spec_budget(device):
+        ahead = sum(r.calls - r.k for r in queue)
+        while ahead < depth:  # calls' draws enqueued behind this one, chained from the last run's end
+            tail_idx = queue[-1].idx_end if queue else run.idx_end
+            queue.append(enqueue(tail_idx, calls if multi else 1))
+            ahead += queue[-1].calls
+    elif run.k >= run.calls:
         queue = []  # (none were kept: a queue exists only after a repeat)
     cur.wait_event(run.done)
     if queue and MT_WAIT_NEXT_JUMPS:
         cur.wait_event(queue[0].p1)
+    out = run.out[k * count:(k + 1) * count] if run.calls > 1 else run.out
     run.out.record_stream(cur)
     if queue:
         _MT_SPEC[d] = queue
     run.state_ready.synchronize()
-    new = hout[run.slot].numpy().view(np.uint32)
+    if multi:
+        new = run.ends[k].numpy().view(np.uint32)
+    else:
+        new = hout[run.slot].numpy().view(np.uint32)
     w2, i2 = new[:624].copy(), int(new[624])
     set_torch_mt_state(w2, i2)
     _MT_LAST[d] = (w2, i2)
-    return run.out
+    return out
 
 
 def mt_release(device=None):
@@ -1172,6 +1313,10 @@ def mt_release(device=None):
     generator workspaces and the device state buffers.  Called when a
     generator leaves torch mode; the next torch-mode call starts from torch's
     state again."""
+    if device is not None:
+        device = torch.device(device)
+        if device.index is None:  # 'cuda' means the current device (ADVICE r04: was a silent no-op)
+            device = torch.device("cuda", torch.cuda.current_device())
     keys = [device.index] if device is not None else sorted({k for k in _MT_SPEC} | {k[0] for k in _MT_WSS}
                                                                | set(_MT_PIN) | set(_MT_LAST))
     for d in keys:
@@ -1184,6 +1329,9 @@ def mt_release(device=None):
         _MT_PIN.pop(d, None)
         _MT_LAST.pop(d, None)
         _MT_PREV.pop(d, None)
+        _MT_NSLOT.pop(d, None)
+        for k in [k for k in _MT_ENDS if k[-2] == d]:
+            del _MT_ENDS[k]
 
 
 # ---------------------------------------------------------------------------

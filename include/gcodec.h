@@ -390,6 +390,21 @@ int gc_mt19937_generate_phase_j(uint32_t *state_dev, const uint32_t *table_dev, 
 int gc_mt19937_generate_split_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
                                 const uint32_t *end_coef, uint64_t end_block, uint32_t *out, uint64_t count,
                                 void *workspace, int phase, gc_stream_t stream);
+/* One run of nend * per_end draws with nend end states (several same-size
+ * calls' draws made by one set of generators: the generator jumps, the
+ * LDS-bound part, are shared by the nend calls).  End k = the state after
+ * (k + 1) * per_end draws (624 words + read index) goes to
+ * ends_out[k * 626 ..]; the last one also over state_dev, so the next run
+ * chains from it.  end_coefs (device): nend tables of 624 words, table k =
+ * gc_mt19937_jump_table_j(624 * B_k, 1, 1) with B_k = floor((idx + (k + 1) *
+ * per_end - 1) / 624), idx = the state's read index (per_end >= 624).
+ * workspace: gc_mt19937_workspace_size_multi_j(nend * per_end, J, nend).
+ * Phases as gc_mt19937_generate_split_j (1: sequence, jumps, end states; 2:
+ * the generators). */
+size_t gc_mt19937_workspace_size_multi_j(uint64_t count, uint64_t J, uint32_t nend);
+int gc_mt19937_generate_multi_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint32_t *ends_out,
+                                uint32_t *out, void *workspace, int phase, gc_stream_t stream);
 /* gc_mt19937_generate_split_j with the draws packed to 24 bits (the
  * GC_RNG_STREAM24 layout: 3 count / 4 words of out).  idx = the state's read
  * index (state_dev[624], which the caller sent); idx and count must be

@@ -32,7 +32,24 @@ GS = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 96, 
 DS = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 3]
 
 
+CADENCE = os.environ.get("CADENCE", "0") == "1"  # each call behind ~2.4 ms of bf16 GEMMs (a backward)
+if CADENCE:
+    _a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    _c = torch.empty_like(_a)
+
+
+def backward():
+    for _ in range(3):
+        torch.mm(_a, _a, out=_c)
+
+
 def per_call(fn):
+    if CADENCE:  # the time a call adds to a backward
+        return _per_call(lambda: (backward(), fn())) - _per_call(backward)
+    return _per_call(fn)
+
+
+def _per_call(fn):
     for _ in range(6):
         fn()
     torch.cuda.synchronize()
@@ -68,14 +85,20 @@ if os.environ.get("AB") == "1":  # interleaved A/B of the packed and plain draws
                   f"{per_call(step):.3f} ms per call", flush=True)
     sys.exit(0)
 
+MS = [int(v) for v in os.environ.get("MULTI", str(codec.MT_MULTI_CALLS)).split(",")]
 for G in GS:
     for D in DS:
-        codec.MT_PIPE_GENERATORS = G or None
-        codec.MT_SPECULATE_DEPTH = D
-        codec.mt_release()
-        e, s = per_call(enc), per_call(step)
-        print(f"generators {G or codec.mt_pipe_generators(n)} depth {D}: encode {e:.3f} ms, absmax + encode "
-              f"{s:.3f} ms per call", flush=True)
+        for M in MS:
+            codec.MT_PIPE_GENERATORS = G or None
+            codec.MT_SPECULATE_DEPTH = D
+            codec.MT_MULTI_CALLS = M
+            codec.mt_release()
+            e, s = per_call(enc), per_call(step)
+            print(f"generators {G or codec.mt_pipe_generators(n * M)} depth {D} calls/run {M}"
+                  f"{' cadence' if CADENCE else ''}{' packed24' if PACKED else ''}: encode {e:.3f} ms, "
+                  f"absmax + encode {s:.3f} ms per call", flush=True)
+if os.environ.get("SWEEP_ONLY") == "1":
+    sys.exit(0)
 codec.MT_PIPE_GENERATORS, codec.MT_SPECULATE_DEPTH = None, 2
 codec.mt_release()
 pe = per_call(lambda: codec.qsgd_encode(x, nm, 4, px.reserve(n), 1, out=words, lanes=lanes))
