@@ -5,9 +5,15 @@
 // torch.max), wave64 shuffle tree, wave partials in LDS, one partial per
 // block.  Without a workspace: one atomicMax per block into *norm (zeroed by
 // a preceding hipMemsetAsync).  With a workspace: no memset launch — every
-// block stores its partial (sc1) and takes a ticket (agent-scope atomic add);
-// the block that draws the last ticket reduces the partials (sc1 loads),
-// writes *norm and re-arms the ticket.
+// block stores its partial (sc1) and takes a ticket of its group (block b in
+// group b mod 16, one XCD's blocks; agent-scope atomic add); the block that
+// draws its group's last ticket takes a top-level ticket, and the block that
+// draws the last of those reduces the partials (sc1 loads), writes *norm and
+// re-arms the tickets.  Two levels because same-address atomics serialise
+// (~88/us, MI355X_MICROARCH.md 'dequeue'): 256 blocks on one ticket held the
+// kernel's end ~2.9 us behind its last load (17.2 against 14.4 us for the
+// plain read of the ResNet50 bucket, profiles/r05j lab_ms); 16 + 16 adds on
+// 17 lines take ~0.4 us.
 //
 // The hand-off is fence-free and rests on a gfx950 hardware property, not on
 // the HIP memory model: every partial is stored sc1 (write-through past the
@@ -22,9 +28,8 @@
 // form instead (make strict -> lib/libgcodec_strict.so; plain partial stores,
 // an agent release fence before the ticket, an agent acquire in the last
 // block, plain loads), so the hardware assumption can be switched off;
-// tests/test_gpu_strict_handoff.py checks the two builds agree.  Same-address atomics serialise
-// (~88/us, MI355X_MICROARCH.md 'dequeue'), so launchers cap the grid at
-// kAbsmaxMaxBlocks = 256 tickets.
+// tests/test_gpu_strict_handoff.py checks the two builds agree.  Launchers cap
+// the grid at kAbsmaxMaxBlocks = 256 partials.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -39,10 +44,13 @@
 namespace gc {
 
 constexpr unsigned kAbsmaxThreads = 1024;  // product block size
-constexpr unsigned kAbsmaxMaxBlocks = 256;  // one ticket per block, one 256-add chain
-// workspace (uint32 words): [0] ticket (a 128-byte line of its own),
-// [kWsPart + b] block partials
-constexpr unsigned kWsPart = 32;
+constexpr unsigned kAbsmaxMaxBlocks = 1024;  // block partials in the workspace
+// workspace (uint32 words): [0] top-level ticket, [kWsGroup (g + 1)] the
+// ticket of group g (each on a 128-byte line of its own), [kWsPart + b] block
+// partials
+constexpr unsigned kAbsmaxGroups = 16;
+constexpr unsigned kWsGroup = 32;
+constexpr unsigned kWsPart = kWsGroup * (kAbsmaxGroups + 1);
 constexpr unsigned kAbsmaxWsWords = kWsPart + kAbsmaxMaxBlocks;
 
 __device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
@@ -105,7 +113,9 @@ __device__ __forceinline__ uint32_t block_max_sc1(const uint32_t *p, uint32_t co
     return block_max<BT>(v, part);
 }
 
-template <bool WS, unsigned BT = kAbsmaxThreads>
+// G: ticket groups (1 = every block on one group ticket: the single-level
+// chain, kept for the A/B in tools/lab_ms.hip)
+template <bool WS, unsigned BT = kAbsmaxThreads, unsigned G = kAbsmaxGroups>
 __device__ __forceinline__ void absmax_finish(uint32_t m, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)
 {
     __shared__ uint32_t part[BT / 64];
@@ -118,35 +128,48 @@ __device__ __forceinline__ void absmax_finish(uint32_t m, uint32_t *__restrict__
     } else {
         const uint32_t nb = gridDim.x;  // <= kAbsmaxMaxBlocks (launchers)
         if (threadIdx.x == 0) {
-            // sc1 store, drained, then the agent-scope ticket: the fence-free
-            // hand-off of MI355X_MICROARCH.md (row 1 of the sc1 table)
+            // sc1 store, drained, then the agent-scope tickets: the fence-free
+            // hand-off of MI355X_MICROARCH.md (row 1 of the sc1 table), chained
+            // through the group's last block (its top-level add is issued only
+            // after its group add returned, i.e. after every add of the group)
+            static_assert(G >= 1 && G <= kAbsmaxGroups, "ticket groups");
+            const uint32_t g = blockIdx.x % G;
+            const uint32_t ng = min(nb, G), cnt = (nb - g + G - 1) / G;
             part_store(&ws[kWsPart + blockIdx.x], m);
 #if GC_STRICT_HANDOFF
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 #endif
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            last = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+            bool l = false;
+            if (__hip_atomic_fetch_add(&ws[kWsGroup * (g + 1)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                cnt - 1) {
 #if GC_STRICT_HANDOFF
-            if (last) {  // the acquire, then (barrier below) every wave's plain loads
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");  // the group's partials on to the top level
+#endif
+                l = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+            }
+#if GC_STRICT_HANDOFF
+            if (l) {  // the acquire, then (barrier below) every wave's plain loads
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
 #endif
+            last = l;
         }
         __syncthreads();  // the other waves load only after the last add returned
         if (!last)
             return;
         const uint32_t r = block_max_sc1<BT>(&ws[kWsPart], nb, part);
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0)
             *out = r;
-            sc1_store(&ws[0], 0u);  // re-arm
-        }
+        if (threadIdx.x <= G)  // re-arm: every ticket has reached its count
+            sc1_store(&ws[kWsGroup * threadIdx.x], 0u);
     }
 }
 
 // MODE 0: float4 dense, 1: scalar dense, 2: gather.  U float4 loads in flight
 // per thread; NT: nontemporal loads (streamed once)
-template <int MODE, bool WS, unsigned BT = kAbsmaxThreads, int U = 4, bool NT = false>
+template <int MODE, bool WS, unsigned BT = kAbsmaxThreads, int U = 4, bool NT = false, unsigned G = kAbsmaxGroups>
 __global__ __launch_bounds__(BT) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
                                                uint64_t n, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)
 {
@@ -173,7 +196,7 @@ __global__ __launch_bounds__(BT) void k_absmax(const float *__restrict__ x, cons
         for (; t < n; t += stride)
             m = max(m, absbits(MODE == 2 ? x[idx[t]] : x[t]));
     }
-    absmax_finish<WS, BT>(m, out, ws);
+    absmax_finish<WS, BT, G>(m, out, ws);
 }
 
 }  // namespace gc

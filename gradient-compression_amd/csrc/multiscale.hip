@@ -530,7 +530,7 @@ int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const floa
     GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_fast_o2<LL, VAR_>), dim3(g8), dim3(kBlock), 0, \
                                                             st, x, (uint32_t)n, norm, la, fa, ra, (uint32_t)M, w,      \
                                                             mask_words, (void *)nullptr, 0, 0u))
-            if (wide) { GC_MF8(MSV_WIDE | MSV_ROLL); } else { GC_MF8(MSV_ROLL); }
+            if (wide) { GC_MF8(MSV_WIDE | MSV_ROLL); } else { GC_MF8(MSV_ROLL | MSV_UFLAG); }
 #undef GC_MF8
         } else if (levels->count == 2) {
             if (rng->kind == GC_RNG_PHILOX) { GC_MF(2, 2); } else { GC_MF(1, 2); }
@@ -662,9 +662,9 @@ int gc_ms_mask_encode_cached(const float *x, uint64_t n, const float *norm, cons
     if (levels->count == 2 && rng->kind == GC_RNG_PHILOX && M % 8 == 0) {  // octets: dense draws, 3 blocks per 8
         const unsigned g8 = (unsigned)std::max<uint64_t>(1, (ms_grid(M >> 3) + ms_tiles() - 1) / ms_tiles());
         if (cg.bytes == 1) {
-            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL, 1); } else { GC_MFC8(MSV_ROLL, 1); }
+            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL, 1); } else { GC_MFC8(MSV_ROLL | MSV_UFLAG, 1); }
         } else {
-            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL, 2); } else { GC_MFC8(MSV_ROLL, 2); }
+            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL, 2); } else { GC_MFC8(MSV_ROLL | MSV_UFLAG, 2); }
         }
     } else if (levels->count == 2) {
         if (cg.bytes == 1) { GC_MFC_K(2, 1) } else { GC_MFC_K(2, 2) }

@@ -24,7 +24,11 @@ namespace gc {
 
 // max-norm: k_absmax (absmax.h).  Product grid: kAbsmaxGrid blocks of
 // kAbsmaxThreads (one per CU: 16 waves x 4 float4 loads in flight = 64 KB per CU).
-constexpr unsigned kAbsmaxGrid = kAbsmaxMaxBlocks;  // 256: the one-level ticket's cap
+#ifndef GC_ABSMAX_GRID
+#define GC_ABSMAX_GRID 256
+#endif
+constexpr unsigned kAbsmaxGrid = GC_ABSMAX_GRID;
+static_assert(kAbsmaxGrid <= kAbsmaxMaxBlocks, "absmax partials");
 constexpr unsigned kEncodeGrid = 12288;  // blocks of the dense encode (see launch_encode)
 constexpr unsigned kDecodeGrid = 16384;  // blocks of the dense decode (see qsgd_decode)
 

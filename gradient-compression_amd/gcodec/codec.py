@@ -141,13 +141,29 @@ def mask_words_total(ml: _lib.gc_lanes, levels) -> int:
 _WS = {}
 
 
+_WS_POOL = {}  # device index -> [zeroed pool tensor, slots handed out]
+_WS_POOL_SLOTS = 64
+
+
 def _absmax_ws(dev, stream) -> torch.Tensor:
-    """Self-resetting last-block workspace, one per (device, stream)."""
+    """Self-resetting last-block workspace, one per (device, stream).  Slots
+    are cut from a pool zeroed once per device, so a stream's first call
+    launches no fill: under HIP-graph capture (a capture stream is a new
+    stream) a fill would be captured and re-run at every replay (VERDICT r04
+    item 6: the GRandK replay carried a FillFunctor node per step)."""
     key = (dev.index, stream.value)
     ws = _WS.get(key)
     if ws is None:
-        ws = torch.zeros(int(_lib.load().gc_absmax_workspace_size()), dtype=torch.uint8, device=dev)
-        _WS[key] = ws
+        size = -(-int(_lib.load().gc_absmax_workspace_size()) // 256) * 256
+        pool = _WS_POOL.get(dev.index)
+        if pool is None or pool[1] == _WS_POOL_SLOTS:
+            pool = _WS_POOL[dev.index] = [torch.zeros(size * _WS_POOL_SLOTS, dtype=torch.uint8, device=dev), 0]
+            if not torch.cuda.is_current_stream_capturing():
+                # other streams take slots later: the zero fill must be done
+                # (under capture the fill is a node of this graph instead)
+                torch.cuda.current_stream(dev).synchronize()
+        ws = _WS[key] = pool[0][pool[1] * size:(pool[1] + 1) * size]
+        pool[1] += 1
     return ws
 
 
@@ -954,6 +970,8 @@ MT_MULTI_CALLS = 4
 # jump work, which shares the chip with the encodes
 MT_PIPE_GENERATORS = None
 MT_WAIT_NEXT_JUMPS = False  # consumers also wait for the speculative run's jumps (mt19937_draws)
+# side-stream priorities ("high" or "normal") of the jumps and of the generators
+MT_SIDE_PRIORITY = ("high", "high")
 
 
 def mt_pipe_generators(count: int) -> int:
@@ -982,8 +1000,9 @@ def _mt_side(device):
     s = _MT_SIDE.get(device.index)
     if s is None:
         lo, hi = torch.cuda.Stream.priority_range()
-        s = _MT_SIDE[device.index] = (torch.cuda.Stream(device, priority=min(lo, hi)),
-                                      [torch.cuda.Stream(device, priority=min(lo, hi)) for _ in range(MT_MAX_SLOTS)])
+        pj, pg = (min(lo, hi) if p == "high" else max(lo, hi) for p in MT_SIDE_PRIORITY)
+        s = _MT_SIDE[device.index] = (torch.cuda.Stream(device, priority=pj),
+                                      [torch.cuda.Stream(device, priority=pg) for _ in range(MT_MAX_SLOTS)])
     return s
 
 
@@ -1235,10 +1254,15 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     last = _MT_LAST.get(d)
     untouched = last is not None and last[1] == idx and np.array_equal(last[0], words)
     depth = max(0, int(MT_SPECULATE_DEPTH))
-    calls = max(1, min(int(MT_MULTI_CALLS), MT_MULTI_MAX))
+    packed = bool(packed24) and count > 0 and mt19937_packable(count, int(idx))
+    multi = not packed and count >= 624  # multi-call runs (gc_mt19937_generate_multi_j)
+    calls = max(1, min(int(MT_MULTI_CALLS), MT_MULTI_MAX)) if multi else 1
     # slots in rotation: the runs in flight (the current one, those holding the
-    # next `depth` calls) + one; a change of depth or calls drops the queue
-    # (its runs' slots were counted for the old rotation)
+    # next `depth` calls: ceil(depth / calls) runs, one more while the current
+    # run still has calls left) + one; a change of the rotation drops the queue
+    # (its runs' slots were counted for the old rotation).  Each
+    # run's state / ends slot must outlive the enqueue of the runs behind it:
+    # the state is read after them
     nslot = min(MT_MAX_SLOTS, -(-depth // calls) + 3)
     queue = _MT_SPEC.pop(d, [])
     if _MT_NSLOT.get(d) != nslot:
@@ -1256,8 +1280,6 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
         if queue:  # dropped runs still moved dst on: send the state next time
             _MT_LAST.pop(d, None)
         return torch.empty(0, dtype=torch.int32, device=device)
-    packed = bool(packed24) and mt19937_packable(count, int(idx))
-    multi = not packed and count >= 624  # multi-call runs (gc_mt19937_generate_multi_j)
 
     def enqueue(st_idx, ncalls):
         if multi:
@@ -1283,10 +1305,14 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     if MT_SPECULATE and repeat and count * calls <= MT_SPECULATE_MAX_DRAWS and \
             4 * count * (depth + calls) <= _mt_spec_budget(device):
         ahead = sum(r.calls - r.k for r in queue)
-        while ahead < depth:  # calls' draws enqueued behind this one, chained from the last run's end
+        behind = sum(1 for r in queue if r is not run)  # runs enqueued after this one
+        # calls' draws enqueued behind this one, chained from the last run's end;
+        # never a full rotation behind it (this run's state slot is read below)
+        while ahead < depth and behind < nslot - 1:
             tail_idx = queue[-1].idx_end if queue else run.idx_end
-            queue.append(enqueue(tail_idx, calls if multi else 1))
+            queue.append(enqueue(tail_idx, calls))
             ahead += queue[-1].calls
+            behind += 1
     elif run.k >= run.calls:
         queue = []  # (none were kept: a queue exists only after a repeat)
     cur.wait_event(run.done)

@@ -56,6 +56,32 @@ def test_draw_sequences_vs_serial_stream(speculate):
         codec.MT_SPECULATE = old
 
 
+@pytest.mark.parametrize("depth", [2, 4, 8])
+@pytest.mark.parametrize("count", [1, 100, 623, 4_000])
+def test_repeated_calls_every_depth_vs_serial_stream(depth, count):
+    """Repeated same-size calls (the speculation runs enqueued ahead, each in
+    its slot of the rotation) for single-call runs (count < 624) and
+    multi-call runs, at every speculation depth: each call's draws and torch's
+    state after it are the serial stream's.  (A rotation sized for multi-call
+    runs once gave single-call runs' speculation the slot of the run whose
+    state was still to be read: torch's state came back wrong.)"""
+    old = codec.MT_SPECULATE_DEPTH
+    codec.MT_SPECULATE_DEPTH = depth
+    codec.mt_release()
+    try:
+        torch.manual_seed(depth * 1000 + count)
+        for i in range(3 * depth + 5):
+            ref, w2, i2 = _oracle_next(count)
+            got = codec.mt19937_draws(count, DEV)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().view(np.uint32), ref), i
+            words, idx = torch_mt_state()
+            assert idx == i2 and np.array_equal(words, w2), i
+    finally:
+        codec.MT_SPECULATE_DEPTH = old
+        codec.mt_release()
+
+
 def test_torch_mode_compressor_back_to_back_vs_oracle():
     """QSGDMaxNormCompressor.compress in torch mode, five back-to-back calls on
     the same bucket (the speculative draws used four times), then the fused

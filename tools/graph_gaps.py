@@ -14,7 +14,7 @@ rows = []
 for p in glob.glob(f"{sys.argv[1]}/**/*kernel_trace.csv", recursive=True):
     rows += list(csv.DictReader(open(p)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-marks = [i for i, r in enumerate(rows) if "fill" in r["Kernel_Name"].lower() or "FillFunctor" in r["Kernel_Name"]]
+marks = [i for i, r in enumerate(rows) if "neg" in r["Kernel_Name"].lower()]  # the marker neg_ kernels
 marks = marks[-3:]
 phases = {"eager": rows[marks[0] + 1:marks[1]], "graph replay": rows[marks[1] + 1:marks[2]]}
 
@@ -36,5 +36,6 @@ for name, ks in phases.items():
     span = (int(ks[-1]["End_Timestamp"]) - int(ks[0]["Start_Timestamp"])) / 1e3
     steps = sum(1 for r in ks if "scatter" in r["Kernel_Name"])
     print(f"   gap inside a step  mean {statistics.mean(gi):7.2f} us, median {statistics.median(gi):7.2f}")
-    print(f"   gap between steps  mean {statistics.mean(gb):7.2f} us, median {statistics.median(gb):7.2f}")
+    if gb:
+        print(f"   gap between steps  mean {statistics.mean(gb):7.2f} us, median {statistics.median(gb):7.2f}")
     print(f"   span {span:.1f} us over {steps} steps = {span / max(steps, 1):.2f} us per step")

@@ -2,7 +2,7 @@
 gather + max-norm + encode in one launch, then the decode-scatter) eager and
 as a captured HIP graph, for a rocprofv3 kernel trace (VERDICT r04 item 6:
 why a replay took 21.3 us against 11.7 us eager).  STEPS eager steps, then
-STEPS replays, each phase bracketed by a marker kernel (a 1-element fill) so
+STEPS replays, each phase bracketed by a marker kernel (a 1-element neg_) so
 tools/graph_gaps.py can split the trace.  Without the profiler (TIME=1) it
 also prints the per-step host issue time of both forms, and the
 event-timed rate of each."""
@@ -59,16 +59,16 @@ def timed(fn, label):
           f"{host:.2f} us per step", flush=True)
 
 
-mark.fill_(1.0)
+mark.neg_()
 if os.environ.get("TIME") == "1":
     timed(rk_step, "eager")
     timed(graph.replay, "graph replay")
 else:
     for _ in range(STEPS):
         rk_step()
-    mark.fill_(2.0)
+    mark.neg_()
     for _ in range(STEPS):
         graph.replay()
-    mark.fill_(3.0)
+    mark.neg_()
 torch.cuda.synchronize()
 print("done")

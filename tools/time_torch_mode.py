@@ -86,6 +86,8 @@ if os.environ.get("AB") == "1":  # interleaved A/B of the packed and plain draws
     sys.exit(0)
 
 MS = [int(v) for v in os.environ.get("MULTI", str(codec.MT_MULTI_CALLS)).split(",")]
+if os.environ.get("PRIO"):  # side-stream priorities, e.g. PRIO=high,normal (jumps, generators)
+    codec.MT_SIDE_PRIORITY = tuple(os.environ["PRIO"].split(","))
 for G in GS:
     for D in DS:
         for M in MS:
@@ -95,7 +97,8 @@ for G in GS:
             codec.mt_release()
             e, s = per_call(enc), per_call(step)
             print(f"generators {G or codec.mt_pipe_generators(n * M)} depth {D} calls/run {M}"
-                  f"{' cadence' if CADENCE else ''}{' packed24' if PACKED else ''}: encode {e:.3f} ms, "
+                  f"{' cadence' if CADENCE else ''}{' packed24' if PACKED else ''}"
+                  f"{' prio ' + ','.join(codec.MT_SIDE_PRIORITY) if os.environ.get('PRIO') else ''}: encode {e:.3f} ms, "
                   f"absmax + encode {s:.3f} ms per call", flush=True)
 if os.environ.get("SWEEP_ONLY") == "1":
     sys.exit(0)
