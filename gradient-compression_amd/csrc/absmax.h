@@ -29,7 +29,7 @@
 // an agent release fence before the ticket, an agent acquire in the last
 // block, plain loads), so the hardware assumption can be switched off;
 // tests/test_gpu_strict_handoff.py checks the two builds agree.  Launchers cap
-// the grid at kAbsmaxMaxBlocks = 256 partials.
+// the grid at kAbsmaxMaxBlocks = 1024 partials.
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -1791,4 +1791,51 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode_fast(const uint32_t *__res
     }
 }
 
+// the same with Q adjacent word quads per lane (Q x 16-byte word loads, Q
+// float4 stores per plane in flight per lane; Mq % (4 Q) == 0)
+template <int LQ, int ORDER, int NL, int Q>
+__global__ __launch_bounds__(kBlock) void k_ms_decode_fast_oq(const uint32_t *__restrict__ words, MaskArg mk,
+                                                              FastDiv fd, uint32_t n, const float *__restrict__ normp,
+                                                              LevelsArg lv, MsFastArg fa, uint32_t Mq, uint32_t wq,
+                                                              int32_t sub, float alpha, float *__restrict__ out)
+{
+    const float norm = *normp;
+    float c[GC_MAX_LEVELS] = {};
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+        c[l] = ORDER == 1 ? norm / lv.s[l] : 0.0f;
+    const bool mk0 = norm >= 0x1p-100f && norm <= 0x1p100f;
+    const uint32_t msk = (1u << wq) - 1u;
+    const uint32_t units = Mq / (4u * Q);
+    constexpr int PW = (LQ + 3) / 4;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < units; tb += gridDim.x * kMsQuadsPerBlock) {
+        const uint32_t t = tb + lane;
+        if (t >= units)
+            continue;
+        uint4 wd[Q];
+#pragma unroll
+        for (int h = 0; h < Q; ++h)
+            wd[h] = *reinterpret_cast<const uint4 *>(words + 4u * Q * t + 4u * h);
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const uint32_t p = wave + 4u * j;
+            if (p >= (uint32_t)LQ)
+                break;
+            const uint32_t i0 = p * Mq + 4u * Q * t;
+            if (i0 >= n)
+                break;
+            uint4 m[Q];
+#pragma unroll
+            for (int h = 0; h < Q; ++h)
+                m[h] = mask_levels4_fast<NL>(mk, fd, i0 + 4u * h);
+#pragma unroll
+            for (int h = 0; h < Q; ++h)
+                if (h == 0 || i0 + 4u * h < n)
+                    decode_plane<ORDER, NL>(wd[h], p * wq, msk, sub, m[h], norm, lv, fa, c, mk0, alpha, out,
+                                            i0 + 4u * h, n);
+        }
+    }
+}
+
 }  // namespace gc

@@ -23,9 +23,12 @@
 namespace gc {
 
 // max-norm: k_absmax (absmax.h).  Product grid: kAbsmaxGrid blocks of
-// kAbsmaxThreads (one per CU: 16 waves x 4 float4 loads in flight = 64 KB per CU).
+// kAbsmaxThreads (two per CU: 32 waves x 4 float4 loads in flight = 128 KB
+// per CU).  On the ResNet50 bucket: 256 / 512 / 1024 blocks 16.4 / 15.7 /
+// 17.9 us, with the two-level tickets (one level, 256 blocks: 17.1 us;
+// profiles/r05m_lab_ms.log)
 #ifndef GC_ABSMAX_GRID
-#define GC_ABSMAX_GRID 256
+#define GC_ABSMAX_GRID 512
 #endif
 constexpr unsigned kAbsmaxGrid = GC_ABSMAX_GRID;
 static_assert(kAbsmaxGrid <= kAbsmaxMaxBlocks, "absmax partials");

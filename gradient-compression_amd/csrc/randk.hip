@@ -32,7 +32,7 @@ namespace gc {
 constexpr unsigned kRkThreads = 1024;
 constexpr uint64_t kRkFusedMax = 16384;  // K of the fused path: uint16 lanes in 32 KB of LDS
 constexpr uint32_t kRkFusedMaxBits = 15; // lane values 0 .. 2 (2^b - 1) fit 16 bits
-constexpr unsigned kRkMaxBlocks = kAbsmaxMaxBlocks;  // one-level ticket (absmax.h)
+constexpr unsigned kRkMaxBlocks = 256;  // one-level ticket chain (~88 same-address adds per us)
 
 // SEG: x is the reference's TensorBuffer as a gc_segments table (the gather
 // reads each index's element straight from its per-parameter tensor: no

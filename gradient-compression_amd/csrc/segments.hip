@@ -255,7 +255,7 @@ int gc_segments_flatten_absmax(const gc_segments *segs, float *flat, float *norm
         if (n == 0)
             return GC_OK;
     }
-    const unsigned grid = (unsigned)std::min<uint64_t>((n + kRange - 1) / kRange, kAbsmaxMaxBlocks);
+    const unsigned grid = (unsigned)std::min<uint64_t>((n + kRange - 1) / kRange, 256);  // one per CU
 #define GC_SF(WS_, ST_) \
     hipLaunchKernelGGL((k_seg_flatten_absmax<WS_, ST_>), dim3(grid), dim3(kAbsmaxThreads), 0, st, sg, n, flat, o, ws)
     if (ws) {

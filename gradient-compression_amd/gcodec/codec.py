@@ -958,13 +958,13 @@ MT_SPECULATE = True  # generate the draws of the next same-size torch-mode calls
 # how many calls ahead: each speculative run holds 4 * count bytes of draws + one generator workspace
 # on the device until its call; runs start only after two calls in a row of the same count, and never
 # above MT_SPECULATE_MAX_DRAWS
-MT_SPECULATE_DEPTH = 4  # calls' draws kept enqueued ahead of the current one
+MT_SPECULATE_DEPTH = 16  # calls' draws kept enqueued ahead of the current one
 MT_SPECULATE_MAX_DRAWS = 1 << 30  # per run (a run of MT_MULTI_CALLS calls holds that many times count)
 MT_MAX_SLOTS = 8  # workspace / pinned-state slots of the runs in flight
 # calls per run once a count repeats: one set of generators (and of generator
 # jumps, the LDS-bound part) makes the draws of this many consecutive calls,
 # each call taking its slice and its own end state (gc_mt19937_generate_multi_j)
-MT_MULTI_CALLS = 4
+MT_MULTI_CALLS = 8
 # generators per pipelined run (mt19937_draws): None = mt_pipe_generators(count).  With the runs
 # made calls ahead, a generator's latency no longer bounds the call; fewer generators cut the
 # jump work, which shares the chip with the encodes
@@ -974,20 +974,22 @@ MT_WAIT_NEXT_JUMPS = False  # consumers also wait for the speculative run's jump
 MT_SIDE_PRIORITY = ("high", "high")
 
 
-def mt_pipe_generators(count: int) -> int:
-    """Generators of one pipelined torch-mode run: about one per 781k draws
-    (128 for 1e8 draws).  Swept on MI355X at 1e8 per call (tools/time_torch_mode.py,
-    profiles/r05i_torch_mode_sweep.log): 128 generators at 4 calls ahead 0.291 ms
-    per encode back to back and 0.309 ms added to a 2.4 ms backward, against
-    0.314 / 0.340 ms at 256 and 0.349 / 0.359 ms at 64."""
+def mt_pipe_generators(count: int, multi: bool = False) -> int:
+    """Generators of one pipelined torch-mode run of `count` draws.  A
+    single-call run: about one per 781k draws (128 for 1e8 draws; swept at
+    1e8 per call, profiles/r05i_torch_mode_sweep.log: 0.291 ms per encode back
+    to back against 0.314 ms at 256 and 0.349 ms at 64).  A multi-call run
+    (MT_MULTI_CALLS calls, gc_mt19937_generate_multi_j): one per 1.56M draws
+    (512 for 8 calls of 1e8; profiles/r05j/r05k/r05m_torch_mode_*.log: 512 and
+    1024 within noise, 16 calls per run over the speculation budget)."""
     if MT_PIPE_GENERATORS:
         return int(MT_PIPE_GENERATORS)
-    return max(1, min(MT_MAX_GENERATORS, -(-count // 781_250)))
+    return max(1, min(MT_MAX_GENERATORS, -(-count // (1_562_500 if multi else 781_250))))
 
 
-def mt_pipe_generator_draws(count: int) -> int:
+def mt_pipe_generator_draws(count: int, multi: bool = False) -> int:
     """Draws per generator J (a multiple of 624) of a pipelined run."""
-    g = mt_pipe_generators(count)
+    g = mt_pipe_generators(count, multi)
     return 624 * max(1, -(-count // (624 * g)))
 
 
@@ -1153,7 +1155,7 @@ def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int) 
     generation of calls * count draws, the end state after each call's slice
     (gc_mt19937_generate_multi_j).  count >= 624."""
     total = count * calls
-    J = mt_pipe_generator_draws(total)
+    J = mt_pipe_generator_draws(total, True)
     gens = -(-total // J)
     js, gss = _mt_side(dev)
     gs = gss[slot]
@@ -1265,9 +1267,11 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     # the state is read after them
     nslot = min(MT_MAX_SLOTS, -(-depth // calls) + 3)
     queue = _MT_SPEC.pop(d, [])
+    dropped = False  # queued runs dropped here: they moved dst past torch's state
     if _MT_NSLOT.get(d) != nslot:
         for r in queue:
             r.done.synchronize()
+        dropped = bool(queue)
         queue = []
         _MT_NSLOT[d] = nslot
 
@@ -1277,7 +1281,7 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
         return k % nslot
 
     if count == 0:
-        if queue:  # dropped runs still moved dst on: send the state next time
+        if queue or dropped:  # dropped runs still moved dst on: send the state next time
             _MT_LAST.pop(d, None)
         return torch.empty(0, dtype=torch.int32, device=device)
 
@@ -1290,7 +1294,7 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     if queue and untouched and queue[0].count == count and queue[0].packed == packed:
         run = queue[0]
     else:
-        if queue or not untouched:  # dst is not torch's state: send it
+        if queue or dropped or not untouched:  # dst is not torch's state: send it
             with torch.cuda.stream(js):
                 h = hin.numpy().view(np.uint32)  # free: earlier copies from it were waited for
                 h[:624] = words

@@ -82,6 +82,31 @@ def test_repeated_calls_every_depth_vs_serial_stream(depth, count):
         codec.mt_release()
 
 
+def test_switching_run_forms_without_reseeding_vs_serial_stream():
+    """Multi-call runs (plain draws, count >= 624), then packed single-call
+    runs, then plain again, with torch's generator never touched in between:
+    the switch changes the slot rotation and drops the queued runs, which had
+    already moved the device state past torch's, so the state must be sent
+    again (bench r05n: a packed call after the multi-call runs returned a
+    read index of -160).  Every call's draws and torch's state after it are
+    the serial stream's."""
+    torch.manual_seed(4321)
+    count = 20_000
+    seq = [False] * 5 + [True] * 4 + [False] * 4 + [True] * 2
+    for i, packed in enumerate(seq):
+        ref, w2, i2 = _oracle_next(count)
+        got = codec.mt19937_draws(count, DEV, packed24=packed)
+        torch.cuda.synchronize()
+        if packed:
+            b = got.cpu().numpy().view(np.uint8).reshape(-1, 3).astype(np.uint32)
+            assert np.array_equal(b[:, 0] | b[:, 1] << 8 | b[:, 2] << 16, ref & 0xFFFFFF), i
+        else:
+            assert np.array_equal(got.cpu().numpy().view(np.uint32), ref), i
+        words, idx = torch_mt_state()
+        assert idx == i2 and np.array_equal(words, w2), i
+    codec.mt_release()
+
+
 def test_torch_mode_compressor_back_to_back_vs_oracle():
     """QSGDMaxNormCompressor.compress in torch mode, five back-to-back calls on
     the same bucket (the speculative draws used four times), then the fused

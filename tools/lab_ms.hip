@@ -63,6 +63,12 @@ __global__ __launch_bounds__(256) void k_read_nt(const float4 *x, uint64_t n4, u
         out[0] = m;
 }
 
+__global__ __launch_bounds__(256) void k_write_nt(float4 *o, uint64_t n4)
+{
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < n4; t += gridDim.x * 256ull)
+        st_nt4(reinterpret_cast<float *>(o + t), make_float4((float)t, 1.0f, 2.0f, 3.0f));
+}
+
 // select-like pattern: L planes of x -> one packed word quad
 template <int L>
 __global__ __launch_bounds__(256) void k_rw_planar(const float *x, uint32_t M, uint32_t *words, uint32_t n)
@@ -351,6 +357,21 @@ int main(int argc, char **argv)
     } else {
         printf("Mq %% 16 != 0: no Q=4 select\n");
     }
+    // the decode with 2 / 4 quads per lane (k_ms_decode_fast_oq) == the product's
+    auto decq = [&](auto kern, uint32_t Q, float *dst) {
+        return [=] {
+            hipLaunchKernelGGL(kern, dim3((Mq / (4 * Q) + 63) / 64), dim3(256), 0, 0, wq, mk, fd, n32, norm, la, fa, Mq,
+                               ql.bits, sub, 1.0f, dst);
+        };
+    };
+    CK(hipMemset(out2, 0, n * 4));
+    decq(k_ms_decode_fast_oq<10, 0, 2, 2>, 2, out2)();
+    cmp("decode oq Q=2", out, out2, n * 4);
+    if (q4) {
+        CK(hipMemset(out2, 0, n * 4));
+        decq(k_ms_decode_fast_oq<10, 0, 2, 4>, 4, out2)();
+        cmp("decode oq Q=4", out, out2, n * 4);
+    }
     p_w1();
     cmp("one-pass mask == two-pass", mw, mw3, (size_t)Mm * 4);
     cmp("one-pass words == two-pass", wq, wq3, (size_t)Mq * 4);
@@ -468,6 +489,12 @@ int main(int argc, char **argv)
     vs.push_back({"one-pass per-quad dense EAGER0 U2", w1(k_ms_fused_w1<2, 2, MSV_EAGER0, 2>, g4(Mm)), xb + mb + qb, {}});
     vs.push_back({"one-pass per-quad KIND0 EAGER0 U2 (r03)", w1(k_ms_fused_w1<0, 2, MSV_EAGER0, 2>, g4(Mm)), xb + mb + qb, {}});
     vs.push_back({"product decode order 0", p_dec(0), xb + mb + qb, {}});
+    vs.push_back({"lab decode Q=2", decq(k_ms_decode_fast_oq<10, 0, 2, 2>, 2, out2), xb + mb + qb, {}});
+    if (q4)
+        vs.push_back({"lab decode Q=4", decq(k_ms_decode_fast_oq<10, 0, 2, 4>, 4, out2), xb + mb + qb, {}});
+    vs.push_back({"roof: write 4n (NT float4)", [&] {
+                      hipLaunchKernelGGL(k_write_nt, dim3(4096), dim3(256), 0, 0, (float4 *)out2, n / 4);
+                  }, xb, {}});
     vs.push_back({"product absmax (memset + atomicMax)", [&] { gc_absmax_f32(x, nullptr, n, norm, nullptr, nullptr); },
                   xb, {}});
     void *aws;

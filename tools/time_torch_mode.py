@@ -96,7 +96,7 @@ for G in GS:
             codec.MT_MULTI_CALLS = M
             codec.mt_release()
             e, s = per_call(enc), per_call(step)
-            print(f"generators {G or codec.mt_pipe_generators(n * M)} depth {D} calls/run {M}"
+            print(f"generators {G or codec.mt_pipe_generators(n * M, M > 1)} depth {D} calls/run {M}"
                   f"{' cadence' if CADENCE else ''}{' packed24' if PACKED else ''}"
                   f"{' prio ' + ','.join(codec.MT_SIDE_PRIORITY) if os.environ.get('PRIO') else ''}: encode {e:.3f} ms, "
                   f"absmax + encode {s:.3f} ms per call", flush=True)
