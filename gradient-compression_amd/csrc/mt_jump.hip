@@ -616,11 +616,14 @@ size_t gc_mt19937_workspace_size_multi_j(uint64_t count, uint64_t J, uint32_t ne
     return 4 * (kWsPart + kMtJumpSplit * (gens - 1 + nend) * kMtN);
 }
 
-int gc_mt19937_generate_multi_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
-                                const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint32_t *ends_out,
-                                uint32_t *out, void *workspace, int phase, gc_stream_t stream)
+}  // extern "C"
+
+// the multi-call run of gc_mt19937_generate_multi_j / _multi24_j: MODE 0
+// plain draws, 3 the 24-bit packed draws
+static int mt_multi(const char *what, int mode, uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens,
+                    uint64_t J, const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint32_t *ends_out,
+                    uint32_t *out, void *workspace, int phase, gc_stream_t stream)
 {
-    const char *what = "gc_mt19937_generate_multi_j";
     GC_REQUIRE(phase >= 1 && phase <= 3, "%s: phase must be 1, 2 or 3", what);
     GC_REQUIRE(state_dev && workspace && end_coefs && ends_out, "%s: null state / workspace / ends", what);
     GC_REQUIRE(nend >= 1 && nend <= 64 && per_end >= kMtN, "%s: nend must be 1..64 and per_end >= 624", what);
@@ -628,6 +631,7 @@ int gc_mt19937_generate_multi_j(uint32_t *state_dev, const uint32_t *table_dev, 
     const uint64_t count = per_end * nend;
     GC_REQUIRE(count < (1ull << 40), "%s: count too large", what);
     GC_REQUIRE(!(phase & 2) || out, "%s: null out", what);
+    GC_REQUIRE(!(phase & 2) || ((uintptr_t)out & 3u) == 0, "%s: out must be 4-byte aligned", what);
     const uint64_t gens = (count + J - 1) / J;
     GC_REQUIRE(gens - 1 <= table_gens && (gens == 1 || table_dev),
                "%s: jump table holds %llu generators, %llu draws need %llu", what, (unsigned long long)table_gens,
@@ -643,11 +647,39 @@ int gc_mt19937_generate_multi_j(uint32_t *state_dev, const uint32_t *table_dev, 
         hipLaunchKernelGGL(k_mt_end_multi, dim3(nend), dim3(256), 0, st, ws, jumps, nend, per_end, state_dev,
                            ends_out);
     }
-    if (phase & 2)
-        hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
-                           J, count, (void *)out, (uint32_t *)nullptr, (const float *)nullptr, (const float *)nullptr,
-                           0.0f);
+    if (phase & 2) {
+        if (mode == 3)
+            hipLaunchKernelGGL(k_mt_gen<3>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens,
+                               (uint64_t)jumps, J, count, (void *)out, (uint32_t *)nullptr, (const float *)nullptr,
+                               (const float *)nullptr, 0.0f);
+        else
+            hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens,
+                               (uint64_t)jumps, J, count, (void *)out, (uint32_t *)nullptr, (const float *)nullptr,
+                               (const float *)nullptr, 0.0f);
+    }
     return launch_status(what);
+}
+
+extern "C" {
+
+int gc_mt19937_generate_multi_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint32_t *ends_out,
+                                uint32_t *out, void *workspace, int phase, gc_stream_t stream)
+{
+    return mt_multi("gc_mt19937_generate_multi_j", 0, state_dev, table_dev, table_gens, J, end_coefs, nend, per_end,
+                    ends_out, out, workspace, phase, stream);
+}
+
+int gc_mt19937_generate_multi24_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                  const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint64_t idx,
+                                  uint32_t *ends_out, uint32_t *out, void *workspace, int phase, gc_stream_t stream)
+{
+    const char *what = "gc_mt19937_generate_multi24_j";
+    GC_REQUIRE(per_end % 4 == 0 && idx % 4 == 0 && idx <= kMtN,
+               "%s: per_end (%llu) and the read index (%llu) must be multiples of 4", what,
+               (unsigned long long)per_end, (unsigned long long)idx);
+    return mt_multi(what, 3, state_dev, table_dev, table_gens, J, end_coefs, nend, per_end, ends_out, out, workspace,
+                    phase, stream);
 }
 
 int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,

@@ -137,6 +137,7 @@ SIGNATURES = {
     "gc_mt19937_generate_split24_j": (C.c_int, [P, P, u64, u64, P, u64, P, u64, u64, P, C.c_int, P]),
     "gc_mt19937_workspace_size_multi_j": (C.c_size_t, [u64, u64, u32]),
     "gc_mt19937_generate_multi_j": (C.c_int, [P, P, u64, u64, P, u32, u64, P, P, P, C.c_int, P]),
+    "gc_mt19937_generate_multi24_j": (C.c_int, [P, P, u64, u64, P, u32, u64, u64, P, P, P, C.c_int, P]),
     "gc_qsgdbp_decode": (C.c_int, [P, P, u64, P, P, P]),
     "gc_randk_workspace_size": (C.c_size_t, []),
     "gc_randk_gather_absmax": (C.c_int, [P, P, u64, P, P, P, P]),

@@ -1150,10 +1150,11 @@ def _mt_spec_budget(dev) -> int:
     return b
 
 
-def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int) -> _MtRun:
+def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int, packed: bool = False) -> _MtRun:
     """Like _mt_enqueue for `calls` consecutive calls of `count` draws: one
     generation of calls * count draws, the end state after each call's slice
-    (gc_mt19937_generate_multi_j).  count >= 624."""
+    (gc_mt19937_generate_multi_j; packed: the 24-bit draws of
+    gc_mt19937_generate_multi24_j, count and idx multiples of 4).  count >= 624."""
     total = count * calls
     J = mt_pipe_generator_draws(total, True)
     gens = -(-total // J)
@@ -1182,13 +1183,23 @@ def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int) 
         with torch.cuda.stream(js):
             dev_ends = _MT_ENDS[("dev",) + key] = torch.empty((MT_MULTI_MAX, 626), dtype=torch.int32, device=dev)
     run = _MtRun()
-    run.count, run.packed, run.slot, run.calls, run.k = count, False, slot, calls, 0
+    run.count, run.packed, run.slot, run.calls, run.k = count, bool(packed), slot, calls, 0
     run.idx_end = idx + total - 624 * blocks[-1]
+
+    def gen(out, phase):
+        if packed:
+            check(lib.gc_mt19937_generate_multi24_j(_p(st_dev), _p(table), tgens, J, _p(ends), calls, count, idx,
+                                                    _p(dev_ends), out, _p(ws), phase, _stream(dev)),
+                  "gc_mt19937_generate_multi24_j")
+        else:
+            check(lib.gc_mt19937_generate_multi_j(_p(st_dev), _p(table), tgens, J, _p(ends), calls, count,
+                                                  _p(dev_ends), out, _p(ws), phase, _stream(dev)),
+                  "gc_mt19937_generate_multi_j")
+
     with torch.cuda.stream(js):
         if busy is not None:
             js.wait_event(busy)  # that slot's previous generators have read the workspace
-        check(lib.gc_mt19937_generate_multi_j(_p(st_dev), _p(table), tgens, J, _p(ends), calls, count, _p(dev_ends),
-                                              None, _p(ws), 1, _stream(dev)), "gc_mt19937_generate_multi_j")
+        gen(None, 1)
         run.p1 = torch.cuda.Event()
         run.p1.record()
         pin[:calls].copy_(dev_ends[:calls], non_blocking=True)
@@ -1201,9 +1212,8 @@ def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int) 
             t.record_stream(gs)
     with torch.cuda.stream(gs):
         gs.wait_event(run.p1)
-        run.out = torch.empty(total, dtype=torch.int32, device=dev)
-        check(lib.gc_mt19937_generate_multi_j(_p(st_dev), _p(table), tgens, J, _p(ends), calls, count, _p(dev_ends),
-                                              _p(run.out), _p(ws), 2, _stream(dev)), "gc_mt19937_generate_multi_j")
+        run.out = torch.empty(total // 4 * 3 if packed else total, dtype=torch.int32, device=dev)
+        gen(_p(run.out), 2)
         run.done = torch.cuda.Event()
         run.done.record()
     _MT_BUSY[key] = run.done
@@ -1257,7 +1267,7 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     untouched = last is not None and last[1] == idx and np.array_equal(last[0], words)
     depth = max(0, int(MT_SPECULATE_DEPTH))
     packed = bool(packed24) and count > 0 and mt19937_packable(count, int(idx))
-    multi = not packed and count >= 624  # multi-call runs (gc_mt19937_generate_multi_j)
+    multi = count >= 624  # multi-call runs (gc_mt19937_generate_multi_j / _multi24_j)
     calls = max(1, min(int(MT_MULTI_CALLS), MT_MULTI_MAX)) if multi else 1
     # slots in rotation: the runs in flight (the current one, those holding the
     # next `depth` calls: ceil(depth / calls) runs, one more while the current
@@ -1287,7 +1297,8 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
 
     def enqueue(st_idx, ncalls):
         if multi:
-            return _mt_enqueue_multi(device, dst, count, ncalls, st_idx, next_slot())
+            return _mt_enqueue_multi(device, dst, count, ncalls, st_idx, next_slot(),
+                                     packed and mt19937_packable(count, st_idx))
         return _mt_enqueue(device, dst, count, st_idx, hout, next_slot(),
                            packed and mt19937_packable(count, st_idx))
 
@@ -1322,7 +1333,8 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     cur.wait_event(run.done)
     if queue and MT_WAIT_NEXT_JUMPS:
         cur.wait_event(queue[0].p1)
-    out = run.out[k * count:(k + 1) * count] if run.calls > 1 else run.out
+    per = count // 4 * 3 if run.packed else count
+    out = run.out[k * per:(k + 1) * per] if run.calls > 1 else run.out
     run.out.record_stream(cur)
     if queue:
         _MT_SPEC[d] = queue

@@ -405,6 +405,14 @@ size_t gc_mt19937_workspace_size_multi_j(uint64_t count, uint64_t J, uint32_t ne
 int gc_mt19937_generate_multi_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
                                 const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint32_t *ends_out,
                                 uint32_t *out, void *workspace, int phase, gc_stream_t stream);
+/* gc_mt19937_generate_multi_j with the draws packed to 24 bits (the
+ * GC_RNG_STREAM24 layout: 3 per_end / 4 words per call, calls back to back).
+ * idx = the state's read index (state_dev[624], which the caller sent); idx
+ * and per_end must be multiples of 4, so every call's draws start on a whole
+ * word. */
+int gc_mt19937_generate_multi24_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                  const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint64_t idx,
+                                  uint32_t *ends_out, uint32_t *out, void *workspace, int phase, gc_stream_t stream);
 /* gc_mt19937_generate_split_j with the draws packed to 24 bits (the
  * GC_RNG_STREAM24 layout: 3 count / 4 words of out).  idx = the state's read
  * index (state_dev[624], which the caller sent); idx and count must be
