@@ -34,6 +34,18 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(declared_symbols())
 
 
+def test_strict_library_exports_every_declared_symbol():
+    """lib/libgcodec_strict.so (GC_STRICT_HANDOFF=1, built by build() beside
+    the product library) exports the same ABI: a stale strict build fails
+    here on the CPU instead of in tests/test_gpu_strict_handoff.py."""
+    path = os.path.join(ROOT, "gradient-compression_amd", "lib", "libgcodec_strict.so")
+    if not os.path.exists(path):
+        pytest.skip("strict library not built")
+    lib = C.CDLL(path)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
 def test_version_and_abi():
     from gcodec import _lib
 
