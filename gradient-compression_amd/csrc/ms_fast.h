@@ -80,6 +80,7 @@ enum : int {
     MSV_FULLDUP = 512,  // octet mask kernel: a second copy of the plane code for wave-uniform full
                         // tiles, without the per-lane tail checks (more VGPRs)
     MSV_UFLAG = 1024,   // octet mask kernel: one copy, the tail checks behind a wave-uniform flag
+    MSV_PLAINST = 2048, // decode / one-pass encode: plain (temporal) stores instead of nontemporal ones
 };
 
 template <int KIND, int VAR>
@@ -202,6 +203,16 @@ __device__ __forceinline__ float4 load4_nt_tail(const float *__restrict__ x, uin
     return v;
 }
 
+__device__ __forceinline__ void st_nt4u(uint32_t *p, const uint4 &v);
+// a word quad stored nontemporal (NT) or plain
+template <bool NT>
+__device__ __forceinline__ void st4u(uint32_t *p, const uint4 &v)
+{
+    if constexpr (NT)
+        st_nt4u(p, v);
+    else
+        *reinterpret_cast<uint4 *>(p) = v;
+}
 __device__ __forceinline__ void st_nt4u(uint32_t *p, const uint4 &v)
 {
     typedef uint32_t u4v __attribute__((ext_vector_type(4)));
@@ -569,7 +580,7 @@ __device__ __forceinline__ uint4 select_plane(const float *__restrict__ x, uint3
 }
 
 // decoded floats of 4 elements (compressors.py:819-826 order 0; 668-680 order 1) * alpha
-template <int ORDER, int NL>
+template <int ORDER, int NL, bool NTS = true>
 __device__ __forceinline__ void decode_plane(const uint4 &wd, uint32_t sh, uint32_t msk, int32_t sub, const uint4 &m,
                                              float norm, const LevelsArg &lv, const MsFastArg &fa,
                                              const float (&c)[GC_MAX_LEVELS], bool mk0, float alpha,
@@ -599,7 +610,10 @@ __device__ __forceinline__ void decode_plane(const uint4 &wd, uint32_t sh, uint3
         op[e] = d * alpha;
     }
     if (i0 + 4 <= n) {
-        st_nt4(out + i0, o);
+        if constexpr (NTS)
+            st_nt4(out + i0, o);
+        else
+            *reinterpret_cast<float4 *>(out + i0) = o;
     } else {
         for (int e = 0; e < 4; ++e)
             if (i0 + e < n)
@@ -1715,7 +1729,8 @@ __global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1_o2(
                         C.w += e + 3 < n ? c : 0u;
                     }
                 }
-                st_nt4u(words + j0, make_uint4(C.x - acc[hq].x, C.y - acc[hq].y, C.z - acc[hq].z, C.w - acc[hq].w));
+                st4u<(VAR & MSV_PLAINST) == 0>(words + j0, make_uint4(C.x - acc[hq].x, C.y - acc[hq].y,
+                                                                     C.z - acc[hq].z, C.w - acc[hq].w));
             }
         }
         if (h) {
@@ -1731,7 +1746,7 @@ __global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1_o2(
                     const uint4 a = part[q][hq][lane];
                     o = make_uint4(o.x | a.x, o.y | a.y, o.z | a.z, o.w | a.w);
                 }
-                st_nt4u(mask_words + 8u * t + 4u * hq, o);
+                st4u<(VAR & MSV_PLAINST) == 0>(mask_words + 8u * t + 4u * hq, o);
             }
         }
         __syncthreads();
@@ -1785,8 +1800,8 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode_fast(const uint32_t *__res
             const uint32_t i0 = p * Mq + 4u * t;
             if (i0 >= n)
                 break;
-            decode_plane<ORDER, NL>(wd, p * wq, msk, sub, mask_levels4_fast<NL>(mk, fd, i0), norm, lv, fa, c, mk0, alpha,
-                                out, i0, n);
+            decode_plane<ORDER, NL, (VAR & MSV_PLAINST) == 0>(wd, p * wq, msk, sub, mask_levels4_fast<NL>(mk, fd, i0),
+                                                              norm, lv, fa, c, mk0, alpha, out, i0, n);
         }
     }
 }

@@ -52,6 +52,24 @@ __global__ void k_fill(float *x, uint64_t n, uint32_t seed)
     }
 }
 
+// N(0, 0.01) by Box-Muller from the same counter hash (LAB_NORMAL=1: the
+// bench's torch.randn-like data, with its tails: norm ~ 5.4 sigma at 23.5 M)
+__global__ void k_fill_normal(float *x, uint64_t n, uint32_t seed)
+{
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+        h ^= h >> 15;
+        h *= 2246822519u;
+        h ^= h >> 13;
+        uint32_t g = h * 3266489917u + 0x9E3779B9u;
+        g ^= g >> 16;
+        g *= 2246822519u;
+        g ^= g >> 13;
+        const float u1 = ((float)(h >> 8) + 0.5f) * 0x1p-24f, u2 = (float)(g >> 8) * 0x1p-24f;
+        x[i] = 0.01f * sqrtf(-2.0f * logf(u1)) * cosf(6.2831853f * u2);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_read_nt(const float4 *x, uint64_t n4, uint32_t *out)
 {
     uint32_t m = 0;
@@ -106,16 +124,17 @@ __global__ __launch_bounds__(256) void k_wr_planar(const uint32_t *words, uint32
 struct Timer {
     hipEvent_t a, b;
     Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
+    hipStream_t st = 0;  // the stream the events are recorded on (the variants' own)
     template <class F>
     float run(F f, int reps = 20)
     {
         f();
         f();
         CK(hipDeviceSynchronize());
-        CK(hipEventRecord(a, 0));
+        CK(hipEventRecord(a, st));
         for (int i = 0; i < reps; ++i)
             f();
-        CK(hipEventRecord(b, 0));
+        CK(hipEventRecord(b, st));
         CK(hipEventSynchronize(b));
         float ms;
         CK(hipEventElapsedTime(&ms, a, b));
@@ -205,7 +224,10 @@ int main(int argc, char **argv)
     CK(hipMalloc(&wq, (size_t)Mq * 4 + 64));
     CK(hipMalloc(&wq2, (size_t)Mq * 4 + 64));
     CK(hipMalloc(&scratch, 64));
-    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, x, n, 11u);
+    if (getenv("LAB_NORMAL"))
+        hipLaunchKernelGGL(k_fill_normal, dim3(4096), dim3(256), 0, 0, x, n, 11u);
+    else
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, x, n, 11u);
     GK(gc_absmax_f32(x, nullptr, n, norm, nullptr, nullptr));
     CK(hipDeviceSynchronize());
 
@@ -365,6 +387,9 @@ int main(int argc, char **argv)
         };
     };
     CK(hipMemset(out2, 0, n * 4));
+    v_dec(k_ms_decode_fast<10, 0, 2, MSV_PLAINST>, out2)();
+    cmp("decode plain stores", out, out2, n * 4);
+    CK(hipMemset(out2, 0, n * 4));
     decq(k_ms_decode_fast_oq<10, 0, 2, 2>, 2, out2)();
     cmp("decode oq Q=2", out, out2, n * 4);
     if (q4) {
@@ -440,6 +465,7 @@ int main(int argc, char **argv)
         std::function<void()> f;
         double bytes;
         std::vector<float> t;
+        hipStream_t st = 0;
     };
     std::vector<V> vs;
     vs.push_back({"roof: read x (NT)", [&] {
@@ -519,6 +545,52 @@ int main(int argc, char **argv)
                                              (uint32_t *)aws);
                       }, xb, {}});
     }
+    // whole steps in sequence (the bucket fits the Infinity Cache, so a kernel's own loop is optimistic):
+    // the decode's store policy decides how much dirty data the next step's absmax waits for
+    vs.push_back({"seq: absmax + one-pass + decode NT (product)", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      p_w1();
+                      p_dec(0)();
+                  }, xb * 3 + mb * 2 + qb * 2, {}});
+    // the decode reading what the one-pass kernel just wrote (NT or plain stores)
+    auto dec3 = [&] { GK(gc_ms_decode(wq3, mw3, nullptr, n, norm, &lv, &ml, &ql, 1, 1.0f, out, nullptr)); };
+    vs.push_back({"seq: one-pass + decode of its own words (NT stores)", [&] {
+                      p_w1();
+                      dec3();
+                  }, 0, {}});
+    vs.push_back({"seq: one-pass plain stores + decode of its own words", [&] {
+                      w1(k_ms_fused_w1_o2<MSV_PREFETCH | MSV_PLAINST>, g8(Mm))();
+                      dec3();
+                  }, 0, {}});
+    vs.push_back({"seq: one-pass + decode of other words", [&] {
+                      p_w1();
+                      GK(gc_ms_decode(wq, mw, nullptr, n, norm, &lv, &ml, &ql, 1, 1.0f, out, nullptr));
+                  }, 0, {}});
+    vs.push_back({"seq: absmax + one-pass + decode plain stores", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      p_w1();
+                      v_dec(k_ms_decode_fast<10, 0, 2, MSV_PLAINST>, out2)();
+                  }, xb * 3 + mb * 2 + qb * 2, {}});
+    vs.push_back({"seq: absmax + mask/cache + select + decode NT (product)", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      p_maskc();
+                      p_selc();
+                      p_dec(0)();
+                  }, 0, {}});
+    vs.push_back({"seq: absmax + mask/cache + select + decode plain stores", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      p_maskc();
+                      p_selc();
+                      v_dec(k_ms_decode_fast<10, 0, 2, MSV_PLAINST>, out2)();
+                  }, 0, {}});
+    // the same sequences on a created (non-null) stream, as a torch process runs them
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    vs.push_back({"seq on a created stream: absmax + one-pass + decode NT", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, s2);
+                      GK(gc_ms_encode_w1(x, n, norm, &lv, &rng, &ml, &ql, mw3, wq3, s2));
+                      GK(gc_ms_decode(wq, mw, nullptr, n, norm, &lv, &ml, &ql, 0, 1.0f, out, s2));
+                  }, 0, {}, s2});
     for (auto &v : vs) {  // each variant once, synchronised, named first (a fault names its variant)
         printf("run-check %s\n", v.name);
         fflush(stdout);
@@ -526,8 +598,10 @@ int main(int argc, char **argv)
         CK(hipDeviceSynchronize());
     }
     for (int rep = 0; rep < 5; ++rep)
-        for (auto &v : vs)
+        for (auto &v : vs) {
+            T.st = v.st;
             v.t.push_back(T.run(v.f, 30));
+        }
     for (auto &v : vs) {
         std::sort(v.t.begin(), v.t.end());
         row(v.name, v.t[v.t.size() / 2], v.bytes);
