@@ -80,7 +80,9 @@ enum : int {
     MSV_FULLDUP = 512,  // octet mask kernel: a second copy of the plane code for wave-uniform full
                         // tiles, without the per-lane tail checks (more VGPRs)
     MSV_UFLAG = 1024,   // octet mask kernel: one copy, the tail checks behind a wave-uniform flag
-    MSV_PLAINST = 2048, // decode / one-pass encode: plain (temporal) stores instead of nontemporal ones
+    MSV_PLAINST = 2048, // plain (temporal) stores of the words / mask words instead of nontemporal ones:
+                        // the next kernel of a step reads them at once (profiles/r05zh, r05zj_lab_ms.log)
+    MSV_NTMASK = 4096,  // decode: the mask words read with nontemporal loads
 };
 
 template <int KIND, int VAR>
@@ -103,7 +105,8 @@ struct MsFastArg {
 
 // the mask level of 4 elements, from W-summed thermometer fields; the plane
 // of element i0 is i0 / M (fast division), all 4 share it (M % 4 == 0)
-template <int NL>
+// NTL: the mask words read with nontemporal loads (lab: MSV_NTMASK)
+template <int NL, bool NTL = false>
 __device__ __forceinline__ uint4 mask_levels4_fast(const MaskArg &mk, const FastDiv &fd, uint32_t i0)
 {
     const uint32_t plane = fdiv(i0, fd);
@@ -113,7 +116,14 @@ __device__ __forceinline__ uint4 mask_levels4_fast(const MaskArg &mk, const Fast
     uint4 m = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int f = 0; f < NL - 1; ++f) {
-        const uint4 wd = *reinterpret_cast<const uint4 *>(mk.words + (uint64_t)f * mk.M + pos);
+        uint4 wd;
+        if constexpr (NTL) {
+            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+            const u4v r = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(mk.words + (uint64_t)f * mk.M + pos));
+            wd = make_uint4(r.x, r.y, r.z, r.w);
+        } else {
+            wd = *reinterpret_cast<const uint4 *>(mk.words + (uint64_t)f * mk.M + pos);
+        }
         m.x += ((wd.x >> sh) & msk) == mk.world;
         m.y += ((wd.y >> sh) & msk) == mk.world;
         m.z += ((wd.z >> sh) & msk) == mk.world;
@@ -852,7 +862,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache(const void *__restri
 
 // the same with two adjacent word quads per lane (8 elements of a plane: one
 // 8- / 16-byte cell load, twice the bytes in flight per wave; Mq % 8 == 0)
-template <int LQ, int NL, int CBY>
+template <int LQ, int NL, int CBY, bool NTS = true>
 __global__ __launch_bounds__(kBlock) void k_ms_select_cache_o2(const void *__restrict__ cache, uint32_t n, MaskArg mk,
                                                                FastDiv fd, uint32_t Mq, uint32_t wq, uint32_t cb,
                                                                uint32_t *__restrict__ words)
@@ -946,8 +956,8 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache_o2(const void *__res
 #pragma unroll
             for (int hq = 0; hq < 2; ++hq) {
                 const uint4 a = part[0][hq][lane], b = part[1][hq][lane], c = part[2][hq][lane];
-                st_nt4u(words + 8u * t + 4u * hq, make_uint4(acc[hq].x + a.x + b.x + c.x, acc[hq].y + a.y + b.y + c.y,
-                                                             acc[hq].z + a.z + b.z + c.z, acc[hq].w + a.w + b.w + c.w));
+                st4u<NTS>(words + 8u * t + 4u * hq, make_uint4(acc[hq].x + a.x + b.x + c.x, acc[hq].y + a.y + b.y + c.y,
+                                                               acc[hq].z + a.z + b.z + c.z, acc[hq].w + a.w + b.w + c.w));
             }
         }
         __syncthreads();
@@ -1517,9 +1527,9 @@ __global__ GC_MS_OCC __launch_bounds__(kBlock) void k_ms_mask_fast_o2(const floa
 #pragma unroll
             for (int hq = 0; hq < 2; ++hq) {
                 const uint4 a = part[0][hq][lane], b = part[1][hq][lane], c = part[2][hq][lane];
-                st_nt4u(mask_words + 8u * t + 4u * hq,
-                        make_uint4(acc[hq].x | a.x | b.x | c.x, acc[hq].y | a.y | b.y | c.y,
-                                   acc[hq].z | a.z | b.z | c.z, acc[hq].w | a.w | b.w | c.w));
+                st4u<(VAR & MSV_PLAINST) == 0>(mask_words + 8u * t + 4u * hq,
+                                               make_uint4(acc[hq].x | a.x | b.x | c.x, acc[hq].y | a.y | b.y | c.y,
+                                                          acc[hq].z | a.z | b.z | c.z, acc[hq].w | a.w | b.w | c.w));
             }
         }
         __syncthreads();
@@ -1586,8 +1596,9 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_fast_o2(const float *__res
 #pragma unroll
             for (int hq = 0; hq < 2; ++hq) {
                 const uint4 a = part[0][hq][lane], b = part[1][hq][lane], c = part[2][hq][lane];
-                st_nt4u(words + 8u * t + 4u * hq, make_uint4(acc[hq].x + a.x + b.x + c.x, acc[hq].y + a.y + b.y + c.y,
-                                                             acc[hq].z + a.z + b.z + c.z, acc[hq].w + a.w + b.w + c.w));
+                st4u<(VAR & MSV_PLAINST) == 0>(words + 8u * t + 4u * hq,
+                                               make_uint4(acc[hq].x + a.x + b.x + c.x, acc[hq].y + a.y + b.y + c.y,
+                                                          acc[hq].z + a.z + b.z + c.z, acc[hq].w + a.w + b.w + c.w));
             }
         }
         __syncthreads();
@@ -1800,8 +1811,9 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode_fast(const uint32_t *__res
             const uint32_t i0 = p * Mq + 4u * t;
             if (i0 >= n)
                 break;
-            decode_plane<ORDER, NL, (VAR & MSV_PLAINST) == 0>(wd, p * wq, msk, sub, mask_levels4_fast<NL>(mk, fd, i0),
-                                                              norm, lv, fa, c, mk0, alpha, out, i0, n);
+            decode_plane<ORDER, NL, (VAR & MSV_PLAINST) == 0>(
+                wd, p * wq, msk, sub, mask_levels4_fast<NL, (VAR & MSV_NTMASK) != 0>(mk, fd, i0), norm, lv, fa, c,
+                mk0, alpha, out, i0, n);
         }
     }
 }

@@ -472,7 +472,9 @@ int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_leve
 #define GC_FW8(VAR_)                                                                                                \
     hipLaunchKernelGGL((k_ms_fused_w1_o2<VAR_>), dim3(g8), dim3(64 * r), 0, st, x, (uint32_t)n, norm, la, fa, ra, Mm, r, \
                        q_lanes->per_word, q_lanes->bits, qmax, Cw, pend, mask_words, words)
-            if (wide) { GC_FW8(MSV_WIDE | MSV_PREFETCH); } else { GC_FW8(MSV_PREFETCH); }
+            // plain stores: the decode that follows at W = 1 reads these words
+            // and mask words at once (profiles/r05zh_lab_ms.log)
+            if (wide) { GC_FW8(MSV_WIDE | MSV_PREFETCH | MSV_PLAINST); } else { GC_FW8(MSV_PREFETCH | MSV_PLAINST); }
 #undef GC_FW8
         } else if (rng->kind == GC_RNG_PHILOX) {
             if (wide) { GC_FW(2, 2, MSV_WIDE); }
@@ -530,7 +532,7 @@ int gc_ms_mask_encode(const float *x, const int64_t *idx, uint64_t n, const floa
     GC_DISPATCH_L2(mask_lanes->per_word, hipLaunchKernelGGL((k_ms_mask_fast_o2<LL, VAR_>), dim3(g8), dim3(kBlock), 0, \
                                                             st, x, (uint32_t)n, norm, la, fa, ra, (uint32_t)M, w,      \
                                                             mask_words, (void *)nullptr, 0, 0u))
-            if (wide) { GC_MF8(MSV_WIDE | MSV_ROLL); } else { GC_MF8(MSV_ROLL | MSV_UFLAG); }
+            if (wide) { GC_MF8(MSV_WIDE | MSV_ROLL | MSV_PLAINST); } else { GC_MF8(MSV_ROLL | MSV_UFLAG | MSV_PLAINST); }
 #undef GC_MF8
         } else if (levels->count == 2) {
             if (rng->kind == GC_RNG_PHILOX) { GC_MF(2, 2); } else { GC_MF(1, 2); }
@@ -595,7 +597,7 @@ int gc_ms_select_encode(const float *x, const int64_t *idx, uint64_t n, const fl
     GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_fast_o2<LL, VAR_>), dim3(g8), dim3(kBlock), 0, st, \
                                                          x, (uint32_t)n, norm, la, fa, ra, mk, fd, (uint32_t)Mq, wq,  \
                                                          qmax, words))
-            if (wide) { GC_SF8(MSV_WIDE | MSV_ROLL); } else { GC_SF8(MSV_ROLL); }
+            if (wide) { GC_SF8(MSV_WIDE | MSV_ROLL | MSV_PLAINST); } else { GC_SF8(MSV_ROLL | MSV_PLAINST); }
 #undef GC_SF8
         } else if (levels->count == 2) {
             if (rng->kind == GC_RNG_PHILOX) { GC_SF(2, 2); } else { GC_SF(1, 2); }
@@ -662,9 +664,9 @@ int gc_ms_mask_encode_cached(const float *x, uint64_t n, const float *norm, cons
     if (levels->count == 2 && rng->kind == GC_RNG_PHILOX && M % 8 == 0) {  // octets: dense draws, 3 blocks per 8
         const unsigned g8 = (unsigned)std::max<uint64_t>(1, (ms_grid(M >> 3) + ms_tiles() - 1) / ms_tiles());
         if (cg.bytes == 1) {
-            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL, 1); } else { GC_MFC8(MSV_ROLL | MSV_UFLAG, 1); }
+            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL | MSV_PLAINST, 1); } else { GC_MFC8(MSV_ROLL | MSV_UFLAG | MSV_PLAINST, 1); }
         } else {
-            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL, 2); } else { GC_MFC8(MSV_ROLL | MSV_UFLAG, 2); }
+            if (wide) { GC_MFC8(MSV_WIDE | MSV_ROLL | MSV_PLAINST, 2); } else { GC_MFC8(MSV_ROLL | MSV_UFLAG | MSV_PLAINST, 2); }
         }
     } else if (levels->count == 2) {
         if (cg.bytes == 1) { GC_MFC_K(2, 1) } else { GC_MFC_K(2, 2) }
@@ -704,7 +706,7 @@ int gc_ms_select_cached(const void *cache, uint64_t n, const gc_levels *levels, 
                                                          st, cache, (uint32_t)n, mk, fd, Mq, q_lanes->bits, cg.cb,    \
                                                          words))
 #define GC_SC8(NL_, CBY_)                                                                                           \
-    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_cache_o2<LL, NL_, CBY_>), dim3(g8), dim3(kBlock), \
+    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_select_cache_o2<LL, NL_, CBY_, false>), dim3(g8), dim3(kBlock), \
                                                          0, st, cache, (uint32_t)n, mk, fd, Mq, q_lanes->bits, cg.cb, \
                                                          words))
     if (Mq % 8 == 0 && ms_select_cache_octets()) {  // two quads per lane
@@ -755,9 +757,17 @@ static int ms_decode(const char *what, const uint32_t *words, const uint32_t *ma
     if (ms_fast_decode_ok(mode, n, levels) && mask_lanes->plane_words >= 2 && mask_lanes->plane_words < (1ull << 32)) {
         const MsFastArg fa = ms_fast_arg(levels);
         const FastDiv fd = make_fastdiv((uint32_t)mask_lanes->plane_words);
-        const unsigned g = ms_grid(q_lanes->plane_words >> 2);
+        // one thread per word quad walking all its planes (MSV_PERTHREAD): each
+        // quad's words are read once, not by every wave of the block; the
+        // words a decode reads were usually written just before it (by the
+        // encode at W = 1, by the SUM otherwise), and re-reading fresh lines
+        // from four waves cost more than the split saves (the whole W = 1
+        // step 71.6 -> 68.7 us with the one-pass kernel's plain stores,
+        // profiles/r05zh_lab_ms.log; the decode alone 18.6 against 19.0 us)
+        const unsigned g = (unsigned)std::min<uint64_t>(((q_lanes->plane_words >> 2) + kBlock - 1) / kBlock, 65535);
 #define GC_DF(ORD_, NL_)                                                                                               \
-    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_decode_fast<LL, ORD_, NL_>), dim3(g), dim3(kBlock), 0, st, \
+    GC_DISPATCH_L2(q_lanes->per_word, hipLaunchKernelGGL((k_ms_decode_fast<LL, ORD_, NL_, MSV_PERTHREAD>), dim3(g),    \
+                                                         dim3(kBlock), 0, st, \
                                                          words, mk, fd, (uint32_t)n, norm, la, fa,                  \
                                                          (uint32_t)q_lanes->plane_words, q_lanes->bits, sub, alpha, out))
         if (levels->count == 2) {

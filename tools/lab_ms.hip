@@ -562,6 +562,92 @@ int main(int argc, char **argv)
                       w1(k_ms_fused_w1_o2<MSV_PREFETCH | MSV_PLAINST>, g8(Mm))();
                       dec3();
                   }, 0, {}});
+    auto decv = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid(Mq / 4)), dim3(256), 0, 0, wq3, MaskArg{mw3, Mm, ml.bits, lv.count - 1, 1},
+                           fd, n32, norm, la, fa, Mq, ql.bits, sub, 1.0f, out);
+    };
+    vs.push_back({"seq: one-pass + decode (lab launch) of its own words", [&] {
+                      p_w1();
+                      decv(k_ms_decode_fast<10, 1, 2, 0>);
+                  }, 0, {}});
+    vs.push_back({"seq: one-pass + decode NT mask loads of its own words", [&] {
+                      p_w1();
+                      decv(k_ms_decode_fast<10, 1, 2, MSV_NTMASK>);
+                  }, 0, {}});
+    vs.push_back({"seq: one-pass plain + decode NT mask loads of its own words", [&] {
+                      w1(k_ms_fused_w1_o2<MSV_PREFETCH | MSV_PLAINST>, g8(Mm))();
+                      decv(k_ms_decode_fast<10, 1, 2, MSV_NTMASK>);
+                  }, 0, {}});
+    vs.push_back({"seq: one-pass + decode PERTHREAD (words loaded once per lane)", [&] {
+                      p_w1();
+                      hipLaunchKernelGGL((k_ms_decode_fast<10, 1, 2, MSV_PERTHREAD>), dim3((Mq / 4 + 255) / 256),
+                                         dim3(256), 0, 0, wq3, MaskArg{mw3, Mm, ml.bits, lv.count - 1, 1}, fd, n32,
+                                         norm, la, fa, Mq, ql.bits, sub, 1.0f, out);
+                  }, 0, {}});
+    auto decpt = [&](const uint32_t *wsrc, const uint32_t *msrc) {
+        hipLaunchKernelGGL((k_ms_decode_fast<10, 1, 2, MSV_PERTHREAD>), dim3((Mq / 4 + 255) / 256), dim3(256), 0, 0,
+                           wsrc, MaskArg{msrc, Mm, ml.bits, lv.count - 1, 1}, fd, n32, norm, la, fa, Mq, ql.bits, sub,
+                           1.0f, out);
+    };
+    vs.push_back({"STEP: absmax + one-pass + decode (product)", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      p_w1();
+                      dec3();
+                  }, 0, {}});
+    vs.push_back({"STEP: absmax + one-pass + decode PERTHREAD", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      p_w1();
+                      decpt(wq3, mw3);
+                  }, 0, {}});
+    vs.push_back({"STEP: absmax + one-pass plain stores + decode PERTHREAD", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      w1(k_ms_fused_w1_o2<MSV_PREFETCH | MSV_PLAINST>, g8(Mm))();
+                      decpt(wq3, mw3);
+                  }, 0, {}});
+    vs.push_back({"one-pass plain stores alone", w1(k_ms_fused_w1_o2<MSV_PREFETCH | MSV_PLAINST>, g8(Mm)), 0, {}});
+    vs.push_back({"STEP q-cache: absmax + mask/cache + select + decode (product)", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      GK(gc_ms_mask_encode_cached(x, n, norm, &lv, &rng, &ml, mw2, cache, nullptr));
+                      GK(gc_ms_select_cached(cache, n, &lv, mw2, &ml, &ql, wq2, nullptr));
+                      GK(gc_ms_decode(wq2, mw2, nullptr, n, norm, &lv, &ml, &ql, 1, 1.0f, out, nullptr));
+                  }, 0, {}});
+    vs.push_back({"STEP q-cache: ... + decode PERTHREAD", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      GK(gc_ms_mask_encode_cached(x, n, norm, &lv, &rng, &ml, mw2, cache, nullptr));
+                      GK(gc_ms_select_cached(cache, n, &lv, mw2, &ml, &ql, wq2, nullptr));
+                      decpt(wq2, mw2);
+                  }, 0, {}});
+    auto selc2 = [&](auto kern, const uint32_t *msrc, uint32_t *dst) {
+        hipLaunchKernelGGL(kern, g8(Mq), dim3(256), 0, 0, (const void *)cache2, n32,
+                           MaskArg{msrc, Mm, ml.bits, lv.count - 1, 1}, fd, Mq, ql.bits, 3u, dst);
+    };
+    vs.push_back({"STEP q-cache, lab launches, NT stores", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      mask8(k_ms_mask_fast_o2<32, MSV_ROLL | MSV_UFLAG, 1>, mw2, cache2)();
+                      selc2(k_ms_select_cache_o2<10, 2, 1, true>, mw2, wq2);
+                      decpt(wq2, mw2);
+                  }, 0, {}});
+    vs.push_back({"STEP q-cache, lab launches, plain stores", [&] {
+                      gc_absmax_f32(x, nullptr, n, norm, aws, nullptr);
+                      mask8(k_ms_mask_fast_o2<32, MSV_ROLL | MSV_UFLAG | MSV_PLAINST, 1>, mw2, cache2)();
+                      selc2(k_ms_select_cache_o2<10, 2, 1, false>, mw2, wq2);
+                      decpt(wq2, mw2);
+                  }, 0, {}});
+    vs.push_back({"mask + cache plain stores alone", mask8(k_ms_mask_fast_o2<32, MSV_ROLL | MSV_UFLAG | MSV_PLAINST, 1>,
+                                                           mw2, cache2), 0, {}});
+    vs.push_back({"decode PERTHREAD alone", [&] {
+                      hipLaunchKernelGGL((k_ms_decode_fast<10, 1, 2, MSV_PERTHREAD>), dim3((Mq / 4 + 255) / 256),
+                                         dim3(256), 0, 0, wq3, MaskArg{mw3, Mm, ml.bits, lv.count - 1, 1}, fd, n32,
+                                         norm, la, fa, Mq, ql.bits, sub, 1.0f, out);
+                  }, 0, {}});
+    vs.push_back({"seq: one-pass + decode: fresh words, old mask", [&] {
+                      p_w1();
+                      GK(gc_ms_decode(wq3, mw, nullptr, n, norm, &lv, &ml, &ql, 1, 1.0f, out, nullptr));
+                  }, 0, {}});
+    vs.push_back({"seq: one-pass + decode: old words, fresh mask", [&] {
+                      p_w1();
+                      GK(gc_ms_decode(wq, mw3, nullptr, n, norm, &lv, &ml, &ql, 1, 1.0f, out, nullptr));
+                  }, 0, {}});
     vs.push_back({"seq: one-pass + decode of other words", [&] {
                       p_w1();
                       GK(gc_ms_decode(wq, mw, nullptr, n, norm, &lv, &ml, &ql, 1, 1.0f, out, nullptr));
