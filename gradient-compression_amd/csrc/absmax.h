@@ -168,11 +168,10 @@ __device__ __forceinline__ void absmax_finish(uint32_t m, uint32_t *__restrict__
 }
 
 // MODE 0: float4 dense, 1: scalar dense, 2: gather.  U float4 loads in flight
-// per thread; NT: nontemporal loads (streamed once); REV (MODE 0): the grid
-// walks x from its end, so the part read last (and left in the Infinity
-// Cache) is x's front, where a following pass over x starts
-template <int MODE, bool WS, unsigned BT = kAbsmaxThreads, int U = 4, bool NT = false, unsigned G = kAbsmaxGroups,
-          bool REV = false>
+// per thread; NT: nontemporal loads (streamed once).  (Round 5 measured a
+// reverse walk meant to leave x's front in the Infinity Cache for the encode:
+// no gain)
+template <int MODE, bool WS, unsigned BT = kAbsmaxThreads, int U = 4, bool NT = false, unsigned G = kAbsmaxGroups>
 __global__ __launch_bounds__(BT) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
                                                uint64_t n, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)
 {
@@ -182,18 +181,17 @@ __global__ __launch_bounds__(BT) void k_absmax(const float *__restrict__ x, cons
     if constexpr (MODE == 0) {
         const float4 *x4 = reinterpret_cast<const float4 *>(x);
         const uint64_t n4 = n >> 2;
-        auto at = [&](uint64_t i) { return REV ? n4 - 1 - i : i; };
         for (; t + (U - 1) * stride < n4; t += U * stride) {
             float4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                v[u] = NT ? ld_nt(x4 + at(t + u * stride)) : x4[at(t + u * stride)];
+                v[u] = NT ? ld_nt(x4 + t + u * stride) : x4[t + u * stride];
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 m = max(m, absbits4(v[u]));
         }
         for (; t < n4; t += stride)
-            m = max(m, absbits4(x4[at(t)]));
+            m = max(m, absbits4(x4[t]));
         if (blockIdx.x == 0 && threadIdx.x < (n & 3))
             m = max(m, absbits(x[(n4 << 2) + threadIdx.x]));
     } else {

@@ -75,14 +75,11 @@ enum : int {
     MSV_ROLL = 128,     // octet mask / select kernels: the plane loop is not unrolled (the product:
                         // fewer VGPRs, more waves; mask 22.7 against 27.4 us, with the q cache 32.4
                         // against 45.0 us, profiles/r04n_lab_ms.log)
-    MSV_PAIR = 256,     // octet one-pass / mask kernels: two planes per loop trip, both octets'
-                        // Philox blocks computed together (6 independent chains per lane)
-    MSV_FULLDUP = 512,  // octet mask kernel: a second copy of the plane code for wave-uniform full
-                        // tiles, without the per-lane tail checks (more VGPRs)
-    MSV_UFLAG = 1024,   // octet mask kernel: one copy, the tail checks behind a wave-uniform flag
+    MSV_UFLAG = 1024,   // octet mask kernel: the per-lane tail tests behind a wave-uniform flag
+                        // (round 5 also measured two planes per loop trip and a second copy of the
+                        // plane code for full tiles: slower, removed)
     MSV_PLAINST = 2048, // plain (temporal) stores of the words / mask words instead of nontemporal ones:
                         // the next kernel of a step reads them at once (profiles/r05zh, r05zj_lab_ms.log)
-    MSV_NTMASK = 4096,  // decode: the mask words read with nontemporal loads
 };
 
 template <int KIND, int VAR>
@@ -105,8 +102,7 @@ struct MsFastArg {
 
 // the mask level of 4 elements, from W-summed thermometer fields; the plane
 // of element i0 is i0 / M (fast division), all 4 share it (M % 4 == 0)
-// NTL: the mask words read with nontemporal loads (lab: MSV_NTMASK)
-template <int NL, bool NTL = false>
+template <int NL>
 __device__ __forceinline__ uint4 mask_levels4_fast(const MaskArg &mk, const FastDiv &fd, uint32_t i0)
 {
     const uint32_t plane = fdiv(i0, fd);
@@ -116,14 +112,7 @@ __device__ __forceinline__ uint4 mask_levels4_fast(const MaskArg &mk, const Fast
     uint4 m = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int f = 0; f < NL - 1; ++f) {
-        uint4 wd;
-        if constexpr (NTL) {
-            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-            const u4v r = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(mk.words + (uint64_t)f * mk.M + pos));
-            wd = make_uint4(r.x, r.y, r.z, r.w);
-        } else {
-            wd = *reinterpret_cast<const uint4 *>(mk.words + (uint64_t)f * mk.M + pos);
-        }
+        const uint4 wd = *reinterpret_cast<const uint4 *>(mk.words + (uint64_t)f * mk.M + pos);
         m.x += ((wd.x >> sh) & msk) == mk.world;
         m.y += ((wd.y >> sh) & msk) == mk.world;
         m.z += ((wd.z >> sh) & msk) == mk.world;
@@ -266,14 +255,14 @@ struct CacheCell<2> {
     typedef uint16_t T;
 };
 
-// TAIL = false: the caller knows i0 + 4 <= n (a wave-uniform full tile)
-template <int CBY, bool TAIL = true>
+// utail = false: the caller knows i0 + 4 <= n (a wave-uniform full tile)
+template <int CBY>
 __device__ __forceinline__ void cache_store(void *__restrict__ cache, uint32_t i0, uint32_t n, const uint4 &c,
                                             bool utail = true)
 {
     typedef typename CacheCell<CBY>::T T;
     T *p = reinterpret_cast<T *>(cache) + i0;
-    bool whole = !TAIL || !utail;
+    bool whole = !utail;
     if (!whole) {
         asm volatile("");  // as in mask_plane_d: the per-lane test only in the tail form
         whole = i0 + 4 <= n;
@@ -342,9 +331,9 @@ __device__ __forceinline__ uint4 cache_cells(const uint2 &u)
 // no per-level divergence.
 // DR: the draws, dr(l) = level l's uint4 for elements i0..i0+3 (ms_draws4,
 // or an octet kernel's shared blocks)
-// TAIL = false: the caller knows i0 + 4 <= n (a wave-uniform full tile; the
+// utail = false: the caller knows i0 + 4 <= n (a wave-uniform full tile; the
 // per-lane tail compares cost about 5 VALU instructions per quad)
-template <int NL, int VAR, bool CACHE, bool TAIL = true, typename DR>
+template <int NL, int VAR, bool CACHE, typename DR>
 __device__ __forceinline__ void mask_plane_d(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
                                              uint32_t lo2, uint32_t hi2, const LevelsArg &lv, const MsFastArg &fa,
                                              const DR &dr, uint32_t bit, uint4 (&mb)[NL - 1], int32_t cq = 0,
@@ -441,7 +430,7 @@ __device__ __forceinline__ void mask_plane_d(const float4 &v, uint32_t n, uint32
             mb[f] = make_uint4(m.x > (uint32_t)f ? bit : 0u, m.y > (uint32_t)f ? bit : 0u,
                                m.z > (uint32_t)f ? bit : 0u, m.w > (uint32_t)f ? bit : 0u);
     }
-    if (TAIL && utail) {
+    if (utail) {
         // a wave-uniform branch of its own (the empty asm keeps the compiler
         // from merging it with the per-lane test below and hoisting that
         // test's index arithmetic into the common path)
@@ -964,123 +953,6 @@ __global__ __launch_bounds__(kBlock) void k_ms_select_cache_o2(const void *__res
     }
 }
 
-// the same with Q adjacent word quads per lane (Q = 4: 16 elements of a plane,
-// one 16- / 32-byte cell load and Q mask-word quads per plane, all planes'
-// loads issued before any is used; Mq % (4 Q) == 0)
-template <int LQ, int NL, int CBY, int Q>
-__global__ __launch_bounds__(kBlock) void k_ms_select_cache_oq(const void *__restrict__ cache, uint32_t n, MaskArg mk,
-                                                               FastDiv fd, uint32_t Mq, uint32_t wq, uint32_t cb,
-                                                               uint32_t *__restrict__ words)
-{
-    static_assert(Q == 2 || Q == 4, "2 or 4 quads per lane");
-    const uint32_t cm = (1u << cb) - 1u;
-    const uint32_t units = Mq / (4u * Q);
-    constexpr int PW = (LQ + 3) / 4;
-    __shared__ uint4 part[3][Q][kMsQuadsPerBlock];
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    typedef typename CacheCell<CBY>::T T;
-    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < units; tb += gridDim.x * kMsQuadsPerBlock) {
-        const uint32_t t = tb + lane;
-        uint4 acc[Q] = {};
-        if (t < units) {
-            uint2 c[PW][Q];
-            uint4 mw[PW][Q][NL - 1];
-            uint32_t shm[PW][Q];
-#pragma unroll
-            for (int j = 0; j < PW; ++j) {
-                const uint32_t p = wave + 4u * j;
-                const uint32_t i0 = p * Mq + 4u * Q * t;
-#pragma unroll
-                for (int hq = 0; hq < Q; ++hq) {
-                    c[j][hq] = make_uint2(0u, 0u);
-                    shm[j][hq] = 0;
-#pragma unroll
-                    for (int f = 0; f < NL - 1; ++f)
-                        mw[j][hq][f] = make_uint4(0u, 0u, 0u, 0u);
-                }
-                if (p < (uint32_t)LQ && i0 < n) {
-                    if (i0 + 4u * Q <= n) {  // the unit's cells in whole 16-byte loads (or one 8-byte)
-                        const T *cp = reinterpret_cast<const T *>(cache) + i0;
-                        if constexpr (4 * CBY * Q == 8) {
-                            const uint2 u = *reinterpret_cast<const uint2 *>(cp);
-                            c[j][0] = make_uint2(u.x, 0u);
-                            c[j][1] = make_uint2(u.y, 0u);
-                        } else {
-#pragma unroll
-                            for (int k = 0; k < 4 * CBY * Q / 16; ++k) {
-                                const uint4 u = reinterpret_cast<const uint4 *>(cp)[k];
-                                if constexpr (CBY == 1) {
-                                    c[j][4 * k] = make_uint2(u.x, 0u);
-                                    c[j][4 * k + 1] = make_uint2(u.y, 0u);
-                                    c[j][4 * k + 2] = make_uint2(u.z, 0u);
-                                    c[j][4 * k + 3] = make_uint2(u.w, 0u);
-                                } else {
-                                    c[j][2 * k] = make_uint2(u.x, u.y);
-                                    c[j][2 * k + 1] = make_uint2(u.z, u.w);
-                                }
-                            }
-                        }
-                    } else {
-#pragma unroll
-                        for (int hq = 0; hq < Q; ++hq)
-                            if (i0 + 4u * hq < n)
-                                c[j][hq] = cache_load<CBY>(cache, i0 + 4u * hq, n);
-                    }
-#pragma unroll
-                    for (int hq = 0; hq < Q; ++hq) {
-                        const uint32_t iq = i0 + 4u * hq;
-                        if (iq >= n)
-                            break;
-                        const uint32_t plane = fdiv(iq, fd);
-                        const uint32_t pos = iq - plane * fd.d;
-                        shm[j][hq] = plane * mk.w;
-#pragma unroll
-                        for (int f = 0; f < NL - 1; ++f)
-                            mw[j][hq][f] = *reinterpret_cast<const uint4 *>(mk.words + (uint64_t)f * mk.M + pos);
-                    }
-                }
-            }
-            const uint32_t msk = (1u << mk.w) - 1u;
-#pragma unroll
-            for (int j = 0; j < PW; ++j) {
-                const uint32_t p = wave + 4u * j;
-                const uint32_t sh = p < (uint32_t)LQ ? p * wq : 0u;
-#pragma unroll
-                for (int hq = 0; hq < Q; ++hq) {
-                    const uint4 cj = cache_cells<CBY>(c[j][hq]);
-                    uint4 m = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-                    for (int f = 0; f < NL - 1; ++f) {
-                        m.x += ((mw[j][hq][f].x >> shm[j][hq]) & msk) == mk.world;
-                        m.y += ((mw[j][hq][f].y >> shm[j][hq]) & msk) == mk.world;
-                        m.z += ((mw[j][hq][f].z >> shm[j][hq]) & msk) == mk.world;
-                        m.w += ((mw[j][hq][f].w >> shm[j][hq]) & msk) == mk.world;
-                    }
-                    acc[hq].x += ((cj.x >> (m.x * cb)) & cm) << sh;
-                    acc[hq].y += ((cj.y >> (m.y * cb)) & cm) << sh;
-                    acc[hq].z += ((cj.z >> (m.z * cb)) & cm) << sh;
-                    acc[hq].w += ((cj.w >> (m.w * cb)) & cm) << sh;
-                }
-            }
-        }
-        if (wave) {
-#pragma unroll
-            for (int hq = 0; hq < Q; ++hq)
-                part[wave - 1][hq][lane] = acc[hq];
-        }
-        __syncthreads();
-        if (wave == 0 && t < units) {
-#pragma unroll
-            for (int hq = 0; hq < Q; ++hq) {
-                const uint4 a = part[0][hq][lane], b = part[1][hq][lane], c = part[2][hq][lane];
-                st_nt4u(words + 4u * Q * t + 4u * hq, make_uint4(acc[hq].x + a.x + b.x + c.x, acc[hq].y + a.y + b.y + c.y,
-                                                                 acc[hq].z + a.z + b.z + c.z, acc[hq].w + a.w + b.w + c.w));
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // ---------------------------------------------------------------------------
 // W = 1: mask + select in ONE pass (compressors.py:778-817 with the MIN
 // all-reduce of reducer.py:1680 over a single rank, the identity: the common
@@ -1201,11 +1073,11 @@ constexpr uint32_t kMsFusedMaxR = 8;  // q words per mask word at W = 1: 32 / (q
 // one plane of the fused encode: the thermometer bits into the mask fields,
 // -q * 2^(k wq) into the wave's q word accumulator (word = C - acc, modular:
 // lane = qmax + q).  Elements past n have x = 0 (no lane) and no mask bit.
-template <int NL, bool TAIL = true>
+template <int NL>
 __device__ __forceinline__ void fused_accumulate(uint32_t n, uint32_t i0, uint32_t sh, uint4 (&mb)[NL - 1],
                                                  const int4 &nq, uint4 (&macc)[NL - 1], uint4 &acc)
 {
-    if (TAIL && i0 + 4 > n) {
+    if (i0 + 4 > n) {
 #pragma unroll
         for (int f = 0; f < NL - 1; ++f) {
             mb[f].x = i0 < n ? mb[f].x : 0u;
@@ -1227,7 +1099,7 @@ __device__ __forceinline__ void fused_accumulate(uint32_t n, uint32_t i0, uint32
     acc.w += (uint32_t)nq.w << sh;
 }
 
-template <int NL, int VAR, bool TAIL = true, typename DR>
+template <int NL, int VAR, typename DR>
 __device__ __forceinline__ void fused_plane_d(const float4 &v, uint32_t n, uint32_t i0, const DivNorm &dv,
                                               uint32_t lo2, const LevelsArg &lv, const MsFastArg &fa, const DR &dr,
                                               uint32_t bitP, uint32_t sh, uint4 (&macc)[NL - 1], uint4 &acc,
@@ -1242,7 +1114,7 @@ __device__ __forceinline__ void fused_plane_d(const float4 &v, uint32_t n, uint3
         fused_quad_fast<NL, VAR>(v, q01, q23, fa, dr, bitP, mb, nq);
     else
         fused_quad_slow<NL, VAR>(v, dv, lv, dr, bitP, mb, nq, qmax);
-    fused_accumulate<NL, TAIL>(n, i0, sh, mb, nq, macc, acc);
+    fused_accumulate<NL>(n, i0, sh, mb, nq, macc, acc);
 }
 
 template <int KIND, int NL, int VAR>
@@ -1367,13 +1239,6 @@ __global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1(con
 // bit for bit: the per-element arithmetic is the same code (mask_plane_d,
 // fused_plane_d, select_lanes), only the draws are shared.
 // ---------------------------------------------------------------------------
-// a compile-time tail flag for generic lambdas (TailTag<false>: the wave's
-// whole tile is below n, no per-lane tail checks)
-template <bool B>
-struct TailTag {
-    static constexpr bool value = B;
-};
-
 // the octet at element i0 (i0 % 8 == 0): 0 past n
 __device__ __forceinline__ void load8_nt(const float *__restrict__ x, uint32_t i0, uint32_t n, float4 &v0, float4 &v1)
 {
@@ -1406,27 +1271,23 @@ __global__ GC_MS_OCC __launch_bounds__(kBlock) void k_ms_mask_fast_o2(const floa
     for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < octs; tb += gridDim.x * kMsQuadsPerBlock) {
         const uint32_t t = tb + lane;
         uint4 acc[2] = {};
-        // TL: TailTag<true> (per-lane tail checks) or TailTag<false> (the
-        // wave's 64 octets of this plane are all below n: wave-uniform)
-        auto plane = [&](auto TL, uint32_t p, uint32_t i0, const float4 (&v)[2], const uint4 (&d)[2][2],
-                         bool utail = true) {
-            constexpr bool TAIL = decltype(TL)::value;
+        // utail = false: the wave's 64 octets of this plane are all below n
+        // (wave-uniform), so no per-lane tail tests (MSV_UFLAG)
+        auto plane = [&](uint32_t p, uint32_t i0, const float4 (&v)[2], const uint4 (&d)[2][2], bool utail) {
 #pragma unroll
             for (int hq = 0; hq < 2; ++hq) {
                 const uint32_t iq = i0 + 4u * hq;
-                if (TAIL && hq == 1 && utail && iq >= n)
+                if (hq == 1 && utail && iq >= n)
                     break;
                 uint4 mb[1];
                 if constexpr (CBY != 0) {
                     uint4 cv;
-                    mask_plane_d<2, VAR, true, TAIL>(v[hq], n, iq, dv, lo2, hi2, lv, fa,
-                                                     [&](int l) { return d[l][hq]; }, 1u << (p * w), mb, cq, cb, &cv,
-                                                     utail);
-                    cache_store<CBY, TAIL>(cache, iq, n, cv, utail);
+                    mask_plane_d<2, VAR, true>(v[hq], n, iq, dv, lo2, hi2, lv, fa, [&](int l) { return d[l][hq]; },
+                                               1u << (p * w), mb, cq, cb, &cv, utail);
+                    cache_store<CBY>(cache, iq, n, cv, utail);
                 } else {
-                    mask_plane_d<2, VAR, false, TAIL>(v[hq], n, iq, dv, lo2, hi2, lv, fa,
-                                                      [&](int l) { return d[1][hq]; }, 1u << (p * w), mb, 0, 0,
-                                                      nullptr, utail);
+                    mask_plane_d<2, VAR, false>(v[hq], n, iq, dv, lo2, hi2, lv, fa, [&](int l) { return d[1][hq]; },
+                                                1u << (p * w), mb, 0, 0, nullptr, utail);
                 }
                 acc[hq].x |= mb[0].x;
                 acc[hq].y |= mb[0].y;
@@ -1434,89 +1295,34 @@ __global__ GC_MS_OCC __launch_bounds__(kBlock) void k_ms_mask_fast_o2(const floa
                 acc[hq].w |= mb[0].w;
             }
         };
-        auto load = [&](auto TL, uint32_t i0, float4 (&v)[2]) {
-            if constexpr (decltype(TL)::value) {
+        const bool tile_full = tb + kMsQuadsPerBlock <= octs;
+#pragma unroll
+        for (int j = 0; j < ((VAR & MSV_ROLL) ? 1 : PW); ++j) {
+#pragma unroll 1
+        for (int j1 = 0; j1 < ((VAR & MSV_ROLL) ? PW : 1); ++j1) {
+            const uint32_t p = wave + 4u * (j + j1);
+            const uint32_t pb = p * M + 8u * tb;  // the wave's first octet (uniform)
+            if (p >= (uint32_t)LM || pb >= n)
+                break;
+            const uint32_t i0 = pb + 8u * lane;
+            if (t >= octs || i0 >= n)
+                continue;
+            // the tail tests behind a wave-uniform flag (MSV_UFLAG), else per lane
+            const bool tl = (VAR & MSV_UFLAG) == 0 || !(tile_full && pb + 8u * kMsQuadsPerBlock <= n);
+            float4 v[2];
+            if (tl) {
                 load8_nt(x, i0, n, v[0], v[1]);
             } else {
                 v[0] = ld_nt(reinterpret_cast<const float4 *>(x + i0));
                 v[1] = ld_nt(reinterpret_cast<const float4 *>(x + i0 + 4));
             }
-        };
-        auto draws = [&](uint32_t i0, uint4 (&d)[2][2]) {
+            uint4 d[2][2];
             if constexpr (CBY != 0)
                 ms2_octet(rng, i0 >> 3, d);
             else
                 ms2_octet_level(rng, i0 >> 3, 1, d[1]);
-        };
-        const bool tile_full = tb + kMsQuadsPerBlock <= octs;
-        if constexpr ((VAR & MSV_PAIR) != 0) {
-            // two planes per trip (wave + 4 j, wave + 4 (j + 1)), both octets'
-            // Philox blocks together; in the tail form an invalid second
-            // plane re-reads the first's octet and is not used
-#pragma unroll 1
-            for (int j = 0; j < PW; j += 2) {
-                const uint32_t p = wave + 4u * j, p2 = p + 4u;
-                const uint32_t pb = p * M + 8u * tb;  // the wave's first octet (uniform)
-                if (p >= (uint32_t)LM || pb >= n)
-                    break;
-                const uint32_t i0 = pb + 8u * lane;
-                if (tile_full && p2 < (uint32_t)LM && pb + 4u * M + 8u * kMsQuadsPerBlock <= n) {
-                    float4 v[2][2];
-                    load(TailTag<false>(), i0, v[0]);
-                    load(TailTag<false>(), i0 + 4u * M, v[1]);
-                    uint4 d[2][2][2];
-                    draws(i0, d[0]);
-                    draws(i0 + 4u * M, d[1]);
-                    plane(TailTag<false>(), p, i0, v[0], d[0]);
-                    plane(TailTag<false>(), p2, i0 + 4u * M, v[1], d[1]);
-                } else if (t < octs && i0 < n) {
-                    const bool two = p2 < (uint32_t)LM && i0 + 4u * M < n;
-                    const uint32_t i1 = two ? i0 + 4u * M : i0;
-                    float4 v[2][2];
-                    load(TailTag<true>(), i0, v[0]);
-                    load(TailTag<true>(), i1, v[1]);
-                    uint4 d[2][2][2];
-                    draws(i0, d[0]);
-                    draws(i1, d[1]);
-                    plane(TailTag<true>(), p, i0, v[0], d[0]);
-                    if (two)
-                        plane(TailTag<true>(), p2, i1, v[1], d[1]);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < ((VAR & MSV_ROLL) ? 1 : PW); ++j) {
-#pragma unroll 1
-            for (int j1 = 0; j1 < ((VAR & MSV_ROLL) ? PW : 1); ++j1) {
-                const uint32_t p = wave + 4u * (j + j1);
-                const uint32_t pb = p * M + 8u * tb;
-                if (p >= (uint32_t)LM || pb >= n)
-                    break;
-                const uint32_t i0 = pb + 8u * lane;
-                float4 v[2];
-                uint4 d[2][2];
-                if constexpr ((VAR & MSV_UFLAG) != 0) {
-                    // one code path; the tail checks behind a wave-uniform flag
-                    const bool tl = !(tile_full && pb + 8u * kMsQuadsPerBlock <= n);
-                    if (t < octs && i0 < n) {
-                        if (tl)
-                            load(TailTag<true>(), i0, v);
-                        else
-                            load(TailTag<false>(), i0, v);
-                        draws(i0, d);
-                        plane(TailTag<true>(), p, i0, v, d, tl);
-                    }
-                } else if ((VAR & MSV_FULLDUP) != 0 && tile_full && pb + 8u * kMsQuadsPerBlock <= n) {
-                    load(TailTag<false>(), i0, v);
-                    draws(i0, d);
-                    plane(TailTag<false>(), p, i0, v, d);
-                } else if (t < octs && i0 < n) {
-                    load(TailTag<true>(), i0, v);
-                    draws(i0, d);
-                    plane(TailTag<true>(), p, i0, v, d);
-                }
-            }
-            }
+            plane(p, i0, v, d, tl);
+        }
         }
         if (wave) {
             part[wave - 1][0][lane] = acc[0];
@@ -1638,58 +1444,6 @@ __global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1_o2(
                 }
             };
             float4 vn[2];
-            if constexpr ((VAR & MSV_PAIR) != 0) {
-                // planes k and k + 1 per trip: both loads, then both octets'
-                // Philox blocks in one basic block (the scheduler interleaves
-                // the 6 chains), then each plane's math.  The second plane of
-                // an odd tail is loaded guarded (zeros past n) and not used.
-                float4 vp[2][2];
-                if constexpr ((VAR & MSV_PREFETCH) != 0) {
-                    if (kend > 0) {
-                        load(0, i0, vp[0]);
-                        load(1, i0 + step, vp[1]);
-                    }
-                }
-#pragma unroll 1
-                for (uint32_t k = 0; k < kend; k += 2) {
-                    float4 v[2][2];
-                    if constexpr ((VAR & MSV_PREFETCH) != 0) {
-#pragma unroll
-                        for (int u = 0; u < 2; ++u) {
-                            v[u][0] = vp[u][0];
-                            v[u][1] = vp[u][1];
-                        }
-                        if (k + 2 < kend) {
-                            load(k + 2, i0 + 2u * step, vp[0]);
-                            load(k + 3, i0 + 3u * step, vp[1]);
-                        }
-                    } else {
-                        load(k, i0, v[0]);
-                        load(k + 1, i0 + step, v[1]);
-                    }
-                    uint4 d[2][2][2];
-                    ms2_octet(rng, i0 >> 3, d[0]);
-                    ms2_octet(rng, (i0 + step) >> 3, d[1]);
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        if (u == 1 && k + 1 >= kend)
-                            break;
-                        const uint32_t bitP = 1u << (h + r * (k + u)), sh = (k + u) * wq;
-                        auto quads = [&](auto TL) {
-#pragma unroll
-                            for (int hq = 0; hq < 2; ++hq)
-                                fused_plane_d<2, VAR, decltype(TL)::value>(
-                                    v[u][hq], n, i0 + u * step + 4u * hq, dv, lo2, lv, fa,
-                                    [&](int l) { return d[u][l][hq]; }, bitP, sh, macc[hq], acc[hq], qmax);
-                        };
-                        if ((VAR & MSV_FULLDUP) != 0 && k + u < kfull)  // a full plane (uniform)
-                            quads(TailTag<false>());
-                        else
-                            quads(TailTag<true>());
-                    }
-                    i0 += 2u * step;
-                }
-            } else {
             if constexpr ((VAR & MSV_PREFETCH) != 0) {
                 if (kend > 0)
                     load(0, i0, vn);
@@ -1708,19 +1462,11 @@ __global__ GC_MS_OCC __launch_bounds__(64 * kMsFusedMaxR) void k_ms_fused_w1_o2(
                 uint4 d[2][2];
                 ms2_octet(rng, i0 >> 3, d);
                 const uint32_t bitP = 1u << (h + r * k), sh = k * wq;
-                auto quads = [&](auto TL) {
 #pragma unroll
-                    for (int hq = 0; hq < 2; ++hq)
-                        fused_plane_d<2, VAR, decltype(TL)::value>(v[hq], n, i0 + 4u * hq, dv, lo2, lv, fa,
-                                                                   [&](int l) { return d[l][hq]; }, bitP, sh,
-                                                                   macc[hq], acc[hq], qmax);
-                };
-                if ((VAR & MSV_FULLDUP) != 0 && k < kfull)  // a full plane: no per-lane tail checks (uniform)
-                    quads(TailTag<false>());
-                else
-                    quads(TailTag<true>());
+                for (int hq = 0; hq < 2; ++hq)
+                    fused_plane_d<2, VAR>(v[hq], n, i0 + 4u * hq, dv, lo2, lv, fa, [&](int l) { return d[l][hq]; },
+                                          bitP, sh, macc[hq], acc[hq], qmax);
                 i0 += step;
-            }
             }
         }
         if (t < octs) {
@@ -1812,55 +1558,8 @@ __global__ __launch_bounds__(kBlock) void k_ms_decode_fast(const uint32_t *__res
             if (i0 >= n)
                 break;
             decode_plane<ORDER, NL, (VAR & MSV_PLAINST) == 0>(
-                wd, p * wq, msk, sub, mask_levels4_fast<NL, (VAR & MSV_NTMASK) != 0>(mk, fd, i0), norm, lv, fa, c,
+                wd, p * wq, msk, sub, mask_levels4_fast<NL>(mk, fd, i0), norm, lv, fa, c,
                 mk0, alpha, out, i0, n);
-        }
-    }
-}
-
-// the same with Q adjacent word quads per lane (Q x 16-byte word loads, Q
-// float4 stores per plane in flight per lane; Mq % (4 Q) == 0)
-template <int LQ, int ORDER, int NL, int Q>
-__global__ __launch_bounds__(kBlock) void k_ms_decode_fast_oq(const uint32_t *__restrict__ words, MaskArg mk,
-                                                              FastDiv fd, uint32_t n, const float *__restrict__ normp,
-                                                              LevelsArg lv, MsFastArg fa, uint32_t Mq, uint32_t wq,
-                                                              int32_t sub, float alpha, float *__restrict__ out)
-{
-    const float norm = *normp;
-    float c[GC_MAX_LEVELS] = {};
-#pragma unroll
-    for (int l = 0; l < NL; ++l)
-        c[l] = ORDER == 1 ? norm / lv.s[l] : 0.0f;
-    const bool mk0 = norm >= 0x1p-100f && norm <= 0x1p100f;
-    const uint32_t msk = (1u << wq) - 1u;
-    const uint32_t units = Mq / (4u * Q);
-    constexpr int PW = (LQ + 3) / 4;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    for (uint32_t tb = blockIdx.x * kMsQuadsPerBlock; tb < units; tb += gridDim.x * kMsQuadsPerBlock) {
-        const uint32_t t = tb + lane;
-        if (t >= units)
-            continue;
-        uint4 wd[Q];
-#pragma unroll
-        for (int h = 0; h < Q; ++h)
-            wd[h] = *reinterpret_cast<const uint4 *>(words + 4u * Q * t + 4u * h);
-#pragma unroll
-        for (int j = 0; j < PW; ++j) {
-            const uint32_t p = wave + 4u * j;
-            if (p >= (uint32_t)LQ)
-                break;
-            const uint32_t i0 = p * Mq + 4u * Q * t;
-            if (i0 >= n)
-                break;
-            uint4 m[Q];
-#pragma unroll
-            for (int h = 0; h < Q; ++h)
-                m[h] = mask_levels4_fast<NL>(mk, fd, i0 + 4u * h);
-#pragma unroll
-            for (int h = 0; h < Q; ++h)
-                if (h == 0 || i0 + 4u * h < n)
-                    decode_plane<ORDER, NL>(wd[h], p * wq, msk, sub, m[h], norm, lv, fa, c, mk0, alpha, out,
-                                            i0 + 4u * h, n);
         }
     }
 }

@@ -325,60 +325,6 @@ int main(int argc, char **argv)
         }), 8.0 * n + 4.0 * M);
     row("product gc_qsgd_decode", T.run([&] { gc_qsgd_decode(words, nullptr, n, norm, bits, &ln, 1.0f, dec, nullptr); }),
         4.0 * n + 4.0 * M);
-    {
-        // absmax -> encode step with the absmax walking x from its end (REV),
-        // temporal or NT loads, so that x's front stays in the Infinity Cache
-        // for the encode (which starts there): both launches, one step
-        RngArgs ra0{42, 0, nullptr, n};
-        const unsigned eg = std::min<unsigned>((unsigned)((M / 4 + 255) / 256), 12288u);
-        auto encp = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(eg), dim3(256), 0, 0, x, (const int64_t *)nullptr, n, norm, 15.0f, 15,
-                               ln.bits, (uint64_t)M, ra0, words2);
-        };
-        auto amx = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(512), dim3(1024), 0, 0, x, (const int64_t *)nullptr, n, (uint32_t *)norm,
-                               (uint32_t *)ws);
-        };
-        constexpr int EP = ENC_INT | ENC_NT | ENC_NTS, ET = ENC_INT | ENC_NTS;
-        for (int rep = 0; rep < 3; ++rep) {
-            row("step: absmax NT fwd + encode NT (product form)", T.run([&] {
-                    amx(k_absmax<0, true, 1024, 4, true, 16, false>);
-                    encp(k_qsgd_encode<6, 0, 0, EP>);
-                }), 8.0 * n + 4.0 * M);
-            row("step: absmax NT REV + encode NT", T.run([&] {
-                    amx(k_absmax<0, true, 1024, 4, true, 16, true>);
-                    encp(k_qsgd_encode<6, 0, 0, EP>);
-                }), 8.0 * n + 4.0 * M);
-            row("step: absmax temporal REV + encode NT", T.run([&] {
-                    amx(k_absmax<0, true, 1024, 4, false, 16, true>);
-                    encp(k_qsgd_encode<6, 0, 0, EP>);
-                }), 8.0 * n + 4.0 * M);
-            row("step: absmax temporal REV + encode temporal", T.run([&] {
-                    amx(k_absmax<0, true, 1024, 4, false, 16, true>);
-                    encp(k_qsgd_encode<6, 0, 0, ET>);
-                }), 8.0 * n + 4.0 * M);
-            row("step: absmax temporal fwd + encode temporal", T.run([&] {
-                    amx(k_absmax<0, true, 1024, 4, false, 16, false>);
-                    encp(k_qsgd_encode<6, 0, 0, ET>);
-                }), 8.0 * n + 4.0 * M);
-            row("alone: absmax temporal REV", T.run([&] { amx(k_absmax<0, true, 1024, 4, false, 16, true>); }),
-                4.0 * n);
-            row("alone: encode NT (product form)", T.run([&] { encp(k_qsgd_encode<6, 0, 0, EP>); }), 4.0 * n + 4.0 * M);
-        }
-        // every form gives the product's words
-        std::vector<uint32_t> ha(M), hb(M);
-        amx(k_absmax<0, true, 1024, 4, false, 16, true>);
-        encp(k_qsgd_encode<6, 0, 0, ET>);
-        CK(hipDeviceSynchronize());
-        CK(hipMemcpy(hb.data(), words2, (size_t)M * 4, hipMemcpyDeviceToHost));
-        amx(k_absmax<0, true, 1024, 4, true, 16, false>);
-        encp(k_qsgd_encode<6, 0, 0, EP>);
-        CK(hipDeviceSynchronize());
-        CK(hipMemcpy(ha.data(), words2, (size_t)M * 4, hipMemcpyDeviceToHost));
-        printf("step forms equal: %s\n", ha == hb ? "yes" : "NO");
-    }
-    if (getenv("LAB_STEP_ONLY"))
-        return 0;
 
     RngArgs ra{42, 0, nullptr, n};
     const float s = 15.0f;

@@ -361,42 +361,9 @@ int main(int argc, char **argv)
     cmp("cache cells per-quad dense", cache, cache2, (size_t)n * cby);
     p_selc();
     cmp("select from cache", wq, wq2, (size_t)Mq * 4);
-    // the select from the cache with 2 / 4 quads per lane (k_ms_select_cache_oq)
-    auto selq = [&](auto kern, uint32_t Q, uint32_t *dst) {
-        return [=] {
-            hipLaunchKernelGGL(kern, dim3((Mq / (4 * Q) + 63) / 64), dim3(256), 0, 0, (const void *)cache, n32, mk, fd,
-                               Mq, ql.bits, 3u, dst);
-        };
-    };
-    CK(hipMemset(wq3, 0, (size_t)Mq * 4));
-    selq(k_ms_select_cache_oq<10, 2, 1, 2>, 2, wq3)();
-    cmp("select from cache oq Q=2", wq2, wq3, (size_t)Mq * 4);
-    const bool q4 = Mq % 16 == 0;
-    if (q4) {
-        CK(hipMemset(wq3, 0, (size_t)Mq * 4));
-        selq(k_ms_select_cache_oq<10, 2, 1, 4>, 4, wq3)();
-        cmp("select from cache oq Q=4", wq2, wq3, (size_t)Mq * 4);
-    } else {
-        printf("Mq %% 16 != 0: no Q=4 select\n");
-    }
-    // the decode with 2 / 4 quads per lane (k_ms_decode_fast_oq) == the product's
-    auto decq = [&](auto kern, uint32_t Q, float *dst) {
-        return [=] {
-            hipLaunchKernelGGL(kern, dim3((Mq / (4 * Q) + 63) / 64), dim3(256), 0, 0, wq, mk, fd, n32, norm, la, fa, Mq,
-                               ql.bits, sub, 1.0f, dst);
-        };
-    };
     CK(hipMemset(out2, 0, n * 4));
     v_dec(k_ms_decode_fast<10, 0, 2, MSV_PLAINST>, out2)();
     cmp("decode plain stores", out, out2, n * 4);
-    CK(hipMemset(out2, 0, n * 4));
-    decq(k_ms_decode_fast_oq<10, 0, 2, 2>, 2, out2)();
-    cmp("decode oq Q=2", out, out2, n * 4);
-    if (q4) {
-        CK(hipMemset(out2, 0, n * 4));
-        decq(k_ms_decode_fast_oq<10, 0, 2, 4>, 4, out2)();
-        cmp("decode oq Q=4", out, out2, n * 4);
-    }
     p_w1();
     cmp("one-pass mask == two-pass", mw, mw3, (size_t)Mm * 4);
     cmp("one-pass words == two-pass", wq, wq3, (size_t)Mq * 4);
@@ -404,25 +371,6 @@ int main(int argc, char **argv)
     cmp("one-pass no-prefetch words", wq, wq3, (size_t)Mq * 4);
     w1(k_ms_fused_w1<2, 2, MSV_EAGER0, 2>, g4(Mm))();
     cmp("one-pass per-quad dense words", wq, wq3, (size_t)Mq * 4);
-    // two planes per trip (MSV_PAIR): outputs equal the product's
-    CK(hipMemset(mw3, 0, (size_t)Mm * 4));
-    CK(hipMemset(wq3, 0, (size_t)Mq * 4));
-    w1(k_ms_fused_w1_o2<MSV_PAIR>, g8(Mm))();
-    cmp("one-pass PAIR mask", mw, mw3, (size_t)Mm * 4);
-    cmp("one-pass PAIR words", wq, wq3, (size_t)Mq * 4);
-    CK(hipMemset(mw3, 0, (size_t)Mm * 4));
-    CK(hipMemset(wq3, 0, (size_t)Mq * 4));
-    w1(k_ms_fused_w1_o2<MSV_PAIR | MSV_PREFETCH>, g8(Mm))();
-    cmp("one-pass PAIR PREFETCH mask", mw, mw3, (size_t)Mm * 4);
-    cmp("one-pass PAIR PREFETCH words", wq, wq3, (size_t)Mq * 4);
-    CK(hipMemset(mw2, 0, (size_t)Mm * 4));
-    CK(hipMemset(cache2, 0, (size_t)n * cby));
-    mask8(k_ms_mask_fast_o2<32, MSV_PAIR, 1>, mw2, cache2)();
-    cmp("cached mask PAIR", mw, mw2, (size_t)Mm * 4);
-    cmp("cache cells PAIR", cache, cache2, (size_t)n * cby);
-    CK(hipMemset(mw2, 0, (size_t)Mm * 4));
-    mask8(k_ms_mask_fast_o2<32, MSV_PAIR, 0>, mw2, nullptr)();
-    cmp("mask PAIR", mw, mw2, (size_t)Mm * 4);
     // the tail forms of the cached mask (cells and mask words equal the product's)
     auto cmpmask = [&](const char *nm, auto kern) {
         CK(hipMemset(mw2, 0, (size_t)Mm * 4));
@@ -435,24 +383,10 @@ int main(int argc, char **argv)
         cmp(b2, cache, cache2, (size_t)n * cby);
     };
     cmpmask("ROLL", k_ms_mask_fast_o2<32, MSV_ROLL, 1>);
-    cmpmask("ROLL FULLDUP", k_ms_mask_fast_o2<32, MSV_ROLL | MSV_FULLDUP, 1>);
     cmpmask("ROLL UFLAG", k_ms_mask_fast_o2<32, MSV_ROLL | MSV_UFLAG, 1>);
     CK(hipMemset(mw2, 0, (size_t)Mm * 4));
     mask8(k_ms_mask_fast_o2<32, MSV_ROLL | MSV_UFLAG, 0>, mw2, nullptr)();
     cmp("mask ROLL UFLAG", mw, mw2, (size_t)Mm * 4);
-    for (auto kv : {std::make_pair("PREFETCH FULLDUP", 0), std::make_pair("PAIR PREFETCH FULLDUP", 1)}) {
-        CK(hipMemset(mw3, 0, (size_t)Mm * 4));
-        CK(hipMemset(wq3, 0, (size_t)Mq * 4));
-        if (kv.second == 0)
-            w1(k_ms_fused_w1_o2<MSV_PREFETCH | MSV_FULLDUP>, g8(Mm))();
-        else
-            w1(k_ms_fused_w1_o2<MSV_PAIR | MSV_PREFETCH | MSV_FULLDUP>, g8(Mm))();
-        char b1[96], b2[96];
-        snprintf(b1, sizeof b1, "one-pass %s mask", kv.first);
-        snprintf(b2, sizeof b2, "one-pass %s words", kv.first);
-        cmp(b1, mw, mw3, (size_t)Mm * 4);
-        cmp(b2, wq, wq3, (size_t)Mq * 4);
-    }
 
     // ---- settled interleaved A/B ----
     Timer T;
@@ -484,30 +418,14 @@ int main(int argc, char **argv)
     vs.push_back({"mask + cache per-quad dense", mask4(k_ms_mask_fast<32, 2, 2, 0, 1>, mw2, cache2), xb + mb + cbytes, {}});
     vs.push_back({"mask + cache per-quad KIND0 (r03)", mask4(k_ms_mask_fast<32, 0, 2, 0, 1>, mw2, cache2), xb + mb + cbytes, {}});
     vs.push_back({"product select from cache", p_selc, cbytes + mb + qb, {}});
-    vs.push_back({"lab select from cache oq Q=2", selq(k_ms_select_cache_oq<10, 2, 1, 2>, 2, wq3), cbytes + mb + qb, {}});
-    if (q4)
-        vs.push_back({"lab select from cache oq Q=4", selq(k_ms_select_cache_oq<10, 2, 1, 4>, 4, wq3), cbytes + mb + qb,
-                      {}});
     vs.push_back({"product one-pass W=1 (octet)", p_w1, xb + mb + qb, {}});
     // the product's octet configurations compiled into the lab (GC_MS_WPE builds pin their occupancy)
     vs.push_back({"lab one-pass octet PREFETCH", w1(k_ms_fused_w1_o2<MSV_PREFETCH>, g8(Mm)), xb + mb + qb, {}});
     vs.push_back({"lab mask + cache octet ROLL", mask8(k_ms_mask_fast_o2<32, MSV_ROLL, 1>, mw2, cache2),
                   xb + mb + cbytes, {}});
     vs.push_back({"lab select octet ROLL", sel(k_ms_select_fast_o2<10, MSV_ROLL>, g8(Mq), wq2), xb + mb + qb, {}});
-    vs.push_back({"lab one-pass octet PAIR", w1(k_ms_fused_w1_o2<MSV_PAIR>, g8(Mm)), xb + mb + qb, {}});
-    vs.push_back({"lab one-pass octet PAIR PREFETCH", w1(k_ms_fused_w1_o2<MSV_PAIR | MSV_PREFETCH>, g8(Mm)),
-                  xb + mb + qb, {}});
-    vs.push_back({"lab mask + cache octet PAIR", mask8(k_ms_mask_fast_o2<32, MSV_PAIR, 1>, mw2, cache2),
-                  xb + mb + cbytes, {}});
-    vs.push_back({"lab mask + cache octet ROLL FULLDUP",
-                  mask8(k_ms_mask_fast_o2<32, MSV_ROLL | MSV_FULLDUP, 1>, mw2, cache2), xb + mb + cbytes, {}});
     vs.push_back({"lab mask + cache octet ROLL UFLAG",
                   mask8(k_ms_mask_fast_o2<32, MSV_ROLL | MSV_UFLAG, 1>, mw2, cache2), xb + mb + cbytes, {}});
-    vs.push_back({"lab one-pass octet PREFETCH FULLDUP", w1(k_ms_fused_w1_o2<MSV_PREFETCH | MSV_FULLDUP>, g8(Mm)),
-                  xb + mb + qb, {}});
-    vs.push_back({"lab one-pass octet PAIR PREFETCH FULLDUP",
-                  w1(k_ms_fused_w1_o2<MSV_PAIR | MSV_PREFETCH | MSV_FULLDUP>, g8(Mm)), xb + mb + qb, {}});
-    vs.push_back({"lab mask octet PAIR", mask8(k_ms_mask_fast_o2<32, MSV_PAIR, 0>, mw2, nullptr), xb + mb, {}});
     vs.push_back({"lab mask octet ROLL", mask8(k_ms_mask_fast_o2<32, MSV_ROLL, 0>, mw2, nullptr), xb + mb, {}});
     vs.push_back({"lab mask octet ROLL UFLAG", mask8(k_ms_mask_fast_o2<32, MSV_ROLL | MSV_UFLAG, 0>, mw2, nullptr),
                   xb + mb, {}});
@@ -515,9 +433,6 @@ int main(int argc, char **argv)
     vs.push_back({"one-pass per-quad dense EAGER0 U2", w1(k_ms_fused_w1<2, 2, MSV_EAGER0, 2>, g4(Mm)), xb + mb + qb, {}});
     vs.push_back({"one-pass per-quad KIND0 EAGER0 U2 (r03)", w1(k_ms_fused_w1<0, 2, MSV_EAGER0, 2>, g4(Mm)), xb + mb + qb, {}});
     vs.push_back({"product decode order 0", p_dec(0), xb + mb + qb, {}});
-    vs.push_back({"lab decode Q=2", decq(k_ms_decode_fast_oq<10, 0, 2, 2>, 2, out2), xb + mb + qb, {}});
-    if (q4)
-        vs.push_back({"lab decode Q=4", decq(k_ms_decode_fast_oq<10, 0, 2, 4>, 4, out2), xb + mb + qb, {}});
     vs.push_back({"roof: write 4n (NT float4)", [&] {
                       hipLaunchKernelGGL(k_write_nt, dim3(4096), dim3(256), 0, 0, (float4 *)out2, n / 4);
                   }, xb, {}});
@@ -569,14 +484,6 @@ int main(int argc, char **argv)
     vs.push_back({"seq: one-pass + decode (lab launch) of its own words", [&] {
                       p_w1();
                       decv(k_ms_decode_fast<10, 1, 2, 0>);
-                  }, 0, {}});
-    vs.push_back({"seq: one-pass + decode NT mask loads of its own words", [&] {
-                      p_w1();
-                      decv(k_ms_decode_fast<10, 1, 2, MSV_NTMASK>);
-                  }, 0, {}});
-    vs.push_back({"seq: one-pass plain + decode NT mask loads of its own words", [&] {
-                      w1(k_ms_fused_w1_o2<MSV_PREFETCH | MSV_PLAINST>, g8(Mm))();
-                      decv(k_ms_decode_fast<10, 1, 2, MSV_NTMASK>);
                   }, 0, {}});
     vs.push_back({"seq: one-pass + decode PERTHREAD (words loaded once per lane)", [&] {
                       p_w1();
