@@ -140,12 +140,15 @@ int gc_ms_mask_layout(uint64_t n, const gc_levels *levels, uint32_t world, gc_la
  * by the caller and then reused (self-resetting; one workspace per stream).
  * Hardware assumption of the workspace form: every block stores its partial
  * with an sc1 (agent-coherent, write-through) store, drains it (s_waitcnt
- * vmcnt(0)) and only then takes a relaxed agent-scope ticket; the last block
- * reads the partials with sc1 loads.  This is the fence-free hand-off
- * MI355X_MICROARCH.md measures on gfx950, not an ordering the HIP memory model
- * promises for relaxed atomics (a release/acquire pair emits an L2
- * write-back that doubles the kernel's time).  tests/test_gpu_parity.py::
- * test_absmax_workspace_reuse_many_grids pins it over 1..256-block grids. */
+ * vmcnt(0)) and only then takes a relaxed agent-scope ticket of its group
+ * (block mod 16); each group's last block then takes a top-level ticket, and
+ * the block that draws the last of those reads the partials with sc1 loads.
+ * This is the fence-free hand-off MI355X_MICROARCH.md measures on gfx950,
+ * not an ordering the HIP memory model promises for relaxed atomics (a
+ * release/acquire pair emits an L2 write-back that doubles the kernel's
+ * time; lib/libgcodec_strict.so is the build with that pair,
+ * tests/test_gpu_strict_handoff.py).  tests/test_gpu_parity.py::
+ * test_absmax_workspace_reuse_many_grids pins it over 1..512-block grids. */
 size_t gc_absmax_workspace_size(void);
 int gc_absmax_f32(const float *x, const int64_t *idx, uint64_t n, float *norm, void *workspace,
                   gc_stream_t stream);

@@ -861,11 +861,13 @@ def test_ms_resnet50_bucket_vs_oracle(levels, world):
         assert bits_eq(u32(d), O.ms_dequantize(qsum, norm, levels, common, order, alpha).view(np.uint32)), order
 
 
-@pytest.mark.parametrize("n", [1, 1000, 300_007, 4_000_037, 26_000_011])
+@pytest.mark.parametrize("n", [1, 1000, 65_536, 69_633, 300_007, 1_000_003, 4_000_037, 26_000_011])
 def test_absmax_workspace_reuse_many_grids(n):
-    """The last-block hand-off of k_absmax (sc1 partials + agent-scope ticket,
-    include/gcodec.h) over grids of 1 to 256 blocks, the self-resetting
-    workspace reused 50 times on one stream, every result vs the oracle."""
+    """The last-block hand-off of k_absmax (sc1 partials + two levels of
+    agent-scope tickets, include/gcodec.h) over grids of 1, 16, 17, 74, 245
+    and 512 blocks (groups of one block, full groups, a ragged last group),
+    the self-resetting workspace reused 50 times on one stream, every result
+    vs the oracle."""
     x = O.gen_input(n, seed=n, kind=1)
     x[(n * 7) // 11] = np.float32(-0.75)  # a unique maximum somewhere inside
     xd = dev(x)
