@@ -168,10 +168,8 @@ constexpr uint32_t G1_BLK = 3;                            // 32-position blocks 
 constexpr uint32_t G1_RANGE = G4_SEG * G1_BLK;            // 96 positions per thread
 constexpr uint32_t G1_TILE_MAX = G1_THREADS * G1_RANGE;   // 98,304 positions per block and round
 constexpr uint32_t G1_GMAX = 256;                         // blocks of the persistent grid (<= one per CU)
-constexpr uint32_t G1_LB = 12;                            // 16-byte loads in flight per thread (tile load)
 constexpr uint32_t G1_MIN_TILE = 16384;                   // small buckets: fewer, larger tiles
 constexpr uint64_t G1_TIMEOUT_TICKS = 1ull << 27;         // s_memrealtime (100 MHz): ~1.3 s, then status 4
-static_assert(G1_TILE_MAX / 4 <= 2 * G1_LB * G1_THREADS, "two load batches cover a tile");
 
 // workspace: the header on a line of its own, then the granules (two round
 // parities x G1_GMAX tiles x 16 entries x {entry, tag}), then (lab builds)
@@ -258,30 +256,48 @@ __device__ __forceinline__ uint64_t g1_load_granule(const uint64_t *p)
 #endif
 }
 
+template <uint32_t V>
+struct G1Count {
+    static constexpr uint32_t value = V;
+};
+
+// The bytes of wave w's ranges (positions 96 * 64 w .. + 6144, and the 16
+// after them: the next range's head) into LDS by that wave alone, so a wave
+// starts its recurrence as soon as its own data is in, while the other waves'
+// loads are still in flight (the block-wide load and its barrier: 42.9 us per
+// pack at 23.5 M; per wave: 42.1 us, profiles/r05zn_g4_shapes.csv).  Returns this lane's OR of the values read
+// (the range check: > 255 means a value outside [0, 255]); the caller ORs it
+// over the block at its next barrier.  Two batches of up to 13 / 12 int4
+// loads per lane, all of a batch issued before any is used.
 template <bool ALIGNED>
-__device__ __forceinline__ uint32_t g1_load_tile(G1Smem &sm, const int32_t *__restrict__ src, uint64_t n,
-                                                 uint64_t start, uint32_t C, unsigned t)
+__device__ __forceinline__ uint32_t g1_load_wave(G1Smem &sm, const int32_t *__restrict__ src, uint64_t n,
+                                                 uint64_t start, uint32_t C, unsigned w, unsigned lane)
 {
     typedef int i4v __attribute__((ext_vector_type(4)));
-    const uint32_t QT = C / 4;  // dwords of the tile (C is a multiple of 96)
+    constexpr uint32_t WQ = G1_RANGE / 4 * 64;  // dwords of a wave's ranges (1536)
+    const uint32_t QT = C / 4, qb = WQ * w;
     uint32_t bad = 0;
-    for (uint32_t q0 = 0; q0 < QT + 4; q0 += G1_LB * G1_THREADS) {
-        int4 v[G1_LB];
-        const bool full = ALIGNED && q0 + G1_LB * G1_THREADS <= QT && start + 4ull * (q0 + G1_LB * G1_THREADS) <= n;
-        if (full) {  // uniform: every load in bounds, all issued before any is used
+    if (qb >= QT)
+        return 0;  // no positions in this wave (wave-uniform)
+    const uint32_t qe = min(qb + WQ, QT) + 4u;  // + the 16-position halo
+    auto batch = [&](uint32_t j0, auto NJ) {
+        constexpr uint32_t J = decltype(NJ)::value;
+        int4 v[J];
+        const uint32_t q0 = qb + 64u * j0;
+        const bool full = ALIGNED && q0 + 64u * J <= qe && start + 4ull * (q0 + 64u * J) <= n;
+        if (full) {  // uniform: every load in bounds
 #pragma unroll
-            for (uint32_t j = 0; j < G1_LB; ++j) {
-                const i4v r = __builtin_nontemporal_load(reinterpret_cast<const i4v *>(src + start) + q0 +
-                                                         j * G1_THREADS + t);
+            for (uint32_t j = 0; j < J; ++j) {
+                const i4v r = __builtin_nontemporal_load(reinterpret_cast<const i4v *>(src + start) + q0 + 64u * j + lane);
                 v[j] = make_int4(r.x, r.y, r.z, r.w);
             }
         } else {
 #pragma unroll
-            for (uint32_t j = 0; j < G1_LB; ++j) {
-                const uint32_t q = q0 + j * G1_THREADS + t;
+            for (uint32_t j = 0; j < J; ++j) {
+                const uint32_t q = q0 + 64u * j + lane;
                 const uint64_t g = start + 4ull * q;
                 int4 r = make_int4(0, 0, 0, 0);
-                if (q < QT + 4) {  // the tile and its 16-position halo (the next tile's head)
+                if (q < qe) {
                     if (ALIGNED && g + 4 <= n)
                         r = *reinterpret_cast<const int4 *>(src + g);
                     else if (g < n) {
@@ -295,16 +311,21 @@ __device__ __forceinline__ uint32_t g1_load_tile(G1Smem &sm, const int32_t *__re
             }
         }
 #pragma unroll
-        for (uint32_t j = 0; j < G1_LB; ++j) {
-            const uint32_t q = q0 + j * G1_THREADS + t;
-            if (q < QT + 4) {
+        for (uint32_t j = 0; j < J; ++j) {
+            const uint32_t q = q0 + 64u * j + lane;
+            if (q < qe) {
                 bad |= (uint32_t)v[j].x | (uint32_t)v[j].y | (uint32_t)v[j].z | (uint32_t)v[j].w;
                 sm.v[q] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(v[j].w, v[j].z, 0x0c0c0400u),
                                                 __builtin_amdgcn_perm(v[j].y, v[j].x, 0x0c0c0400u), 0x05040100u);
             }
         }
-    }
-    return __syncthreads_or(bad > 255u);
+    };
+    static_assert(64 * (13 + 12) >= WQ + 4, "two batches cover a wave's ranges and the halo");
+    batch(0, G1Count<13>{});
+    if (qb + 64u * 13 < qe)  // wave-uniform
+        batch(13, G1Count<12>{});
+    wave_lds_sync();  // the wave's lanes read each other's bytes
+    return bad;
 }
 
 // pack one word of mode `mode` from the bytes at tile offset a (zero past n).
@@ -398,8 +419,8 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
         const uint64_t tile_start = ((uint64_t)r * G + b) * C;
         const uint32_t tag = (uint32_t)(seq + r + 1);
         G1_STAMP(0);
-        // 1. the tile's bytes
-        const uint32_t bad = g1_load_tile<ALIGNED>(sm, src, n, tile_start, C, t);
+        // 1. this wave's bytes (the range check is ORed over the block below)
+        const uint32_t badw = g1_load_wave<ALIGNED>(sm, src, n, tile_start, C, w, lane);
         G1_STAMP(1);
         // 2. this thread's table over its 96 positions (identity past the tile)
         const bool in_tile = G1_RANGE * t < C;
@@ -531,7 +552,7 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
             }
             wave_lds_sync();
         }
-        __syncthreads();
+        const uint32_t bad = __syncthreads_or(badw > 255u);
         // 4. the block's tree over the wave roots (wave 0) -> x[1], published
         if (w == 0) {
 #pragma unroll
