@@ -17,6 +17,7 @@
 // Pack: ONE persistent launch, one 1024-thread workgroup per CU (k_g4p_one).
 // Round r, block b owns tile r*G + b (C positions, <= 98,304):
 //   1. the tile's values -> LDS as bytes (+ a 16-byte halo), range check;
+//      loaded by quarters of the block, one after another (g1_load_wave);
 //   2. per thread 96 positions: window classes (SWAR byte tests + OR
 //      doubling), the table by a backward recurrence chained over three
 //      32-position blocks (registers only, static indices);
@@ -42,6 +43,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 
 #ifndef GC_STRICT_HANDOFF
 #define GC_STRICT_HANDOFF 0
@@ -211,6 +213,7 @@ struct G1Smem {
     uint32_t woff[G1_WAVES];                      // each wave's first word within the tile
     uint64_t base_b;                              // the block's word base within the round
     uint32_t s_b, s_end, tw, tile_words;
+    uint32_t stage[G1_WAVES / 4];                 // STAGE: per quarter, its waves whose first batch is in (4 a round)
 };
 // entries of the block's word list: the tree storage, free by then
 constexpr uint32_t G1_WLCAP = (uint32_t)(sizeof(((G1Smem *)nullptr)->k) / 2);
@@ -269,16 +272,44 @@ struct G1Count {
 // (the range check: > 255 means a value outside [0, 255]); the caller ORs it
 // over the block at its next barrier.  Two batches of up to 13 / 12 int4
 // loads per lane, all of a batch issued before any is used.
-template <bool ALIGNED>
+// STAGE: the tile is loaded by quarters (waves 4k .. 4k + 3, one per SIMD).
+// Quarter k issues its loads once quarter k - 1's first batches are in (an LDS
+// count per quarter and round), so the quarters' data arrives one after
+// another and quarter k's recurrence runs while quarters > k still load;
+// unstaged, every wave's loads went out at once and all finished together,
+// near the end of the 13 us load.  Each quarter keeps ~100 KB in flight per
+// CU (its second batches + the next quarter's first), above what the CU's
+// share of HBM needs.  Groups of 2 or 8 waves, or the hand-on after a wave's
+// last batch, or batches of 9 / 8 / 8 were slower (41.0 / 40.2 / 40.5 /
+// 39.1-39.5 against 38.4-38.5 us; issue priorities by quarter (s_setprio)
+// instead of the count: 40.8, no change).  The wait is bounded: it orders
+// the loads and nothing else depends on it.
+template <bool ALIGNED, bool STAGE>
 __device__ __forceinline__ uint32_t g1_load_wave(G1Smem &sm, const int32_t *__restrict__ src, uint64_t n,
-                                                 uint64_t start, uint32_t C, unsigned w, unsigned lane)
+                                                 uint64_t start, uint32_t C, unsigned w, unsigned lane,
+                                                 uint32_t target)
 {
     typedef int i4v __attribute__((ext_vector_type(4)));
     constexpr uint32_t WQ = G1_RANGE / 4 * 64;  // dwords of a wave's ranges (1536)
     const uint32_t QT = C / 4, qb = WQ * w;
     uint32_t bad = 0;
-    if (qb >= QT)
+    const uint32_t quarter = w / 4;
+    auto signal = [&] {  // this wave's first batch is in: the next quarter may issue
+        if (STAGE && lane == 0)
+            __hip_atomic_fetch_add(&sm.stage[quarter], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    if (STAGE && quarter > 0) {  // a performance hint only: bounded, so a late quarter never waits forever
+        for (uint32_t it = 0; it < 4096; ++it) {
+            const uint32_t c = __hip_atomic_load(&sm.stage[quarter - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (__builtin_amdgcn_readfirstlane(c) >= target)
+                break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (qb >= QT) {
+        signal();
         return 0;  // no positions in this wave (wave-uniform)
+    }
     const uint32_t qe = min(qb + WQ, QT) + 4u;  // + the 16-position halo
     auto batch = [&](uint32_t j0, auto NJ) {
         constexpr uint32_t J = decltype(NJ)::value;
@@ -322,6 +353,7 @@ __device__ __forceinline__ uint32_t g1_load_wave(G1Smem &sm, const int32_t *__re
     };
     static_assert(64 * (13 + 12) >= WQ + 4, "two batches cover a wave's ranges and the halo");
     batch(0, G1Count<13>{});
+    signal();
     if (qb + 64u * 13 < qe)  // wave-uniform
         batch(13, G1Count<12>{});
     wave_lds_sync();  // the wave's lanes read each other's bytes
@@ -395,7 +427,7 @@ __device__ __forceinline__ uint32_t g1_modes_present(uint32_t mode, bool active)
 // every block runs all R rounds.  A block waits only for blocks of its own
 // launch; one not yet resident gets a CU once another kernel's blocks leave.
 // A wait longer than G1_TIMEOUT_TICKS ends the call with status 4.
-template <bool ALIGNED>
+template <bool ALIGNED, bool STAGE>
 __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restrict__ src, uint64_t n, uint32_t C,
                                                         uint32_t R, int32_t *__restrict__ out, uint64_t cap,
                                                         uint64_t *__restrict__ nwords, uint32_t *__restrict__ status,
@@ -409,6 +441,11 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
     const uint64_t seq = __hip_atomic_load(&hdr->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t carry_s = 0, bad_all = 0, nospc = 0, tmo = 0;
     uint64_t carry_base = 0;
+    if (STAGE) {
+        if (tid < G1_WAVES / 4)
+            sm.stage[tid] = 0;
+        __syncthreads();
+    }
     for (uint32_t r = 0; r < R; ++r) {
         // the thread index re-made opaque each round, so the many per-thread
         // LDS and global offsets are not hoisted out of the round loop (they
@@ -420,7 +457,7 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
         const uint32_t tag = (uint32_t)(seq + r + 1);
         G1_STAMP(0);
         // 1. this wave's bytes (the range check is ORed over the block below)
-        const uint32_t badw = g1_load_wave<ALIGNED>(sm, src, n, tile_start, C, w, lane);
+        const uint32_t badw = g1_load_wave<ALIGNED, STAGE>(sm, src, n, tile_start, C, w, lane, 4u * (r + 1));
         G1_STAMP(1);
         // 2. this thread's table over its 96 positions (identity past the tile)
         const bool in_tile = G1_RANGE * t < C;
@@ -1047,6 +1084,18 @@ static uint32_t g1_cus(hipStream_t st)
     return (uint32_t)c;
 }
 
+// the staged tile load (k_g4p_one<…, STAGE>): 38.4-38.5 against 40.5 us per
+// xi pack at 23.5 M, 32.8 against 34.8 us for the sign bits
+// (profiles/r05zp_g4_stage.log).  GC_G4_STAGE=0 selects the unstaged form (A/B)
+static bool greedy4_stage()
+{
+    static const bool on = [] {
+        const char *e = getenv("GC_G4_STAGE");
+        return !(e && atol(e) == 0);
+    }();
+    return on;
+}
+
 // the pack's geometry for n positions on `cus` CUs: G blocks, R rounds, C
 // positions per tile (a multiple of 96, <= G1_TILE_MAX), G * R * C >= n
 struct G1Geom {
@@ -1097,12 +1146,11 @@ int gc_greedy4_pack_device(const int32_t *src, uint64_t n, int32_t *out, uint64_
     const G1Geom g = g1_geom(n, g1_cus(st));
     G1Hdr *hdr = reinterpret_cast<G1Hdr *>(workspace);
     uint64_t *gran = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(workspace) + sizeof(G1Hdr));
-    if (aligned16(src))
-        hipLaunchKernelGGL(k_g4p_one<true>, dim3(g.G), dim3(G1_THREADS), 0, st, src, n, g.C, g.R, out, cap, nwords,
-                           status, hdr, gran);
-    else
-        hipLaunchKernelGGL(k_g4p_one<false>, dim3(g.G), dim3(G1_THREADS), 0, st, src, n, g.C, g.R, out, cap, nwords,
-                           status, hdr, gran);
+    const bool al = aligned16(src), stg = greedy4_stage();
+    auto kern = al ? (stg ? k_g4p_one<true, true> : k_g4p_one<true, false>)
+                   : (stg ? k_g4p_one<false, true> : k_g4p_one<false, false>);
+    hipLaunchKernelGGL(kern, dim3(g.G), dim3(G1_THREADS), 0, st, src, n, g.C, g.R, out, cap, nwords, status, hdr,
+                       gran);
     return launch_status("gc_greedy4_pack_device");
 }
 
