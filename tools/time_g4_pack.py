@@ -48,3 +48,18 @@ for name, src in (("xi", xi), ("sign", sg)):
         best.append(e0.elapsed_time(e1) / REPS * 1e3)
     print(f"{env} {name}: words {nw} sha1 {dig}  us/pack best {min(best):.2f} all "
           f"{' '.join(f'{v:.2f}' for v in best)}", flush=True)
+    w = pk.words[:nw].clone()
+    pk.unpack(w)
+    nv = pk.unpack_result()
+    same = bool(nv >= n and torch.equal(pk.values[:n].to(src.dtype), src))
+    best = []
+    for _ in range(LOOPS):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(REPS):
+            pk.unpack(w)
+        e1.record()
+        torch.cuda.synchronize()
+        best.append(e0.elapsed_time(e1) / REPS * 1e3)
+    print(f"{env} {name}: unpack round trip exact {same}  us/unpack best {min(best):.2f} all "
+          f"{' '.join(f'{v:.2f}' for v in best)}", flush=True)
