@@ -865,9 +865,10 @@ def packers_leg(torch, gcodec, codec, dev, gen, rank) -> dict:
     t_d = (time.perf_counter() - t0) / 10 * 1e3
     res["qsgdbp_compress_ms"] = t_c
     res["qsgdbp_decompress_ms"] = t_d
-    res["qsgdbp_note"] = ("compress = absmax + quantize_split + 2 device greedy4 packs + 3 host syncs (norm, word "
-                          "counts); decompress = 2 device greedy4 unpacks (2 host syncs: value counts) + the fused "
-                          "combine (gc_qsgdbp_decode); the reference packs on the host at 0.56 M elem/s (BASELINE.md)")
+    res["qsgdbp_note"] = ("compress = absmax + quantize_split + 2 device greedy4 packs + 2 host syncs (both word "
+                          "counts in one read, then the norm); decompress = 2 device greedy4 unpacks (1 host sync: "
+                          "both value counts) + the fused combine (gc_qsgdbp_decode); the reference packs on the "
+                          "host at 0.56 M elem/s (BASELINE.md)")
     del x, xi, sg, q8, bw, pk
     return res
 

@@ -1415,6 +1415,10 @@ def qsgdbp_decode(sign: torch.Tensor, xi: torch.Tensor, c: torch.Tensor, n: int)
 def _g4_result(res: torch.Tensor, what: str) -> int:
     """(count, status) written by the device packer: one 16-byte D2H read."""
     count, status = (int(v) for v in res.cpu().tolist())
+    return _g4_check(count, status, what)
+
+
+def _g4_check(count: int, status: int, what: str) -> int:
     if status & 1:
         raise _lib.GCodecError(_lib.GC_ERANGE, f"{what}: a value outside [0, 255] (the greedy format's domain)")
     if status & 2:
@@ -1487,6 +1491,81 @@ def greedy4_pack(src: torch.Tensor) -> torch.Tensor:
     nw = check(lib.gc_greedy4_pack(a.ctypes.data_as(C.c_void_p), a.size, out.ctypes.data_as(C.c_void_p),
                                    out.size), "gc_greedy4_pack")
     return torch.from_numpy(out[:nw].copy())
+
+
+_G4_WS = {}  # (device index, stream) -> the pack workspace, zeroed once (every pack leaves it so)
+
+
+def _g4_pack_ws(dev, stream) -> torch.Tensor:
+    key = (dev.index, stream.value)  # stream: the raw HIP stream (_stream)
+    ws = _G4_WS.get(key)
+    if ws is None:
+        ws = _G4_WS[key] = torch.zeros(int(_lib.load().gc_greedy4_workspace_size(0)), dtype=torch.uint8, device=dev)
+    return ws
+
+
+def greedy4_pack_many(*srcs: torch.Tensor) -> list:
+    """greedy4_pack of several arrays with one host synchronisation: on the
+    device every pack is enqueued on the caller's stream (one workspace per
+    stream, zeroed once), then the word counts of all of them come back in one
+    D2H read.  QSGDBPCompressor.compress packs the sign bits and the
+    magnitudes this way (compressors.py:357-358 packs them one after the other
+    on the host).  Host tensors: greedy4_pack each."""
+    if not srcs or not all(t.is_cuda for t in srcs):
+        return [greedy4_pack(t) for t in srcs]
+    dev = _dev(srcs[0])
+    if any(_dev(t) != dev for t in srcs):
+        raise ValueError("greedy4_pack_many: arrays on different devices")
+    lib = _lib.load()
+    st = _stream(dev)
+    ws = _g4_pack_ws(dev, st)
+    res = torch.empty(2 * len(srcs), dtype=torch.int64, device=dev)  # (count, status) per pack, written by each
+    outs, keep = [], []
+    for i, src in enumerate(srcs):
+        a = src.detach().contiguous().view(-1)
+        if a.dtype != torch.int32:
+            a = a.to(torch.int32)
+        keep.append(a)  # alive until the launches are enqueued (the stream orders their use)
+        cap = a.numel() // 3 + 2
+        words = torch.empty(cap, dtype=torch.int32, device=dev)
+        check(lib.gc_greedy4_pack_device(_p(a), a.numel(), _p(words), cap, C.c_void_p(res.data_ptr() + 16 * i),
+                                         C.c_void_p(res.data_ptr() + 16 * i + 8), _p(ws), st),
+              "gc_greedy4_pack_device")
+        outs.append(words)
+    pairs = res.cpu().view(-1, 2).tolist()
+    if any(int(stt) & 4 for _, stt in pairs):
+        _G4_WS.pop((dev.index, st.value), None)  # a timed-out pack: zero it again
+    return [w[:_g4_check(int(c), int(stt), "greedy4_pack")] for w, (c, stt) in zip(outs, pairs)]
+
+
+def greedy4_unpack_many(*words: torch.Tensor) -> list:
+    """greedy4_unpack of several word arrays with one host synchronisation
+    (every unpack enqueued, then all value counts in one D2H read); host
+    tensors: greedy4_unpack each."""
+    if not words or not all(t.is_cuda for t in words):
+        return [greedy4_unpack(t) for t in words]
+    dev = _dev(words[0])
+    if any(_dev(t) != dev for t in words):
+        raise ValueError("greedy4_unpack_many: arrays on different devices")
+    lib = _lib.load()
+    st = _stream(dev)
+    res = torch.empty(2 * len(words), dtype=torch.int64, device=dev)
+    outs, keep = [], []
+    for i, w in enumerate(words):
+        a = w.detach().contiguous().view(-1)
+        if a.dtype != torch.int32:
+            a = a.to(torch.int32)
+        nw = a.numel()
+        cap = 15 * nw
+        out = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+        ws = torch.empty(int(lib.gc_greedy4_unpack_workspace_size(nw)), dtype=torch.uint8, device=dev)
+        keep += [a, ws]  # alive until enqueued: the stream orders their reuse by the allocator
+        check(lib.gc_greedy4_unpack_device(_p(a), nw, _p(out), cap, C.c_void_p(res.data_ptr() + 16 * i),
+                                           C.c_void_p(res.data_ptr() + 16 * i + 8), _p(ws), st),
+              "gc_greedy4_unpack_device")
+        outs.append(out)
+    pairs = res.cpu().view(-1, 2).tolist()
+    return [o[:_g4_check(int(c), int(stt), "greedy4_unpack")] for o, (c, stt) in zip(outs, pairs)]
 
 
 def greedy4_unpack(words: torch.Tensor) -> torch.Tensor:

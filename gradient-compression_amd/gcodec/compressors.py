@@ -133,8 +133,12 @@ class QSGDBPCompressor(_Base):
         norm = self.backend.absmax(tensor)  # compressors.py:341 (the bucket's own max)
         rng = self._reserve(tensor.numel(), 1, tensor.device)
         xi, sign = self.backend.qsgd_quantize_split(tensor, norm, self._quantization_level, rng)
-        sign_packed = self.backend.greedy4_pack(sign)
-        xi_packed = self.backend.greedy4_pack(xi)
+        many = getattr(self.backend, "greedy4_pack_many", None)
+        if many is not None:  # both packs enqueued, one host sync for the two word counts
+            sign_packed, xi_packed = many(sign, xi)
+        else:
+            sign_packed = self.backend.greedy4_pack(sign)
+            xi_packed = self.backend.greedy4_pack(xi)
         xi_size = torch.tensor(xi_packed.size(), device=tensor.device)
         # norm / s, correctly rounded (numpy float32 division; the packers above already synchronised)
         c = torch.tensor(np.float32(norm.item()) / np.float32(s), dtype=torch.float32, device=tensor.device)
@@ -142,8 +146,12 @@ class QSGDBPCompressor(_Base):
 
     def decompress(self, norm, sign_packed, xi_packed, tensor_size):
         n = int(tensor_size)
-        sign = self.backend.greedy4_unpack(sign_packed)
-        xi = self.backend.greedy4_unpack(xi_packed)
+        many = getattr(self.backend, "greedy4_unpack_many", None)
+        if many is not None:  # both unpacks enqueued, one host sync for the two value counts
+            sign, xi = many(sign_packed, xi_packed)
+        else:
+            sign = self.backend.greedy4_unpack(sign_packed)
+            xi = self.backend.greedy4_unpack(xi_packed)
         fused = getattr(self.backend, "qsgdbp_decode", None)
         if fused is not None and xi.is_cuda:
             return fused(sign, xi, norm, n)  # one kernel (gc_qsgdbp_decode)

@@ -103,6 +103,43 @@ def test_qsgdbp_resnet50_bucket_packs_exactly(bits):
         assert torch.equal(u[:n], src)
 
 
+def test_pack_many_equals_one_by_one():
+    """greedy4_pack_many (one host sync for all word counts, the per-stream
+    workspace reused across calls) gives each array the words greedy4_pack
+    gives it: sizes from 1 to a multi-round 3 M, an unaligned slice, an empty
+    array, repeated calls, and a side stream of its own."""
+    rng = np.random.default_rng(12)
+    arrs = [rng.choice([0, 1, 3, 9, 15, 100, 255], m, p=[.3, .2, .15, .15, .1, .05, .05]).astype(np.int32)
+            for m in (1, 15, 4097, 300_001, 3_000_000)]
+    d = [torch.from_numpy(a).to(DEV) for a in arrs]
+    srcs = d + [d[3][1:], torch.empty(0, dtype=torch.int32, device=DEV)]
+    want = [codec.greedy4_pack(t.cpu()).numpy() for t in srcs]
+    for _ in range(3):
+        got = codec.greedy4_pack_many(*srcs)
+        assert len(got) == len(srcs)
+        for g, w in zip(got, want):
+            assert g.is_cuda and np.array_equal(g.cpu().numpy(), w)
+    side = torch.cuda.Stream(DEV)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        got = codec.greedy4_pack_many(d[4], d[2])
+    assert np.array_equal(got[0].cpu().numpy(), want[4]) and np.array_equal(got[1].cpu().numpy(), want[2])
+    host = codec.greedy4_pack_many(srcs[2].cpu(), srcs[3].cpu())  # host tensors: the host packer
+    assert not host[0].is_cuda and np.array_equal(host[1].numpy(), want[3])
+    vals = codec.greedy4_unpack_many(*got, *codec.greedy4_pack_many(*srcs))
+    want_u = [codec.greedy4_unpack(torch.from_numpy(w)).numpy() for w in (want[4], want[2], *want)]
+    assert len(vals) == len(want_u)
+    for v, w in zip(vals, want_u):
+        assert v.is_cuda and np.array_equal(v.cpu().numpy(), w)
+
+
+def test_pack_many_rejects_out_of_domain():
+    ok = torch.tensor([1, 2, 3], dtype=torch.int32, device=DEV)
+    with pytest.raises(gcodec.GCodecError):
+        codec.greedy4_pack_many(ok, torch.tensor([1, 256], dtype=torch.int32, device=DEV))
+    assert np.array_equal(codec.greedy4_pack_many(ok)[0].cpu().numpy(), codec.greedy4_pack(ok.cpu()).numpy())
+
+
 def test_device_packer_unaligned_source():
     """src not 16-byte aligned (a slice at +1 element): the scalar-load path."""
     rng = np.random.default_rng(8)
