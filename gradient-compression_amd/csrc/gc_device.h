@@ -194,15 +194,72 @@ __device__ __forceinline__ void ms2_octet_level(const RngArgs &r, uint64_t g, ui
     }
 }
 
+// ---------------------------------------------------------------------------
+// KIND 4 / 5: split-plane draws (GC_RNG_SPLIT8 / GC_RNG_SPLIT16).  Of each
+// draw only the 24 bits the rounding reads are kept, cut in two planes: the
+// HI plane holds bits 24-HB .. 23 (HB = 8: one byte per draw, 16: two), padded
+// to 16 bytes, then the LO plane holds bits 0 .. 23-HB.  The encode decides
+// [r24 < F] from the HI plane alone unless HI equals the top HB bits of F-1
+// (about 1 draw in 2^HB), and reads the LO plane only for those quads
+// (enc_tile_int_split).  One level; n = the call's draws.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t split_hpad(uint64_t n, uint32_t hb)
+{
+    return (n * (hb / 8) + 15) & ~(uint64_t)15;
+}
+__host__ __device__ __forceinline__ uint64_t split_bytes(uint64_t n, uint32_t hb)
+{
+    return split_hpad(n, hb) + ((n * ((24 - hb) / 8) + 15) & ~(uint64_t)15);
+}
+
+// the full 24-bit draws of quad i0 .. i0+3 (left of them in range) from both planes
+template <uint32_t HB>
+__device__ __forceinline__ uint4 split_quad(const RngArgs &r, uint64_t i0, uint64_t left)
+{
+    const uint8_t *h = reinterpret_cast<const uint8_t *>(r.stream);
+    const uint8_t *l = h + split_hpad(r.n, HB);
+    uint4 d = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t *dp = &d.x;
+    if (left >= 4) {
+        if constexpr (HB == 8) {
+            const uint32_t hq = *reinterpret_cast<const uint32_t *>(h + i0);
+            const uint2 lq = *reinterpret_cast<const uint2 *>(l + 2 * i0);
+            d.x = (hq & 0xFFu) << 16 | (lq.x & 0xFFFFu);
+            d.y = ((hq >> 8) & 0xFFu) << 16 | (lq.x >> 16);
+            d.z = ((hq >> 16) & 0xFFu) << 16 | (lq.y & 0xFFFFu);
+            d.w = (hq >> 24) << 16 | (lq.y >> 16);
+        } else {
+            const uint2 hq = *reinterpret_cast<const uint2 *>(h + 2 * i0);
+            const uint32_t lq = *reinterpret_cast<const uint32_t *>(l + i0);
+            d.x = (hq.x & 0xFFFFu) << 8 | (lq & 0xFFu);
+            d.y = (hq.x >> 16) << 8 | ((lq >> 8) & 0xFFu);
+            d.z = (hq.y & 0xFFFFu) << 8 | ((lq >> 16) & 0xFFu);
+            d.w = (hq.y >> 16) << 8 | (lq >> 24);
+        }
+        return d;
+    }
+    for (uint32_t e = 0; e < (uint32_t)min(left, (uint64_t)4); ++e) {
+        const uint64_t i = i0 + e;
+        if constexpr (HB == 8)
+            dp[e] = (uint32_t)h[i] << 16 | (uint32_t)reinterpret_cast<const uint16_t *>(l)[i];
+        else
+            dp[e] = (uint32_t)reinterpret_cast<const uint16_t *>(h)[i] << 8 | (uint32_t)l[i];
+    }
+    return d;
+}
+
 // Four draws for elements i0..i0+3 (i0 % 4 == 0) at scale `level`.
 // KIND 0: Philox, one block per quad and level; 1: a draw stream; 2: the
 // dense two-level Philox stream above (one or two blocks per quad and level:
 // the generic kernels' path; the octet kernels of ms_fast.h share blocks);
-// 3: a draw stream packed to 24 bits (GC_RNG_STREAM24).
+// 3: a draw stream packed to 24 bits (GC_RNG_STREAM24); 4 / 5: split-plane
+// draws (both planes read: the generic paths; one level).
 template <int KIND, int IMPL = GC_PHILOX_IMPL>
 __device__ __forceinline__ uint4 draws4(const RngArgs &r, uint32_t level, uint64_t i0)
 {
-    if constexpr (KIND == 2) {
+    if constexpr (KIND == 4 || KIND == 5) {
+        return split_quad<KIND == 4 ? 8u : 16u>(r, i0, i0 < r.n ? r.n - i0 : 0);
+    } else if constexpr (KIND == 2) {
         // block numbers stay wave-uniform (philox4x32_10_g keeps y on the
         // scalar unit); the quad half h = bit 2 of i0 is per lane
         const uint64_t g = i0 >> 3;
@@ -271,6 +328,8 @@ __device__ __forceinline__ uint32_t draw1(const RngArgs &r, uint32_t level, uint
         const uint4 d = draws4<KIND>(r, level, i & ~(uint64_t)3);
         const uint32_t j = (uint32_t)(i & 3);
         return j == 0 ? d.x : (j == 1 ? d.y : (j == 2 ? d.z : d.w));
+    } else if constexpr (KIND == 4 || KIND == 5) {
+        return split_quad<KIND == 4 ? 8u : 16u>(r, i, 1).x;
     } else if constexpr (KIND == 3) {
         const uint8_t *b = reinterpret_cast<const uint8_t *>(r.stream) + 3 * ((uint64_t)level * r.n + i);
         return b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16;

@@ -178,7 +178,10 @@ constexpr uint64_t G1_TIMEOUT_TICKS = 1ull << 27;         // s_memrealtime (100 
 // the phase stamps
 struct G1Hdr {
     uint64_t seq;           // tags used so far: round r of a launch tags seq + r + 1
-    uint64_t pad[31];
+    uint32_t done;          // blocks of the running launch that have finished (block 0 re-arms it)
+    uint32_t tmo;           // nonzero: a block of the running launch timed out (block 0 re-arms it)
+    uint64_t test_delay;    // tests only (tests/test_gpu_greedy4.py): block 0 starts this many ticks late
+    uint64_t pad[29];
 };
 static_assert(sizeof(G1Hdr) == 256, "header size");
 constexpr uint32_t G1_NSTAMP = 8;
@@ -436,6 +439,14 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
     __shared__ G1Smem sm;
     const unsigned tid = threadIdx.x;
     const uint32_t b = blockIdx.x, G = gridDim.x;
+    if (b == 0) {  // the late-block test hook (0 in every product workspace)
+        const uint64_t d = hdr->test_delay;
+        if (d) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < d)
+                __builtin_amdgcn_s_sleep(127);
+        }
+    }
     // every block reads seq before its round-0 granules exist; block 0 moves
     // it on only after it has read every block's round-0 granules
     const uint64_t seq = __hip_atomic_load(&hdr->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -820,9 +831,34 @@ __global__ __launch_bounds__(G1_THREADS) void k_g4p_one(const int32_t *__restric
         __syncthreads();  // the next round rewrites the LDS image and the trees
         G1_STAMP(6);
     }
+    // The status: the range and capacity flags are the same in every block
+    // (from the shared tables), a timeout is per block (block 0
+    // alone reported its own, so a block that timed out and wrote none of its
+    // words went unseen).  Every block ORs its timeout into hdr->tmo, then
+    // counts itself done; block 0 waits (bounded) for all G, reports, and
+    // re-arms both for the next launch.  A block that never finishes within the
+    // bound is a timeout too (the workspace must then be zeroed again).
+    if (tid == 0) {
+        if (tmo)
+            __hip_atomic_fetch_or(&hdr->tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&hdr->done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (b == 0 && tid == 0) {
+        uint32_t late = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(&hdr->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < G) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > G1_TIMEOUT_TICKS) {
+                late = 1;
+                break;
+            }
+        }
+        const uint32_t any_tmo = __hip_atomic_load(&hdr->tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | late;
+        __hip_atomic_store(&hdr->tmo, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&hdr->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *nwords = carry_base;
-        *status = (bad_all ? G4_STATUS_RANGE : 0u) | (nospc ? G4_STATUS_NOSPC : 0u) | (tmo ? G4_STATUS_TIMEOUT : 0u);
+        *status = (bad_all ? G4_STATUS_RANGE : 0u) | (nospc ? G4_STATUS_NOSPC : 0u) |
+                  ((tmo | any_tmo) ? G4_STATUS_TIMEOUT : 0u);
     }
 }
 

@@ -2,7 +2,7 @@
 // (multiscale.hip; compressors.py:754-826 and 612-680).  Same outputs as the
 // generic kernels, bit for bit; what changes is the cost per element:
 //   * the level decision and the selected level's rounding use the integer
-//     stochastic rounding of qsgd_encode.h (ENC_INT): one signed Markstein
+//     stochastic rounding of qsgd_encode.h (the integer form): one signed Markstein
 //     quotient per element, then per level one packed scale, one
 //     v_cvt_flr_i32_f32 and one v_mad_u32_u24;
 //   * the mask-plane position of an element (i / M_mask) is a multiply-high

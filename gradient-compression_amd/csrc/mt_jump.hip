@@ -26,11 +26,16 @@
 //               draws coalesced; the last generator writes the state back
 // Bit-exact with the serial stream (tests/test_gpu_parity.py vs the oracle's
 // MT19937 and the reference's torch-mode goldens).
+#include <algorithm>
 #include <type_traits>
 
 #include "gc_device.h"
 #include "gc_host.h"
 #include "qsgd_encode.h"
+
+#ifndef GC_SPLIT_LAB
+#define GC_SPLIT_LAB 0
+#endif
 
 namespace gc {
 
@@ -255,7 +260,7 @@ __device__ __forceinline__ float mt_quot(float v, const DivNorm &dv)
 template <int MODE>
 __device__ __forceinline__ void mt_store_q(void *out, uint64_t e, float v, uint32_t r, const DivNorm &dv, float s)
 {
-    const uint32_t q = enc_lane<0>(v, mt_quot(v, dv), s, 0, r);
+    const uint32_t q = enc_lane(v, mt_quot(v, dv), s, 0, r);
     if constexpr (MODE == 1)
         reinterpret_cast<int8_t *>(out)[e] = (int8_t)q;
     else
@@ -295,16 +300,27 @@ __device__ __forceinline__ void mt_load_row(float *row, const float *__restrict_
 static_assert(kMtPre == 4 && kMtRounds == 3, "mt_wait_row's count");
 __device__ __forceinline__ void mt_wait_row() { asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); }
 
+// where the split-plane modes (4, 5) put the draws of element e: call k =
+// e / per_end goes to region slot(k) = (ring0 + k) % ring of `bytes` bytes
+// (ring 0: slot k), the call's HI plane then its LO plane (gc_device.h
+// split_hpad).  A workgroup's blocks cross at most one call boundary each
+// (per_end >= 624): the two regions in play are tracked per block.
+struct SplitOut {
+    uint8_t *base;
+    uint64_t per_end, bytes;
+    uint32_t ring, ring0;
+};
+
 template <int MODE>
 __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t jumps,
                                                          uint64_t J, uint64_t count,
                                                          void *__restrict__ out, uint32_t *__restrict__ state,
                                                          const float *__restrict__ x, const float *__restrict__ normp,
-                                                         float s)
+                                                         float s, uint64_t g0, SplitOut so)
 {
     __shared__ __attribute__((aligned(16))) uint32_t buf[2][kMtN];
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
-    const uint64_t g = blockIdx.x;
+    const uint64_t g = g0 + blockIdx.x;
     if (g == 0)
         for (uint32_t i = tid; i < kMtN; i += kMtGenThreads)
             buf[0][i] = ws[kWsWin + i];
@@ -374,6 +390,92 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
             }
             lds_barrier();
         }
+    } else if constexpr (MODE == 4 || MODE == 5) {
+        // split planes (GC_RNG_SPLIT8 / SPLIT16), one draw per tempering thread
+        // and round like MODE 0 (all 256 lanes busy; a wave's 1- / 2-byte
+        // stores are contiguous): the top HB of the draw's low 24 bits to the
+        // HI plane, the rest to the LO plane of its call's region
+        constexpr uint32_t HB = MODE == 4 ? 8u : 16u;
+        const uint64_t hpad = split_hpad(so.per_end, HB);
+        uint64_t kc = pos0 / so.per_end;         // call of the current block's first draw
+        uint64_t bnd = (kc + 1) * so.per_end;    // first draw of the next call
+        auto region = [&](uint64_t k) {
+            const uint64_t slot = so.ring ? (so.ring0 + k) % so.ring : k;
+            return so.base + slot * so.bytes;
+        };
+        auto emit1 = [&](uint64_t e, uint32_t raw, uint8_t *rc, uint8_t *rn) {
+            const uint32_t y = mtj_temper(raw);
+            const bool nx = e >= bnd;
+            uint8_t *r = nx ? rn : rc;
+            const uint64_t loc = e - (nx ? bnd : bnd - so.per_end);
+            if constexpr (HB == 8) {
+                r[loc] = (uint8_t)(y >> 16);
+                reinterpret_cast<uint16_t *>(r + hpad)[loc] = (uint16_t)y;
+            } else {
+                reinterpret_cast<uint16_t *>(r)[loc] = (uint16_t)(y >> 8);
+                r[hpad + loc] = (uint8_t)y;
+            }
+        };
+        // whole quads (read index and per_end multiples of 4: every quad's four
+        // draws sit in one call, 8- / 4-byte aligned): thread ct tempers draws
+        // 4q .. 4q+3 and stores one HI word pair / word and one LO word / pair
+        auto emit4 = [&](uint64_t e, const uint32_t *src, uint8_t *rc, uint8_t *rn) {
+            const uint4 w = *reinterpret_cast<const uint4 *>(src);  // 16-byte aligned: ptr0 % 4 == 0
+            const uint32_t a = mtj_temper(w.x), b = mtj_temper(w.y), c = mtj_temper(w.z), d = mtj_temper(w.w);
+            const bool nx = e >= bnd;
+            uint8_t *r = nx ? rn : rc;
+            const uint64_t loc = e - (nx ? bnd : bnd - so.per_end);
+            if constexpr (HB == 8) {
+                if (GC_SPLIT_LAB != 2)
+                *reinterpret_cast<uint32_t *>(r + loc) =
+                    ((a >> 16) & 0xFFu) | ((b >> 8) & 0xFF00u) | (c & 0xFF0000u) | ((d << 8) & 0xFF000000u);
+                if (GC_SPLIT_LAB != 1)
+                *reinterpret_cast<uint2 *>(r + hpad + 2 * loc) =
+                    make_uint2((a & 0xFFFFu) | (b << 16), (c & 0xFFFFu) | (d << 16));
+            } else {
+                if (GC_SPLIT_LAB != 2)
+                *reinterpret_cast<uint2 *>(r + 2 * loc) =
+                    make_uint2(((a >> 8) & 0xFFFFu) | ((b << 8) & 0xFFFF0000u),
+                               ((c >> 8) & 0xFFFFu) | ((d << 8) & 0xFFFF0000u));
+                if (GC_SPLIT_LAB != 1)
+                *reinterpret_cast<uint32_t *>(r + hpad + loc) =
+                    (a & 0xFFu) | ((b & 0xFFu) << 8) | ((c & 0xFFu) << 16) | (d << 24);
+            }
+        };
+        const bool quads = (ptr0 & 3u) == 0 && (so.per_end & 3u) == 0;  // uniform
+        {
+            uint8_t *rc = region(kc), *rn = region(kc + 1);
+            if (quads) {
+                for (uint32_t q = ct; 4 * q < head; q += kMtTemperThreads)
+                    emit4(pos0 + 4 * q, &buf[0][ptr0 + 4 * q], rc, rn);
+            } else {
+                for (uint32_t i = ct; i < head; i += kMtTemperThreads)
+                    emit1(pos0 + i, buf[0][ptr0 + i], rc, rn);
+            }
+        }
+        lds_barrier();
+        for (uint32_t t = 1; t <= twists; ++t) {
+            const uint32_t *cur = buf[t & 1u];
+            const uint64_t at = pos0 + head + (uint64_t)(t - 1) * kMtN;
+            const uint32_t take = (uint32_t)min((uint64_t)kMtN, end - at);
+            if (at >= bnd) {  // uniform: the block starts in the next call
+                ++kc;
+                bnd += so.per_end;
+            }
+            uint8_t *rc = region(kc), *rn = region(kc + 1);
+            if (quads) {
+                for (uint32_t q = ct; 4 * q < take; q += kMtTemperThreads)
+                    emit4(at + 4 * q, cur + 4 * q, rc, rn);
+            } else {
+#pragma unroll
+                for (uint32_t r = 0; r < kMtRounds; ++r) {
+                    const uint32_t i = ct + kMtTemperThreads * r;
+                    if (i < take)
+                        emit1(at + i, cur[i], rc, rn);
+                }
+            }
+            lds_barrier();
+        }
     } else if constexpr (MODE == 3) {
         // 24-bit packed draws (GC_RNG_STREAM24): thread ct tempers draws
         // 4q .. 4q+3 of a block and stores their low 24 bits as 3 words.  The
@@ -409,7 +511,7 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
         const uint64_t body = pos0 + head;  // element of block 1's first draw
         for (uint32_t i = ct; i < head; i += kMtTemperThreads) {
             const float v = x[pos0 + i];
-            qbuf[0][i] = (QT)enc_lane<0>(v, mt_quot(v, dv), s, 0, mtj_temper(buf[0][ptr0 + i]));
+            qbuf[0][i] = (QT)enc_lane(v, mt_quot(v, dv), s, 0, mtj_temper(buf[0][ptr0 + i]));
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the head's loads: the ring's counts start from zero
 #pragma unroll
@@ -430,7 +532,7 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
                     const uint32_t i = ct + kMtTemperThreads * r;
                     const uint32_t ic = min(i, kMtN - 1);  // past 623: recomputes word 623 (same x, same draw)
                     const float v = xring[d][i];
-                    qbuf[t & 1u][ic] = (QT)enc_lane<0>(v, mt_quot(v, dv), s, 0, mtj_temper(cur[ic]));
+                    qbuf[t & 1u][ic] = (QT)enc_lane(v, mt_quot(v, dv), s, 0, mtj_temper(cur[ic]));
                 }
                 mt_load_row(xring[d], x, at + (uint64_t)kMtPre * kMtN, end, ct);
                 lds_barrier();
@@ -558,16 +660,16 @@ static int mt_run(const char *what, int mode, uint32_t *state_dev, const uint32_
     uint32_t *gstate = split ? nullptr : state_dev;
     if (mode == 0)
         hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
-                           J, count, out, gstate, x, norm, s);
+                           J, count, out, gstate, x, norm, s, (uint64_t)0, SplitOut{});
     else if (mode == 1)
         hipLaunchKernelGGL(k_mt_gen<1>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
-                           J, count, out, gstate, x, norm, s);
+                           J, count, out, gstate, x, norm, s, (uint64_t)0, SplitOut{});
     else if (mode == 2)
         hipLaunchKernelGGL(k_mt_gen<2>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
-                           J, count, out, gstate, x, norm, s);
+                           J, count, out, gstate, x, norm, s, (uint64_t)0, SplitOut{});
     else
         hipLaunchKernelGGL(k_mt_gen<3>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps,
-                           J, count, out, gstate, x, norm, s);
+                           J, count, out, gstate, x, norm, s, (uint64_t)0, SplitOut{});
     return launch_status(what);
 }
 
@@ -622,7 +724,8 @@ size_t gc_mt19937_workspace_size_multi_j(uint64_t count, uint64_t J, uint32_t ne
 // plain draws, 3 the 24-bit packed draws
 static int mt_multi(const char *what, int mode, uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens,
                     uint64_t J, const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint32_t *ends_out,
-                    uint32_t *out, void *workspace, int phase, gc_stream_t stream)
+                    uint32_t *out, void *workspace, int phase, gc_stream_t stream, SplitOut so = SplitOut{},
+                    uint64_t g_first = 0, uint64_t g_count = ~0ull)
 {
     GC_REQUIRE(phase >= 1 && phase <= 3, "%s: phase must be 1, 2 or 3", what);
     GC_REQUIRE(state_dev && workspace && end_coefs && ends_out, "%s: null state / workspace / ends", what);
@@ -648,14 +751,24 @@ static int mt_multi(const char *what, int mode, uint32_t *state_dev, const uint3
                            ends_out);
     }
     if (phase & 2) {
+        // generators g_first .. g_first + g_count - 1 (clamped to the run)
+        const uint64_t g1 = std::min(gens, g_first + std::min(g_count, gens));
+        if (g_first >= g1)
+            return launch_status(what);
+        const dim3 grid((unsigned)(g1 - g_first));
+#define GC_MTG(M_)                                                                                                   \
+    hipLaunchKernelGGL(k_mt_gen<M_>, grid, dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps, J, count,          \
+                       (void *)out, (uint32_t *)nullptr, (const float *)nullptr, (const float *)nullptr, 0.0f, g_first, \
+                       so)
         if (mode == 3)
-            hipLaunchKernelGGL(k_mt_gen<3>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens,
-                               (uint64_t)jumps, J, count, (void *)out, (uint32_t *)nullptr, (const float *)nullptr,
-                               (const float *)nullptr, 0.0f);
+            GC_MTG(3);
+        else if (mode == 4)
+            GC_MTG(4);
+        else if (mode == 5)
+            GC_MTG(5);
         else
-            hipLaunchKernelGGL(k_mt_gen<0>, dim3((unsigned)gens), dim3(kMtGenThreads), 0, st, ws, gens,
-                               (uint64_t)jumps, J, count, (void *)out, (uint32_t *)nullptr, (const float *)nullptr,
-                               (const float *)nullptr, 0.0f);
+            GC_MTG(0);
+#undef GC_MTG
     }
     return launch_status(what);
 }
@@ -680,6 +793,33 @@ int gc_mt19937_generate_multi24_j(uint32_t *state_dev, const uint32_t *table_dev
                (unsigned long long)per_end, (unsigned long long)idx);
     return mt_multi(what, 3, state_dev, table_dev, table_gens, J, end_coefs, nend, per_end, ends_out, out, workspace,
                     phase, stream);
+}
+
+uint64_t gc_rng_split_bytes(uint64_t n, uint32_t hi_bits)
+{
+    return (hi_bits == 8 || hi_bits == 16) ? split_bytes(n, hi_bits) : 0;
+}
+
+int gc_mt19937_generate_multi_split_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                      const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint64_t idx,
+                                      uint32_t hi_bits, uint32_t *ends_out, void *out, uint32_t ring, uint32_t ring0,
+                                      uint64_t g_first, uint64_t g_count, void *workspace, int phase,
+                                      gc_stream_t stream)
+{
+    const char *what = "gc_mt19937_generate_multi_split_j";
+    GC_REQUIRE(hi_bits == 8 || hi_bits == 16, "%s: hi_bits must be 8 or 16", what);
+    GC_REQUIRE(idx <= kMtN, "%s: read index %llu above 624", what, (unsigned long long)idx);
+    GC_REQUIRE(!(phase & 2) || ((uintptr_t)out & 15u) == 0, "%s: out must be 16-byte aligned", what);
+    GC_REQUIRE(ring == 0 || ring >= 2, "%s: a ring holds 0 (none) or at least 2 regions", what);
+    GC_REQUIRE(ring == 0 || ring0 < ring, "%s: ring0 must be below ring", what);
+    SplitOut so;
+    so.base = reinterpret_cast<uint8_t *>(out);
+    so.per_end = per_end;
+    so.bytes = split_bytes(per_end, hi_bits);
+    so.ring = ring;
+    so.ring0 = ring0;
+    return mt_multi(what, hi_bits == 8 ? 4 : 5, state_dev, table_dev, table_gens, J, end_coefs, nend, per_end,
+                    ends_out, reinterpret_cast<uint32_t *>(out), workspace, phase, stream, so, g_first, g_count);
 }
 
 int gc_mt19937_generate_jumped(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint32_t *out,

@@ -368,11 +368,14 @@ static RngArgs rng_args(const gc_rng *r, uint64_t n)
 static int check_rng(const gc_rng *r, const char *what, bool stream24 = false)
 {
     GC_REQUIRE(r, "%s: null rng", what);
-    GC_REQUIRE(r->kind == GC_RNG_PHILOX || r->kind == GC_RNG_STREAM || (stream24 && r->kind == GC_RNG_STREAM24),
+    const bool single = r->kind == GC_RNG_STREAM24 || r->kind == GC_RNG_SPLIT8 || r->kind == GC_RNG_SPLIT16;
+    GC_REQUIRE(r->kind == GC_RNG_PHILOX || r->kind == GC_RNG_STREAM || (stream24 && single),
                "%s: unknown rng kind %u", what, r->kind);
     GC_REQUIRE(r->kind == GC_RNG_PHILOX || r->stream, "%s: STREAM rng without a stream pointer", what);
     GC_REQUIRE(r->kind != GC_RNG_STREAM24 || ((uintptr_t)r->stream & 3u) == 0,
                "%s: STREAM24 draws must be 4-byte aligned", what);
+    GC_REQUIRE((r->kind != GC_RNG_SPLIT8 && r->kind != GC_RNG_SPLIT16) || ((uintptr_t)r->stream & 15u) == 0,
+               "%s: split-plane draws must be 16-byte aligned", what);
     return GC_OK;
 }
 
@@ -401,9 +404,12 @@ static void launch_encode(const float *x, const int64_t *idx, uint64_t n, const 
     // up to 12288 blocks (48 per CU, ~1.4 tiles per thread at 1e8 floats)
     // keeps more of the 6 plane streams in flight than a 2048-block grid-stride.
     const uint64_t quads = ln->plane_words >> 2;
-    constexpr int ABL = ENC_INT | ENC_NT | ENC_NTS;
-    hipLaunchKernelGGL((k_qsgd_encode<L, KIND, MODE, ABL>), dim3(grid_for(quads, kEncodeGrid)), dim3(kBlock), 0, st, x,
-                       idx, n, norm, s, qmax, ln->bits, ln->plane_words, ra, words);
+    if constexpr ((KIND == 4 || KIND == 5) && MODE == 0 && L <= 16)  // split-plane draws, dense x (16-byte aligned)
+        hipLaunchKernelGGL((k_qsgd_encode_split<L, KIND>), dim3(grid_for(quads, kEncodeGrid)), dim3(kBlock), 0, st,
+                           x, n, norm, s, qmax, ln->bits, ln->plane_words, ra, words);
+    else
+        hipLaunchKernelGGL((k_qsgd_encode<L, KIND, MODE>), dim3(grid_for(quads, kEncodeGrid)), dim3(kBlock), 0, st,
+                           x, idx, n, norm, s, qmax, ln->bits, ln->plane_words, ra, words);
 }
 
 }  // namespace gc
@@ -464,7 +470,25 @@ int gc_qsgd_encode(const float *x, const int64_t *idx, uint64_t n, const float *
     const int mode = idx ? 2 : (aligned16(x) ? 0 : 1);
     const float sf = (float)s;
     const int32_t qmax = (int32_t)s;
-    if (rng->kind == GC_RNG_STREAM24) {
+    if (rng->kind == GC_RNG_SPLIT8 || rng->kind == GC_RNG_SPLIT16) {
+        const bool h8 = rng->kind == GC_RNG_SPLIT8;
+        if (mode == 0) {
+            if (h8)
+                GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 4, 0>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)))
+            else
+                GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 5, 0>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)))
+        } else if (mode == 1) {
+            if (h8)
+                GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 4, 1>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)))
+            else
+                GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 5, 1>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)))
+        } else {
+            if (h8)
+                GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 4, 2>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)))
+            else
+                GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 5, 2>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)))
+        }
+    } else if (rng->kind == GC_RNG_STREAM24) {
         if (mode == 0) {
             GC_DISPATCH_L(lanes->per_word, (launch_encode<LL, 3, 0>(x, idx, n, norm, sf, qmax, lanes, ra, words, st)));
         } else if (mode == 1) {

@@ -1,8 +1,10 @@
 // qsgd_encode.h — the fused QSGD-MaxNorm encode kernel (quantize + stochastic
 // round + carry-free planar pack), compressors.py:299-316.
 //
-// Shared by qsgd.hip (the product instantiation, ABL = 0) and
-// tools/encode_lab.hip (ablation variants for measurement only).
+// The product kernel only: full tiles take the integer stochastic rounding,
+// nontemporal loads of x and nontemporal stores of the words (tools/lab2,
+// profiles/r01m_*, r01n_*).  The measurement variants of earlier rounds
+// (ablations, instruction mixes, schedules) live in tools/encode_lab_kernel.h.
 //
 // Per element, the reference's arithmetic in its own order:
 //   ql = RN(|x| / norm)        IEEE division (see div_norm below)
@@ -17,38 +19,16 @@
 
 namespace gc {
 
-enum : int {
-    ENC_ABL_NORNG = 1,  // measurement only: draws = element index (no Philox)
-    ENC_ABL_NODIV = 2,  // measurement only: ql = |x| * (1/norm) (not exact)
-    ENC_PHX0 = 4,       // Philox instruction mix 0 (same outputs)
-    ENC_PHX2 = 8,       // Philox instruction mix 2 (same outputs)
-    ENC_MED3 = 16,      // clamp with v_max + v_min instead of v_med3_f32
-    ENC_ABL_L2 = 32,    // measurement only: loads from a 16 KB window (compute floor)
-    ENC_REV = 64,       // walk the full tiles from the top down (Infinity-Cache reuse after absmax)
-    ENC_GRP2 = 128,     // schedule the planes in pairs (fewer live Philox chains -> fewer VGPRs)
-    ENC_GRP3 = 256,     // schedule the planes in triples
-    ENC_SEQ = 512,      // one plane at a time: per-plane range check, sched barrier between planes
-    ENC_PF = 1024,      // register prefetch: the next tile's L loads are issued before this tile's math
-    ENC_DIV2 = 2048,    // the compiler's two-correction quotient (div_fast2) instead of Markstein's
-    ENC_NT = 4096,      // nontemporal loads of x
-    ENC_INT = 8192,     // integer stochastic rounding on full tiles (same outputs; b <= 8)
-    ENC_NTS = 16384,    // nontemporal stores of the packed words
-};
-
-template <int ABL>
+// the packed words: written once, never read back by this kernel (NT store)
 __device__ __forceinline__ void store_words(uint32_t *p, const uint4 &v)
 {
-    if constexpr ((ABL & ENC_NTS) != 0) {
-        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-        const u4v r = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(r, reinterpret_cast<u4v *>(p));
-    } else {
-        *reinterpret_cast<uint4 *>(p) = v;
-    }
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    const u4v r = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(r, reinterpret_cast<u4v *>(p));
 }
 
 // ---------------------------------------------------------------------------
-// Integer form of the stochastic rounding (ENC_INT), bit-identical to
+// Integer form of the stochastic rounding (full tiles), bit-identical to
 // enc_lane on the fast path (|x| <= norm, no tiny |x|, norm in range):
 //   q  = RN(x / norm)                 signed Markstein quotient (RN is odd)
 //   Ls = RN(q * s*2^24)               = RN(|x|/norm * s) * 2^24 exactly (power-of-two
@@ -117,13 +97,127 @@ __device__ __forceinline__ int32_t enc_q_wide(float x, float Ls, uint32_t r, int
     return __mul24((int32_t)(t >> 24), med3_i32(__float_as_int(x), lo, hi));
 }
 
-template <int KIND, int ABL>
-__device__ __forceinline__ uint4 draws4_abl(const RngArgs &rng, uint32_t level, uint64_t i0);
+// One full tile from split-plane draws (KIND 4 / 5, gc_device.h).  With c =
+// ceil(|Ls|) = fl*2^24 + F the bit is [m < F], m = the 24-bit draw.  Knowing
+// only m's top HB bits hm (low bits zero), [hm < F] is already right unless
+// F - 1 and m share their top HB bits (then hm <= F - 1 < hm + 2^(24-HB) and
+// the low bits decide).  Pass 1 reads the HI plane and checks every element
+// of the tile for that tie; a tile with one returns false and the caller's
+// general path encodes it from both planes (about 24 / 2^HB of the tiles: 1 in
+// 2,700 for HB = 16).  Pass 2 recomputes Ls (cheaper than holding 4L values
+// across the check) and packs with the HI bits alone: the LO plane is never
+// read for such tiles.  A flag where F = 0 is harmless (the general path is
+// exact either way).  Otherwise enc_tile_int's arithmetic.
+__device__ __forceinline__ uint32_t ld_nt_u32(const uint8_t *p)
+{
+    return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(p));
+}
+__device__ __forceinline__ uint2 ld_nt_u2(const uint8_t *p)
+{
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    const u2v v = __builtin_nontemporal_load(reinterpret_cast<const u2v *>(p));
+    return make_uint2(v.x, v.y);
+}
+
+// the HI bits of draw e (0..3) of a plane's quad, in place (low 24-HB bits zero)
+template <uint32_t HB>
+__device__ __forceinline__ uint32_t split_hi(const uint32_t (&hw)[HB / 8], int e)
+{
+    constexpr uint32_t HM = ((1u << HB) - 1u) << (24u - HB);
+    if constexpr (HB == 8)
+        return e == 0 ? (hw[0] << 16) & HM : e == 1 ? (hw[0] << 8) & HM : e == 2 ? hw[0] & HM : (hw[0] >> 8) & HM;
+    else
+        return e == 0 ? (hw[0] << 8) & HM : e == 1 ? (hw[0] >> 8) & HM
+             : e == 2 ? (hw[HB / 8 - 1] << 8) & HM : (hw[HB / 8 - 1] >> 8) & HM;
+}
+
+// c (WIDE) or -c (narrow) of one element from its Ls
+template <bool WIDE>
+__device__ __forceinline__ int32_t split_c(float ls)
+{
+    if constexpr (WIDE)
+        return (int32_t)(uint32_t)__builtin_ceilf(fabsf(ls));
+    else
+        return cvt_flr_neg_abs(ls);
+}
+
+template <int L, int KIND, bool WIDE>
+__device__ __forceinline__ bool enc_tile_int_split(const float4 (&xv)[L], uint32_t t4, uint32_t M32, const DivNorm &dv,
+                                                   float S24, uint32_t w, uint32_t Cw, const RngArgs &rng, uint4 &acc)
+{
+    constexpr uint32_t HB = KIND == 4 ? 8u : 16u, LB = 24u - HB;
+    constexpr uint32_t HM = ((1u << HB) - 1u) << LB;
+    constexpr int H = L / 2;
+    const uint8_t *hp = reinterpret_cast<const uint8_t *>(rng.stream);
+    uint32_t hw[L][HB / 8];
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+        const uint32_t i0 = k * M32 + t4;
+        if constexpr (HB == 8) {
+            hw[k][0] = ld_nt_u32(hp + i0);
+        } else {
+            const uint2 v = ld_nt_u2(hp + 2u * i0);
+            hw[k][0] = v.x;
+            hw[k][HB / 8 - 1] = v.y;
+        }
+    }
+    // pass 1: c per element (xv dies here), the signs, the tie check
+    int32_t cc[L][4];
+    uint64_t neg = 0;  // bit 4k + e: x < 0 (or -0, whose c is 0: no effect); L <= 16
+    bool tie = false;
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+        const gc_f2 l01 = ls2(xv[k].x, xv[k].y, dv, S24);
+        const gc_f2 l23 = ls2(xv[k].z, xv[k].w, dv, S24);
+        const float ls[4] = {l01.x, l01.y, l23.x, l23.y};
+        const float xs[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            cc[k][e] = split_c<WIDE>(ls[e]);
+            neg |= (uint64_t)(__float_as_uint(xs[e]) >> 31) << (4 * k + e);
+            const uint32_t cm1 = WIDE ? (uint32_t)cc[k][e] - 1u : ~(uint32_t)cc[k][e];  // c - 1
+            tie |= ((cm1 ^ split_hi<HB>(hw[k], e)) & HM) == 0u;
+        }
+    }
+    if (__builtin_expect(tie, 0))
+        return false;
+    // pass 2: the lanes from the HI bits alone (x = +-0 has c = 0 and xi = 0)
+    int32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+        const uint32_t sh = (uint32_t)(k < H ? k : k - H) * w;
+        int32_t *a = k < H ? lo : hi;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t rd = split_hi<HB>(hw[k], e);
+            int32_t v;
+            if constexpr (WIDE)  // xi = (c + (~m & 0xFFFFFF)) >> 24 = fl + [m < F]
+                v = (int32_t)((uint32_t)add_low24(~rd, cc[k][e]) >> 24);
+            else  // (m - c) >> 24 = -xi (m < 2^24 here)
+                v = ((int32_t)rd + cc[k][e]) >> 24;
+            v <<= sh;
+            a[e] += ((neg >> (4 * k + e)) & 1u) ? -v : v;
+        }
+    }
+    const uint32_t hs = (uint32_t)H * w;
+    if constexpr (WIDE) {
+        acc.x = Cw + ((uint32_t)lo[0] + ((uint32_t)hi[0] << hs));
+        acc.y = Cw + ((uint32_t)lo[1] + ((uint32_t)hi[1] << hs));
+        acc.z = Cw + ((uint32_t)lo[2] + ((uint32_t)hi[2] << hs));
+        acc.w = Cw + ((uint32_t)lo[3] + ((uint32_t)hi[3] << hs));
+    } else {
+        acc.x = Cw - ((uint32_t)lo[0] + ((uint32_t)hi[0] << hs));
+        acc.y = Cw - ((uint32_t)lo[1] + ((uint32_t)hi[1] << hs));
+        acc.z = Cw - ((uint32_t)lo[2] + ((uint32_t)hi[2] << hs));
+        acc.w = Cw - ((uint32_t)lo[3] + ((uint32_t)hi[3] << hs));
+    }
+    return true;
+}
 
 // one full tile (L planes x 4 words) on the integer path.  Lanes k < H
 // accumulate at shift k*w, lanes k >= H at (k-H)*w, so every 24-bit
 // multiplier is +-2^sh with sh <= 15; word = C -+ (lo + (hi << H*w)).
-template <int L, int KIND, int ABL, bool WIDE>
+template <int L, int KIND, bool WIDE>
 __device__ __forceinline__ uint4 enc_tile_int(const float4 (&xv)[L], uint32_t t4, uint32_t M32, const DivNorm &dv,
                                               float S24, uint32_t w, uint32_t Cw, const RngArgs &rng)
 {
@@ -133,7 +227,7 @@ __device__ __forceinline__ uint4 enc_tile_int(const float4 (&xv)[L], uint32_t t4
     for (int k = 0; k < L; ++k) {
         const gc_f2 l01 = ls2(xv[k].x, xv[k].y, dv, S24);
         const gc_f2 l23 = ls2(xv[k].z, xv[k].w, dv, S24);
-        const uint4 r = draws4_abl<KIND, ABL>(rng, 0, k * M32 + t4);
+        const uint4 r = draws4<KIND>(rng, 0, k * M32 + t4);
         const uint32_t sh = (uint32_t)(k < H ? k : k - H) * w;
         const int32_t bl = -(1 << sh), bh = 1 << sh;
         int32_t *a = k < H ? lo : hi;
@@ -165,7 +259,7 @@ __device__ __forceinline__ uint4 enc_tile_int(const float4 (&xv)[L], uint32_t t4
     return acc;
 }
 
-// fast-path tile check for ENC_INT: every |x| <= norm (inf / NaN excluded by
+// fast-path tile check of the integer form: every |x| <= norm (inf / NaN excluded by
 // the bit compare) and no nonzero |x| below the division's low threshold.
 // 2*bits drops the sign; 2*bits - 2 wraps +-0 to 0xFFFFFFFE.
 struct RangeI {
@@ -183,12 +277,11 @@ struct RangeI {
 
 // lane value of one element (ql = |x| / norm).  A NaN quotient (0/0, NaN
 // input) gives xi = 0 (fmaxf(NaN, 0) = 0); an infinite one saturates at s.
-template <int ABL = 0>
 __device__ __forceinline__ uint32_t enc_lane(float x, float ql, float s, int32_t qmax, uint32_t r)
 {
     // v_med3_f32(l, 0, s): clamps to [0, s]; a NaN l yields 0 (checked against
     // the oracle by tests/test_gpu_parity.py::test_encode_non_finite_and_tiny_inputs)
-    const float l = (ABL & ENC_MED3) ? fminf(fmaxf(ql * s, 0.0f), s) : __builtin_amdgcn_fmed3f(ql * s, 0.0f, s);
+    const float l = __builtin_amdgcn_fmed3f(ql * s, 0.0f, s);
     const uint32_t fl = (uint32_t)(int32_t)l;
     const float p = __builtin_amdgcn_fractf(l);
     const float u = (float)(r & 0xFFFFFFu) * 0x1p-24f;
@@ -199,49 +292,22 @@ __device__ __forceinline__ uint32_t enc_lane(float x, float ql, float s, int32_t
     return (xi ^ sg) + ((uint32_t)qmax - sg);
 }
 
-template <int ABL>
 __device__ __forceinline__ float4 quot4_fast(const float4 &v, const DivNorm &d)
 {
     float4 q;
-    if constexpr ((ABL & ENC_ABL_NODIV) != 0) {
-        q.x = fabsf(v.x) * d.r;
-        q.y = fabsf(v.y) * d.r;
-        q.z = fabsf(v.z) * d.r;
-        q.w = fabsf(v.w) * d.r;
-    } else if constexpr ((ABL & ENC_DIV2) != 0) {
-        q.x = div_fast2(fabsf(v.x), d);
-        q.y = div_fast2(fabsf(v.y), d);
-        q.z = div_fast2(fabsf(v.z), d);
-        q.w = div_fast2(fabsf(v.w), d);
-    } else {
-        q.x = div_fast(fabsf(v.x), d);
-        q.y = div_fast(fabsf(v.y), d);
-        q.z = div_fast(fabsf(v.z), d);
-        q.w = div_fast(fabsf(v.w), d);
-    }
+    q.x = div_fast(fabsf(v.x), d);
+    q.y = div_fast(fabsf(v.y), d);
+    q.z = div_fast(fabsf(v.z), d);
+    q.w = div_fast(fabsf(v.w), d);
     return q;
 }
 
-template <int KIND, int ABL>
-__device__ __forceinline__ uint4 draws4_abl(const RngArgs &rng, uint32_t level, uint64_t i0)
-{
-    if constexpr ((ABL & ENC_ABL_NORNG) != 0) {
-        const uint32_t b = (uint32_t)i0 * 2654435761u;
-        return make_uint4(b, b + 1u, b + 2u, b + 3u);
-    } else if constexpr ((ABL & ENC_PHX0) != 0) {
-        return draws4<KIND, 0>(rng, level, i0);
-    } else if constexpr ((ABL & ENC_PHX2) != 0) {
-        return draws4<KIND, 2>(rng, level, i0);
-    } else {
-        return draws4<KIND>(rng, level, i0);
-    }
-}
-
 // Full tiles: every one of the L planes of words 4t..4t+3 is in range, so
-// no per-element bounds, 32-bit element indices, L float4 loads in flight.
-// Tail quads, gathers, unaligned x and the non-fast-division case go through
-// the generic body.
-template <int L, int KIND, int MODE, int ABL, int MINW = 1>
+// no per-element bounds, 32-bit element indices, L float4 loads in flight
+// (nontemporal: x is streamed once per pass), the integer stochastic rounding
+// when the tile passes its range check.  Tail quads, gathers, unaligned x and
+// the non-fast-division case go through the generic body.
+template <int L, int KIND, int MODE, int MINW = 1>
 __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__restrict__ x, const int64_t *__restrict__ idx,
                                                         uint64_t n, const float *__restrict__ normp, float s,
                                                         int32_t qmax, uint32_t w, uint64_t M, RngArgs rng,
@@ -249,7 +315,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
 {
     const float norm = *normp;
     const DivNorm dv = make_div(norm);
-    const bool fast = dv.fast || (ABL & ENC_ABL_NODIV) != 0;
+    const bool fast = dv.fast;
     const uint64_t quads = M >> 2;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -258,132 +324,53 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
     const uint64_t last = (uint64_t)(L - 1) * M;
     const uint64_t full = (MODE == 0 && fast && n >= last + 4 && n < (1ull << 32)) ? (n - last) >> 2 : 0;
     const uint32_t M32 = (uint32_t)M;
-    // ENC_INT constants (uniform): b <= 7 (s * 2^24 < 2^31) takes the signed
-    // floor form, b = 8 the unsigned ceil form
+    // integer-path constants (uniform): b <= 7 (s * 2^24 < 2^31) takes the
+    // signed floor form, b = 8 the unsigned ceil form
     const bool intok = s <= 255.0f, narrow = s <= 127.0f;
     const float S24 = s * 16777216.0f;
     const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
     uint32_t Cw = 0;
     for (int k = 0; k < L; ++k)
         Cw += (uint32_t)qmax << (k * w);
-    if constexpr ((ABL & ENC_PF) != 0) {
-        float4 nx[L];
-        if (t < full) {
-#pragma unroll
-            for (int k = 0; k < L; ++k)
-                nx[k] = *reinterpret_cast<const float4 *>(x + (k * M32 + (uint32_t)t * 4u));
-        }
-        for (; t < full; t += stride) {
-            const uint32_t t4 = (uint32_t)t * 4u;
-            float4 xv[L];
-#pragma unroll
-            for (int k = 0; k < L; ++k)
-                xv[k] = nx[k];
-            if (t + stride < full) {
-                const uint32_t n4 = (uint32_t)(t + stride) * 4u;
-#pragma unroll
-                for (int k = 0; k < L; ++k)
-                    nx[k] = *reinterpret_cast<const float4 *>(x + (k * M32 + n4));
-            }
-            float4 q[L];
-            Range rg;
-#pragma unroll
-            for (int k = 0; k < L; ++k) {
-                q[k] = quot4_fast<ABL>(xv[k], dv);
-                rg.add4(xv[k]);
-            }
-            if (__builtin_expect(rg.slow(dv), 0)) {
-#pragma unroll
-                for (int k = 0; k < L; ++k)
-                    q[k] = quot4_ieee(xv[k], norm);
-            }
-            uint4 acc = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-            for (int k = 0; k < L; ++k) {
-                const uint4 r = draws4_abl<KIND, ABL>(rng, 0, k * M32 + t4);
-                const uint32_t sh = (uint32_t)k * w;
-                acc.x |= enc_lane<ABL>(xv[k].x, q[k].x, s, qmax, r.x) << sh;
-                acc.y |= enc_lane<ABL>(xv[k].y, q[k].y, s, qmax, r.y) << sh;
-                acc.z |= enc_lane<ABL>(xv[k].z, q[k].z, s, qmax, r.z) << sh;
-                acc.w |= enc_lane<ABL>(xv[k].w, q[k].w, s, qmax, r.w) << sh;
-            }
-            *reinterpret_cast<uint4 *>(words + t4) = acc;
-        }
-    }
     for (; t < full; t += stride) {
-        const uint32_t t4 = (uint32_t)((ABL & ENC_REV) ? (full - 1 - t) : t) * 4u;
+        const uint32_t t4 = (uint32_t)t * 4u;
         float4 xv[L];
 #pragma unroll
-        for (int k = 0; k < L; ++k) {
-            const float4 *p = reinterpret_cast<const float4 *>(x + ((ABL & ENC_ABL_L2) ? ((k * M32 + t4) & 4095u)
-                                                                                      : (k * M32 + t4)));
-            if constexpr ((ABL & ENC_NT) != 0) {
-                typedef float f4v __attribute__((ext_vector_type(4)));
-                const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
-                xv[k] = make_float4(r.x, r.y, r.z, r.w);
-            } else {
-                xv[k] = *p;
-            }
-        }
-        if constexpr ((ABL & ENC_INT) != 0) {
-            if (intok) {
-                RangeI rg;
+        for (int k = 0; k < L; ++k)
+            xv[k] = ld_nt(reinterpret_cast<const float4 *>(x + (k * M32 + t4)));
+        if (intok) {
+            RangeI rg;
 #pragma unroll
-                for (int k = 0; k < L; ++k)
-                    rg.add4(xv[k]);
-                if (__builtin_expect(!rg.slow(lo2, hi2), 1)) {
-                    const uint4 acc = narrow ? enc_tile_int<L, KIND, ABL, false>(xv, t4, M32, dv, S24, w, Cw, rng)
-                                             : enc_tile_int<L, KIND, ABL, true>(xv, t4, M32, dv, S24, w, Cw, rng);
-                    store_words<ABL>(words + t4, acc);
-                    continue;
-                }
-            }
-        }
-        if constexpr ((ABL & ENC_SEQ) != 0) {
-            uint4 acc = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-            for (int k = 0; k < L; ++k) {
-                if (k)
-                    __builtin_amdgcn_sched_barrier(0);
-                const uint32_t i0 = k * M32 + t4;
-                const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
-                Range rg;
+            for (int k = 0; k < L; ++k)
                 rg.add4(xv[k]);
-                const float4 q = __builtin_expect(rg.slow(dv), 0) ? quot4_ieee(xv[k], norm) : quot4_fast<ABL>(xv[k], dv);
-                const uint32_t sh = (uint32_t)k * w;
-                acc.x |= enc_lane<ABL>(xv[k].x, q.x, s, qmax, r.x) << sh;
-                acc.y |= enc_lane<ABL>(xv[k].y, q.y, s, qmax, r.y) << sh;
-                acc.z |= enc_lane<ABL>(xv[k].z, q.z, s, qmax, r.z) << sh;
-                acc.w |= enc_lane<ABL>(xv[k].w, q.w, s, qmax, r.w) << sh;
+            if (__builtin_expect(!rg.slow(lo2, hi2), 1)) {
+                const uint4 acc = narrow ? enc_tile_int<L, KIND, false>(xv, t4, M32, dv, S24, w, Cw, rng)
+                                         : enc_tile_int<L, KIND, true>(xv, t4, M32, dv, S24, w, Cw, rng);
+                store_words(words + t4, acc);
+                continue;
             }
-            *reinterpret_cast<uint4 *>(words + t4) = acc;
-            continue;
         }
         float4 q[L];
         Range rg;
 #pragma unroll
         for (int k = 0; k < L; ++k) {
-            q[k] = quot4_fast<ABL>(xv[k], dv);
+            q[k] = quot4_fast(xv[k], dv);
             rg.add4(xv[k]);
         }
-        if ((ABL & ENC_ABL_NODIV) == 0 && __builtin_expect(rg.slow(dv), 0)) {
+        if (__builtin_expect(rg.slow(dv), 0)) {
 #pragma unroll
             for (int k = 0; k < L; ++k)
                 q[k] = quot4_ieee(xv[k], norm);
         }
         uint4 acc = make_uint4(0u, 0u, 0u, 0u);
-        constexpr int G = (ABL & ENC_GRP2) ? 2 : ((ABL & ENC_GRP3) ? 3 : L);
 #pragma unroll
         for (int k = 0; k < L; ++k) {
-            if (k && (k % G) == 0)
-                __builtin_amdgcn_sched_barrier(0);
-            const uint32_t i0 = k * M32 + t4;
-            const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
+            const uint4 r = draws4<KIND>(rng, 0, k * M32 + t4);
             const uint32_t sh = (uint32_t)k * w;
-            acc.x |= enc_lane<ABL>(xv[k].x, q[k].x, s, qmax, r.x) << sh;
-            acc.y |= enc_lane<ABL>(xv[k].y, q[k].y, s, qmax, r.y) << sh;
-            acc.z |= enc_lane<ABL>(xv[k].z, q[k].z, s, qmax, r.z) << sh;
-            acc.w |= enc_lane<ABL>(xv[k].w, q[k].w, s, qmax, r.w) << sh;
+            acc.x |= enc_lane(xv[k].x, q[k].x, s, qmax, r.x) << sh;
+            acc.y |= enc_lane(xv[k].y, q[k].y, s, qmax, r.y) << sh;
+            acc.z |= enc_lane(xv[k].z, q[k].z, s, qmax, r.z) << sh;
+            acc.w |= enc_lane(xv[k].w, q[k].w, s, qmax, r.w) << sh;
         }
         *reinterpret_cast<uint4 *>(words + t4) = acc;
     }
@@ -402,17 +389,15 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
                     const int k = k0 + j;
                     const uint64_t i0 = (uint64_t)k * M + 4 * t;
                     if (k < L && i0 < n) {
-                        const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
+                        const uint4 r = draws4<KIND>(rng, 0, i0);
                         Range rg;
                         rg.add4(v[j]);
-                        const float4 q = fast && ((ABL & ENC_ABL_NODIV) != 0 || !rg.slow(dv))
-                                             ? quot4_fast<ABL>(v[j], dv)
-                                             : quot4_ieee(v[j], norm);
+                        const float4 q = fast && !rg.slow(dv) ? quot4_fast(v[j], dv) : quot4_ieee(v[j], norm);
                         const uint32_t sh = (uint32_t)k * w;
-                        acc.x |= enc_lane<ABL>(v[j].x, q.x, s, qmax, r.x) << sh;
-                        acc.y |= (i0 + 1 < n ? enc_lane<ABL>(v[j].y, q.y, s, qmax, r.y) : 0u) << sh;
-                        acc.z |= (i0 + 2 < n ? enc_lane<ABL>(v[j].z, q.z, s, qmax, r.z) : 0u) << sh;
-                        acc.w |= (i0 + 3 < n ? enc_lane<ABL>(v[j].w, q.w, s, qmax, r.w) : 0u) << sh;
+                        acc.x |= enc_lane(v[j].x, q.x, s, qmax, r.x) << sh;
+                        acc.y |= (i0 + 1 < n ? enc_lane(v[j].y, q.y, s, qmax, r.y) : 0u) << sh;
+                        acc.z |= (i0 + 2 < n ? enc_lane(v[j].z, q.z, s, qmax, r.z) : 0u) << sh;
+                        acc.w |= (i0 + 3 < n ? enc_lane(v[j].w, q.w, s, qmax, r.w) : 0u) << sh;
                     }
                 }
             }
@@ -436,23 +421,113 @@ __global__ __launch_bounds__(kBlock, MINW) void k_qsgd_encode(const float *__res
                     v.z = i0 + 2 < n ? (MODE == 2 ? x[idx[i0 + 2]] : x[i0 + 2]) : 0.0f;
                     v.w = i0 + 3 < n ? (MODE == 2 ? x[idx[i0 + 3]] : x[i0 + 3]) : 0.0f;
                 }
-                const uint4 r = draws4_abl<KIND, ABL>(rng, 0, i0);
+                const uint4 r = draws4<KIND>(rng, 0, i0);
                 float4 q;
                 Range rg;
                 rg.add4(v);
-                if (fast && ((ABL & ENC_ABL_NODIV) != 0 || !rg.slow(dv)))
-                    q = quot4_fast<ABL>(v, dv);
+                if (fast && !rg.slow(dv))
+                    q = quot4_fast(v, dv);
                 else
                     q = quot4_ieee(v, norm);
                 const uint32_t sh = (uint32_t)k * w;
-                acc.x |= enc_lane<ABL>(v.x, q.x, s, qmax, r.x) << sh;
-                acc.y |= (i0 + 1 < n ? enc_lane<ABL>(v.y, q.y, s, qmax, r.y) : 0u) << sh;
-                acc.z |= (i0 + 2 < n ? enc_lane<ABL>(v.z, q.z, s, qmax, r.z) : 0u) << sh;
-                acc.w |= (i0 + 3 < n ? enc_lane<ABL>(v.w, q.w, s, qmax, r.w) : 0u) << sh;
+                acc.x |= enc_lane(v.x, q.x, s, qmax, r.x) << sh;
+                acc.y |= (i0 + 1 < n ? enc_lane(v.y, q.y, s, qmax, r.y) : 0u) << sh;
+                acc.z |= (i0 + 2 < n ? enc_lane(v.z, q.z, s, qmax, r.z) : 0u) << sh;
+                acc.w |= (i0 + 3 < n ? enc_lane(v.w, q.w, s, qmax, r.w) : 0u) << sh;
             }
         }
         *reinterpret_cast<uint4 *>(words + 4 * t) = acc;
     }
+}
+
+// the exact encode of word quad tq from split-plane draws, a plane at a time
+// (partial planes: n): the path of tiles with a tie, slow ranges, b > 8 and
+// tails.  Not inlined: the split tile's registers are not shared with it.
+template <int L, int KIND>
+__device__ __noinline__ void split_exact_quad(const float *__restrict__ x, uint64_t n, const DivNorm &dv, float s,
+                                              int32_t qmax, uint32_t w, uint64_t M, const RngArgs &rng,
+                                              uint32_t *__restrict__ words, uint64_t tq)
+{
+    uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll 1
+    for (int k = 0; k < L; ++k) {
+        const uint64_t i0 = (uint64_t)k * M + 4 * tq;
+        if (i0 >= n)
+            break;
+        float4 v;
+        if (i0 + 4 <= n) {
+            v = ld_nt(reinterpret_cast<const float4 *>(x + i0));
+        } else {
+            v.x = x[i0];
+            v.y = i0 + 1 < n ? x[i0 + 1] : 0.0f;
+            v.z = i0 + 2 < n ? x[i0 + 2] : 0.0f;
+            v.w = 0.0f;
+        }
+        const float4 q = quot4_exact(v, dv);
+        const uint4 r = draws4<KIND>(rng, 0, i0);
+        const uint32_t sh = (uint32_t)k * w;
+        acc.x |= enc_lane(v.x, q.x, s, qmax, r.x) << sh;
+        acc.y |= (i0 + 1 < n ? enc_lane(v.y, q.y, s, qmax, r.y) : 0u) << sh;
+        acc.z |= (i0 + 2 < n ? enc_lane(v.z, q.z, s, qmax, r.z) : 0u) << sh;
+        acc.w |= (i0 + 3 < n ? enc_lane(v.w, q.w, s, qmax, r.w) : 0u) << sh;
+    }
+    *reinterpret_cast<uint4 *>(words + 4 * tq) = acc;
+}
+
+// The encode from split-plane draws (GC_RNG_SPLIT8 / SPLIT16): a kernel of its
+// own, so the one heavy path (enc_tile_int_split) does not share its register
+// allocation with the Philox / stream paths (125 VGPRs: 4 waves per SIMD).
+// Full tiles in range take the split tile; a tile with a tie, a slow range,
+// b > 8, or a tail quad takes split_exact_quad, a separate function, so the
+// compiler can neither hoist its LO-plane loads above the tie check nor hold
+// its values across the split tile.
+template <int L, int KIND>
+__global__ __launch_bounds__(kBlock) void k_qsgd_encode_split(const float *__restrict__ x, uint64_t n,
+                                                              const float *__restrict__ normp, float s, int32_t qmax,
+                                                              uint32_t w, uint64_t M, RngArgs rng,
+                                                              uint32_t *__restrict__ words)
+{
+    static_assert(KIND == 4 || KIND == 5, "split-plane draws only");
+    static_assert(L <= 16, "the sign mask holds 4 L bits");
+    const float norm = *normp;
+    const DivNorm dv = make_div(norm);
+    const uint64_t quads = M >> 2;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t last = (uint64_t)(L - 1) * M;
+    const uint64_t full = (dv.fast && n >= last + 4 && n < (1ull << 32)) ? (n - last) >> 2 : 0;
+    const uint32_t M32 = (uint32_t)M;
+    const bool intok = s <= 255.0f, narrow = s <= 127.0f;
+    const float S24 = s * 16777216.0f;
+    const uint32_t lo2 = 2u * dv.lo1, hi2 = 2u * __float_as_uint(norm);
+    uint32_t Cw = 0;
+    for (int k = 0; k < L; ++k)
+        Cw += (uint32_t)qmax << (k * w);
+    for (; t < full; t += stride) {
+        const uint32_t t4 = (uint32_t)t * 4u;
+        bool done = false;
+        if (intok) {
+            float4 xv[L];
+#pragma unroll
+            for (int k = 0; k < L; ++k)
+                xv[k] = ld_nt(reinterpret_cast<const float4 *>(x + (k * M32 + t4)));
+            RangeI rg;
+#pragma unroll
+            for (int k = 0; k < L; ++k)
+                rg.add4(xv[k]);
+            if (__builtin_expect(!rg.slow(lo2, hi2), 1)) {
+                uint4 acc;
+                done = narrow ? enc_tile_int_split<L, KIND, false>(xv, t4, M32, dv, S24, w, Cw, rng, acc)
+                              : enc_tile_int_split<L, KIND, true>(xv, t4, M32, dv, S24, w, Cw, rng, acc);
+                if (done)
+                    store_words(words + t4, acc);
+            }
+        }
+        if (__builtin_expect(!done, 0))
+            split_exact_quad<L, KIND>(x, n, dv, s, qmax, w, M, rng, words, t);
+    }
+    for (; t < quads; t += stride)
+        split_exact_quad<L, KIND>(x, n, dv, s, qmax, w, M, rng, words, t);
 }
 
 }  // namespace gc

@@ -99,14 +99,14 @@ __global__ __launch_bounds__(kRkThreads) void k_randk_gather(const float *__rest
             const uint4 rd = draws4<KIND>(rng, 0, i0);
             Range rg;
             rg.add4(v);
-            const float4 ql = (dv.fast && !rg.slow(dv)) ? quot4_fast<0>(v, dv) : quot4_ieee(v, norm);
-            lane[i0] = (uint16_t)enc_lane<0>(v.x, ql.x, s, qmax, rd.x);
+            const float4 ql = (dv.fast && !rg.slow(dv)) ? quot4_fast(v, dv) : quot4_ieee(v, norm);
+            lane[i0] = (uint16_t)enc_lane(v.x, ql.x, s, qmax, rd.x);
             if (i0 + 1 < k)
-                lane[i0 + 1] = (uint16_t)enc_lane<0>(v.y, ql.y, s, qmax, rd.y);
+                lane[i0 + 1] = (uint16_t)enc_lane(v.y, ql.y, s, qmax, rd.y);
             if (i0 + 2 < k)
-                lane[i0 + 2] = (uint16_t)enc_lane<0>(v.z, ql.z, s, qmax, rd.z);
+                lane[i0 + 2] = (uint16_t)enc_lane(v.z, ql.z, s, qmax, rd.z);
             if (i0 + 3 < k)
-                lane[i0 + 3] = (uint16_t)enc_lane<0>(v.w, ql.w, s, qmax, rd.w);
+                lane[i0 + 3] = (uint16_t)enc_lane(v.w, ql.w, s, qmax, rd.w);
         }
         __syncthreads();
         for (uint32_t p = threadIdx.x; p < M; p += kRkThreads) {

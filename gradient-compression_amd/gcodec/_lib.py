@@ -22,6 +22,7 @@ GC_ENODEV = -5
 
 GC_I8, GC_I32, GC_I64 = 1, 4, 8
 GC_RNG_PHILOX, GC_RNG_STREAM, GC_RNG_STREAM24 = 0, 1, 2
+GC_RNG_SPLIT8, GC_RNG_SPLIT16 = 3, 4  # split-plane draws (include/gcodec.h)
 GC_MAX_LEVELS = 8
 GC_MT_JUMP_DRAWS = 262080  # include/gcodec.h: draws per generator of the parallel MT19937 stream
 
@@ -138,6 +139,9 @@ SIGNATURES = {
     "gc_mt19937_workspace_size_multi_j": (C.c_size_t, [u64, u64, u32]),
     "gc_mt19937_generate_multi_j": (C.c_int, [P, P, u64, u64, P, u32, u64, P, P, P, C.c_int, P]),
     "gc_mt19937_generate_multi24_j": (C.c_int, [P, P, u64, u64, P, u32, u64, u64, P, P, P, C.c_int, P]),
+    "gc_rng_split_bytes": (u64, [u64, u32]),
+    "gc_mt19937_generate_multi_split_j": (C.c_int, [P, P, u64, u64, P, u32, u64, u64, u32, P, P, u32, u32, u64, u64,
+                                                    P, C.c_int, P]),
     "gc_qsgdbp_decode": (C.c_int, [P, P, u64, P, P, P]),
     "gc_randk_workspace_size": (C.c_size_t, []),
     "gc_randk_gather_absmax": (C.c_int, [P, P, u64, P, P, P, P]),

@@ -150,18 +150,26 @@ def _absmax_ws(dev, stream) -> torch.Tensor:
     are cut from a pool zeroed once per device, so a stream's first call
     launches no fill: under HIP-graph capture (a capture stream is a new
     stream) a fill would be captured and re-run at every replay (VERDICT r04
-    item 6: the GRandK replay carried a FillFunctor node per step)."""
+    item 6: the GRandK replay carried a FillFunctor node per step).
+
+    A pool is never made under capture: its zero fill would only
+    be a graph node, so eager streams taking slots from it later would find
+    unzeroed tickets, and every replay would reset the slots of streams in
+    use.  A capture that needs a slot when no pool has one left raises; one
+    eager call on the device beforehand makes the pool (64 slots, a new pool
+    when they run out; a slot is 256 bytes and stays with its stream)."""
     key = (dev.index, stream.value)
     ws = _WS.get(key)
     if ws is None:
         size = -(-int(_lib.load().gc_absmax_workspace_size()) // 256) * 256
         pool = _WS_POOL.get(dev.index)
         if pool is None or pool[1] == _WS_POOL_SLOTS:
+            if torch.cuda.is_current_stream_capturing():
+                raise _lib.GCodecError(_lib.GC_EINVAL, "absmax: no zeroed workspace slot for a stream first seen "
+                                       "under HIP-graph capture; run one eager absmax on this device first")
             pool = _WS_POOL[dev.index] = [torch.zeros(size * _WS_POOL_SLOTS, dtype=torch.uint8, device=dev), 0]
-            if not torch.cuda.is_current_stream_capturing():
-                # other streams take slots later: the zero fill must be done
-                # (under capture the fill is a node of this graph instead)
-                torch.cuda.current_stream(dev).synchronize()
+            # other streams take slots later: the zero fill must be done
+            torch.cuda.current_stream(dev).synchronize()
         ws = _WS[key] = pool[0][pool[1] * size:(pool[1] + 1) * size]
         pool[1] += 1
     return ws
@@ -955,11 +963,15 @@ _MT_BUSY = {}  # (device index, slot) -> event after the last generators that re
 _MT_PREV = {}  # device index -> the count of the last mt19937_draws call
 _MT_NSLOT = {}  # device index -> the slot rotation the queued runs were enqueued with
 MT_SPECULATE = True  # generate the draws of the next same-size torch-mode calls ahead (mt19937_draws)
-# how many calls ahead: each speculative run holds 4 * count bytes of draws + one generator workspace
-# on the device until its call; runs start only after two calls in a row of the same count, and never
-# above MT_SPECULATE_MAX_DRAWS
-MT_SPECULATE_DEPTH = 16  # calls' draws kept enqueued ahead of the current one
+# how many calls ahead: each speculative run holds its calls' draws (mt_format_bytes each) + one
+# generator workspace on the device until its call; runs start only after two calls in a row of the
+# same count, and never above MT_SPECULATE_MAX_DRAWS
+MT_SPECULATE_DEPTH = 16  # calls' draws kept enqueued ahead of the current one (at most)
 MT_SPECULATE_MAX_DRAWS = 1 << 30  # per run (a run of MT_MULTI_CALLS calls holds that many times count)
+# device bytes the draws of the runs in flight (the current run's and those queued ahead) may hold
+# (bounded, visible through mt_reserved_bytes): the calls per run and the depth shrink to
+# fit it (_mt_plan); None = min(1 GiB, two runs of MT_MULTI_CALLS calls)
+MT_SPECULATE_BUDGET = None
 MT_MAX_SLOTS = 8  # workspace / pinned-state slots of the runs in flight
 # calls per run once a count repeats: one set of generators (and of generator
 # jumps, the LDS-bound part) makes the draws of this many consecutive calls,
@@ -1052,11 +1064,12 @@ class _MtRun:
     __slots__ = ("count", "packed", "out", "slot", "idx_end", "p1", "state_ready", "done", "calls", "k", "ends")
 
 
-def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int, packed: bool = False) -> _MtRun:
+def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int, fmt: str = "plain") -> _MtRun:
     """Phase 1 on the jump stream: sequence + jumps + the end state (written
     over st_dev, gc_mt19937_generate_split_j) and its copy into hout[slot];
     phase 2 on the generator stream, after phase 1: the draws (packed: their
     low 24 bits, 3 bytes each, gc_mt19937_generate_split24_j)."""
+    packed = fmt == "packed24"
     J = mt_pipe_generator_draws(count)
     gens = -(-count // J)
     js, gss = _mt_side(dev)
@@ -1068,7 +1081,8 @@ def _mt_enqueue(dev, st_dev, count: int, idx: int, hout, slot: int, packed: bool
     busy = _MT_BUSY.get((dev.index, slot))
     lib = _lib.load()
     run = _MtRun()
-    run.count, run.packed, run.slot, run.idx_end = count, packed, slot, idx + count - 624 * block
+    run.count, run.packed, run.slot, run.idx_end = count, "packed24" if packed else "plain", slot, \
+        idx + count - 624 * block
     run.calls, run.k, run.ends = 1, 0, None
     with torch.cuda.stream(js):
         if busy is not None:
@@ -1137,24 +1151,59 @@ def _mt_end_coefs(dev, blocks: tuple) -> torch.Tensor:
     return t
 
 
-_MT_BUDGET = {}  # device index -> bytes the queued draws may hold
+_MT_WARNED = set()  # (count, format) the budget turned speculation off for (warned once)
 
 
-def _mt_spec_budget(dev) -> int:
-    """Device bytes the speculative draws may hold: 1/32 of the device's memory
-    (9 GB on a 288 GB MI355X; ADVICE r04: the queued runs are invisible to the
-    caller)."""
-    b = _MT_BUDGET.get(dev.index)
-    if b is None:
-        b = _MT_BUDGET[dev.index] = int(torch.cuda.get_device_properties(dev).total_memory) // 32
-    return b
+def _mt_plan(count: int, fmt: str, multi: bool):
+    """(calls per run, calls kept ahead) for repeated calls of `count` draws in
+    format fmt under the speculation budget: the draws of the current run and
+    of the runs ahead, mt_format_bytes(count, fmt) per call, fit in
+    MT_SPECULATE_BUDGET bytes (default: the smaller of 1 GiB and two runs of
+    MT_MULTI_CALLS calls).  A run takes at most half of what fits, the rest is
+    depth (at most MT_SPECULATE_DEPTH).  When not even one call fits ahead the
+    speculation is off for this count (warned once: the calls then wait for
+    their draws)."""
+    calls_max = max(1, min(int(MT_MULTI_CALLS), MT_MULTI_MAX)) if multi else 1
+    bpc = max(1, mt_format_bytes(count, fmt))
+    budget = MT_SPECULATE_BUDGET
+    if budget is None:
+        budget = min(1 << 30, 2 * calls_max * bpc)
+    hold = int(budget) // bpc
+    calls = max(1, min(calls_max, hold // 2))
+    depth = max(0, min(int(MT_SPECULATE_DEPTH), hold - calls))
+    if depth == 0 and MT_SPECULATE and int(MT_SPECULATE_DEPTH) > 0 and (count, fmt) not in _MT_WARNED:
+        import warnings
+        _MT_WARNED.add((count, fmt))
+        warnings.warn(f"gcodec torch mode: {count} draws per call ({bpc} bytes as {fmt}) leave no room ahead in "
+                      f"the speculation budget of {int(budget)} bytes (codec.MT_SPECULATE_BUDGET): each call "
+                      "waits for its own draws", RuntimeWarning, stacklevel=3)
+    return calls, depth
 
 
-def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int, packed: bool = False) -> _MtRun:
+def mt_format_bytes(count: int, fmt: str) -> int:
+    """Device bytes of one call's `count` draws in format fmt ("plain": 4 per
+    draw, "packed24": 3, "split8" / "split16": the two planes of
+    gc_rng_split_bytes, 16-byte padded)."""
+    if fmt == "plain":
+        return 4 * count
+    if fmt == "packed24":
+        return 3 * count
+    return int(_lib.load().gc_rng_split_bytes(count, _SPLIT_BITS[fmt]))
+
+
+_SPLIT_BITS = {"split8": 8, "split16": 16}
+_FMT_KIND = {"plain": _lib.GC_RNG_STREAM, "packed24": _lib.GC_RNG_STREAM24, "split8": _lib.GC_RNG_SPLIT8,
+             "split16": _lib.GC_RNG_SPLIT16}
+
+
+def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int, fmt: str = "plain") -> _MtRun:
     """Like _mt_enqueue for `calls` consecutive calls of `count` draws: one
     generation of calls * count draws, the end state after each call's slice
-    (gc_mt19937_generate_multi_j; packed: the 24-bit draws of
-    gc_mt19937_generate_multi24_j, count and idx multiples of 4).  count >= 624."""
+    (gc_mt19937_generate_multi_j; "packed24": the 24-bit draws of
+    gc_mt19937_generate_multi24_j; "split8" / "split16": the split-plane
+    regions of gc_mt19937_generate_multi_split_j, one per call; both need
+    count and idx multiples of 4).  count >= 624."""
+    packed = fmt == "packed24"
     total = count * calls
     J = mt_pipe_generator_draws(total, True)
     gens = -(-total // J)
@@ -1183,11 +1232,16 @@ def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int, 
         with torch.cuda.stream(js):
             dev_ends = _MT_ENDS[("dev",) + key] = torch.empty((MT_MULTI_MAX, 626), dtype=torch.int32, device=dev)
     run = _MtRun()
-    run.count, run.packed, run.slot, run.calls, run.k = count, bool(packed), slot, calls, 0
+    run.count, run.packed, run.slot, run.calls, run.k = count, fmt, slot, calls, 0
     run.idx_end = idx + total - 624 * blocks[-1]
 
     def gen(out, phase):
-        if packed:
+        if fmt in _SPLIT_BITS:
+            check(lib.gc_mt19937_generate_multi_split_j(_p(st_dev), _p(table), tgens, J, _p(ends), calls, count, idx,
+                                                        _SPLIT_BITS[fmt], _p(dev_ends), out, 0, 0, 0,
+                                                        0xFFFFFFFFFFFFFFFF, _p(ws), phase, _stream(dev)),
+                  "gc_mt19937_generate_multi_split_j")
+        elif packed:
             check(lib.gc_mt19937_generate_multi24_j(_p(st_dev), _p(table), tgens, J, _p(ends), calls, count, idx,
                                                     _p(dev_ends), out, _p(ws), phase, _stream(dev)),
                   "gc_mt19937_generate_multi24_j")
@@ -1212,7 +1266,10 @@ def _mt_enqueue_multi(dev, st_dev, count: int, calls: int, idx: int, slot: int, 
             t.record_stream(gs)
     with torch.cuda.stream(gs):
         gs.wait_event(run.p1)
-        run.out = torch.empty(total // 4 * 3 if packed else total, dtype=torch.int32, device=dev)
+        if fmt in _SPLIT_BITS:
+            run.out = torch.empty(calls * mt_format_bytes(count, fmt), dtype=torch.uint8, device=dev)
+        else:
+            run.out = torch.empty(total // 4 * 3 if packed else total, dtype=torch.int32, device=dev)
         gen(_p(run.out), 2)
         run.done = torch.cuda.Event()
         run.done.record()
@@ -1227,17 +1284,29 @@ def mt19937_packable(count: int, idx: int) -> bool:
 
 
 def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
+    """`count` draws of torch's CPU generator on `device` (see mt19937_reserve):
+    the plain 32-bit draws, or with packed24 where mt19937_packable their low
+    24 bits, 3 bytes each (GC_RNG_STREAM24; the caller tells the two apart by
+    numel)."""
+    return mt19937_reserve(count, device, "packed24" if packed24 else "plain")[0]
+
+
+def mt19937_reserve(count: int, device, fmt: str = "plain"):
     """`count` draws of torch's CPU generator, produced on `device`; torch's
     generator state advances exactly as torch.bernoulli would advance it
     (synchronously: the new state is in torch's generator when this returns).
+    Returns (draws tensor, gc_rng kind).
 
-    packed24: where mt19937_packable (count and torch's read index multiples
-    of 4), return only each draw's low 24 bits, 3 bytes per draw little-endian
-    (3 count / 4 int32 words: GC_RNG_STREAM24, the QSGD encode reads a 12-byte
-    quad per 4 elements), else the plain draws; the caller tells the two apart
-    by numel.  torch's rounding reads only those 24 bits (compressors.py:301
-    via torch.rand), so the encode is bit-identical either way and moves 25 %
-    fewer draw bytes (written once, read once).
+    fmt: "plain" = the 32-bit draws (int32, GC_RNG_STREAM).  Where
+    mt19937_packable (count and torch's read index multiples of 4) the draws
+    can be cut to the 24 bits torch's rounding reads (compressors.py:301 via
+    torch.rand), so the encode is bit-identical and moves fewer draw bytes:
+    "packed24" = 3 bytes per draw (GC_RNG_STREAM24).  For count >= 624 (any
+    read index) "split8" / "split16" = one HI plane of the top 8 / 16 of those
+    bits and one LO plane of the rest (uint8 region of mt_format_bytes bytes,
+    GC_RNG_SPLIT8 / SPLIT16): the encode reads the LO plane only where the HI
+    bits tie (about 1 draw in 2^8 / 2^16).  A request the run cannot honour
+    gets plain draws.
 
     The draws are generated on two high-priority side streams
     (gc_mt19937_generate_split_j): phase 1 (jump stream) = the state's
@@ -1265,10 +1334,15 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     _MT_PREV[d] = count
     last = _MT_LAST.get(d)
     untouched = last is not None and last[1] == idx and np.array_equal(last[0], words)
-    depth = max(0, int(MT_SPECULATE_DEPTH))
-    packed = bool(packed24) and count > 0 and mt19937_packable(count, int(idx))
-    multi = count >= 624  # multi-call runs (gc_mt19937_generate_multi_j / _multi24_j)
-    calls = max(1, min(int(MT_MULTI_CALLS), MT_MULTI_MAX)) if multi else 1
+
+    multi = count >= 624  # multi-call runs (gc_mt19937_generate_multi_j / _multi24_j / _multi_split_j)
+    if fmt not in _FMT_KIND:
+        raise ValueError(f"mt19937_reserve: unknown draw format {fmt!r}")
+    if fmt == "packed24" and not (count > 0 and mt19937_packable(count, int(idx))):
+        fmt = "plain"
+    if fmt in _SPLIT_BITS and not multi:  # the split planes come from multi-call runs (count >= 624)
+        fmt = "plain"
+    calls, depth = _mt_plan(count, fmt, multi) if count > 0 else (1, 0)
     # slots in rotation: the runs in flight (the current one, those holding the
     # next `depth` calls: ceil(depth / calls) runs, one more while the current
     # run still has calls left) + one; a change of the rotation drops the queue
@@ -1293,16 +1367,15 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     if count == 0:
         if queue or dropped:  # dropped runs still moved dst on: send the state next time
             _MT_LAST.pop(d, None)
-        return torch.empty(0, dtype=torch.int32, device=device)
+        return torch.empty(0, dtype=torch.int32, device=device), _lib.GC_RNG_STREAM
 
     def enqueue(st_idx, ncalls):
+        f = fmt if fmt != "packed24" or mt19937_packable(count, st_idx) else "plain"
         if multi:
-            return _mt_enqueue_multi(device, dst, count, ncalls, st_idx, next_slot(),
-                                     packed and mt19937_packable(count, st_idx))
-        return _mt_enqueue(device, dst, count, st_idx, hout, next_slot(),
-                           packed and mt19937_packable(count, st_idx))
+            return _mt_enqueue_multi(device, dst, count, ncalls, st_idx, next_slot(), f)
+        return _mt_enqueue(device, dst, count, st_idx, hout, next_slot(), f)
 
-    if queue and untouched and queue[0].count == count and queue[0].packed == packed:
+    if queue and untouched and queue[0].count == count and queue[0].packed == fmt:
         run = queue[0]
     else:
         if queue or dropped or not untouched:  # dst is not torch's state: send it
@@ -1317,8 +1390,7 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     run.k = k + 1
     if run.k >= run.calls:
         queue.pop(0)
-    if MT_SPECULATE and repeat and count * calls <= MT_SPECULATE_MAX_DRAWS and \
-            4 * count * (depth + calls) <= _mt_spec_budget(device):
+    if MT_SPECULATE and repeat and depth > 0 and count * calls <= MT_SPECULATE_MAX_DRAWS:
         ahead = sum(r.calls - r.k for r in queue)
         behind = sum(1 for r in queue if r is not run)  # runs enqueued after this one
         # calls' draws enqueued behind this one, chained from the last run's end;
@@ -1333,7 +1405,7 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     cur.wait_event(run.done)
     if queue and MT_WAIT_NEXT_JUMPS:
         cur.wait_event(queue[0].p1)
-    per = count // 4 * 3 if run.packed else count
+    per = {"plain": count, "packed24": count // 4 * 3}.get(run.packed) or mt_format_bytes(count, run.packed)
     out = run.out[k * per:(k + 1) * per] if run.calls > 1 else run.out
     run.out.record_stream(cur)
     if queue:
@@ -1346,7 +1418,33 @@ def mt19937_draws(count: int, device, packed24: bool = False) -> torch.Tensor:
     w2, i2 = new[:624].copy(), int(new[624])
     set_torch_mt_state(w2, i2)
     _MT_LAST[d] = (w2, i2)
-    return out
+    return out, _FMT_KIND[run.packed]
+
+
+def mt_reserved_bytes(device=None) -> int:
+    """Device bytes the torch-mode machinery holds on `device` (all devices if
+    None) between calls, invisible to the caller: the queued speculative runs'
+    draws, the generator workspaces, the jump and end-coefficient tables and
+    the per-slot end-state buffers.  mt_release() frees them."""
+    if device is not None:
+        device = torch.device(device)
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+    want = (lambda d: True) if device is None else (lambda d: d == device.index)
+
+    def nb(t):
+        return t.numel() * t.element_size()
+
+    total = 0
+    for d, runs in _MT_SPEC.items():
+        if want(d):
+            total += sum(nb(r.out) for r in runs if getattr(r, "out", None) is not None)
+    total += sum(nb(t) for k, t in _MT_WSS.items() if want(k[0]))
+    total += sum(nb(v[0]) for k, v in _MT_TABLE.items() if want(k[0]))
+    total += sum(nb(t) for k, t in _MT_ENDCAT.items() if want(k[0]))
+    total += sum(nb(t) for k, t in _MT_END.items() if want(k[0]))
+    total += sum(nb(t) for k, t in _MT_ENDS.items() if k[0] == "dev" and want(k[1]))
+    return int(total)
 
 
 def mt_release(device=None):
@@ -1454,9 +1552,10 @@ class Greedy4Device:
     def pack(self, a: torch.Tensor):
         """a: int32 [n] on the device -> self.words (count via result())."""
         assert a.dtype == torch.int32 and a.numel() == self.n and a.is_contiguous()
-        check(_lib.load().gc_greedy4_pack_device(_p(a), self.n, _p(self.words), self.cap, _p(self.res),
-                                                 C.c_void_p(self.res.data_ptr() + 8), _p(self.ws),
-                                                 _stream(self.device)), "gc_greedy4_pack_device")
+        with _g4_one_pack(self.device):
+            check(_lib.load().gc_greedy4_pack_device(_p(a), self.n, _p(self.words), self.cap, _p(self.res),
+                                                     C.c_void_p(self.res.data_ptr() + 8), _p(self.ws),
+                                                     _stream(self.device)), "gc_greedy4_pack_device")
 
     def unpack(self, w: torch.Tensor):
         """w: int32 words on the device -> self.values (count via unpack_result())."""
@@ -1466,8 +1565,14 @@ class Greedy4Device:
                                                    _stream(self.device)), "gc_greedy4_unpack_device")
 
     def result(self, what: str = "greedy4_pack") -> int:
-        """The last pack's word count."""
-        return _g4_result(self.res, what)
+        """The last pack's word count.  After a timed-out pack (status 4) the
+        workspace is zeroed again before raising (blocks that start
+        late tag their granules with the next launch's tags, which the next
+        pack would otherwise compose as valid)."""
+        count, status = (int(v) for v in self.res.cpu().tolist())
+        if status & 4:
+            self.ws.zero_()
+        return _g4_check(count, status, what)
 
     def unpack_result(self, what: str = "greedy4_unpack") -> int:
         """The last unpack's value count."""
@@ -1493,14 +1598,39 @@ def greedy4_pack(src: torch.Tensor) -> torch.Tensor:
     return torch.from_numpy(out[:nw].copy())
 
 
-_G4_WS = {}  # (device index, stream) -> the pack workspace, zeroed once (every pack leaves it so)
+_G4_WS = {}  # device index -> the pack workspace, zeroed once (every pack leaves it so)
+_G4_LAST = {}  # device index -> (event after the last pack enqueued on the device, its stream)
 
 
-def _g4_pack_ws(dev, stream) -> torch.Tensor:
-    key = (dev.index, stream.value)  # stream: the raw HIP stream (_stream)
-    ws = _G4_WS.get(key)
+class _g4_one_pack:
+    """One persistent pack in flight per device (gcodec.h): a pack
+    enqueued on a stream other than the previous pack's waits for that pack's
+    event, then records its own."""
+
+    def __init__(self, dev):
+        self.dev = dev
+
+    def __enter__(self):
+        cur = torch.cuda.current_stream(self.dev)
+        last = _G4_LAST.get(self.dev.index)
+        if last is not None and last[1] != cur:
+            cur.wait_event(last[0])
+        self.cur = cur
+        return self
+
+    def __exit__(self, *exc):
+        ev = torch.cuda.Event()
+        ev.record(self.cur)
+        _G4_LAST[self.dev.index] = (ev, self.cur)
+        return False
+
+
+def _g4_pack_ws(dev) -> torch.Tensor:
+    """The device's one pack workspace (one pack in flight per device)."""
+    ws = _G4_WS.get(dev.index)
     if ws is None:
-        ws = _G4_WS[key] = torch.zeros(int(_lib.load().gc_greedy4_workspace_size(0)), dtype=torch.uint8, device=dev)
+        ws = _G4_WS[dev.index] = torch.zeros(int(_lib.load().gc_greedy4_workspace_size(0)), dtype=torch.uint8,
+                                             device=dev)
     return ws
 
 
@@ -1518,23 +1648,24 @@ def greedy4_pack_many(*srcs: torch.Tensor) -> list:
         raise ValueError("greedy4_pack_many: arrays on different devices")
     lib = _lib.load()
     st = _stream(dev)
-    ws = _g4_pack_ws(dev, st)
-    res = torch.empty(2 * len(srcs), dtype=torch.int64, device=dev)  # (count, status) per pack, written by each
+    ws = _g4_pack_ws(dev)
+    res = torch.zeros(2 * len(srcs), dtype=torch.int64, device=dev)  # (count, status) per pack, written by each
     outs, keep = [], []
-    for i, src in enumerate(srcs):
-        a = src.detach().contiguous().view(-1)
-        if a.dtype != torch.int32:
-            a = a.to(torch.int32)
-        keep.append(a)  # alive until the launches are enqueued (the stream orders their use)
-        cap = a.numel() // 3 + 2
-        words = torch.empty(cap, dtype=torch.int32, device=dev)
-        check(lib.gc_greedy4_pack_device(_p(a), a.numel(), _p(words), cap, C.c_void_p(res.data_ptr() + 16 * i),
-                                         C.c_void_p(res.data_ptr() + 16 * i + 8), _p(ws), st),
-              "gc_greedy4_pack_device")
-        outs.append(words)
+    with _g4_one_pack(dev):
+        for i, src in enumerate(srcs):
+            a = src.detach().contiguous().view(-1)
+            if a.dtype != torch.int32:
+                a = a.to(torch.int32)
+            keep.append(a)  # alive until the launches are enqueued (the stream orders their use)
+            cap = a.numel() // 3 + 2
+            words = torch.empty(cap, dtype=torch.int32, device=dev)
+            check(lib.gc_greedy4_pack_device(_p(a), a.numel(), _p(words), cap, C.c_void_p(res.data_ptr() + 16 * i),
+                                             C.c_void_p(res.data_ptr() + 16 * i + 8), _p(ws), st),
+                  "gc_greedy4_pack_device")
+            outs.append(words)
     pairs = res.cpu().view(-1, 2).tolist()
     if any(int(stt) & 4 for _, stt in pairs):
-        _G4_WS.pop((dev.index, st.value), None)  # a timed-out pack: zero it again
+        ws.zero_()  # a timed-out pack: zero the workspace again (the stream orders it after the packs)
     return [w[:_g4_check(int(c), int(stt), "greedy4_pack")] for w, (c, stt) in zip(outs, pairs)]
 
 

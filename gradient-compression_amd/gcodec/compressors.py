@@ -36,12 +36,12 @@ def _qdtype(bits: int) -> torch.dtype:
     return torch.int8 if bits < 8 else torch.int32
 
 
-# torch mode: whether the QSGD encode asks for 24-bit packed draws
-# (rng.Generator.reserve packed24).  Off: on MI355X the packed generator made
-# the back-to-back 1e8 encode slower, 0.39 against 0.34 ms per call
-# (profiles/r04p_torch_mode_ab.log) although it moves 200 MB less per call —
-# the call is bound by the side streams' jump + generator chain, not HBM.
-PACKED24_DRAWS = False
+# torch mode: the draw format the packed QSGD encode asks for
+# (rng.Generator.reserve fmt; codec.mt19937_reserve): "plain" 32-bit draws,
+# "packed24" (3 bytes per draw), or the split planes "split8" / "split16"
+# (the encode reads 1 / 2 bytes per draw and the rest only where the rounding
+# is undecided).  Formats the run cannot take fall back to plain draws.
+TORCH_DRAW_FORMAT = "split16"
 
 
 class _Base:
@@ -51,9 +51,9 @@ class _Base:
         self._device = device
         self._gen = generator or default_generator
 
-    def _reserve(self, n: int, levels: int, device, packed24: bool = False):
-        if packed24:  # torch mode: 24-bit packed draws where the run allows (rng.Generator.reserve)
-            return self._gen.reserve(n, levels, device=device, backend=self.backend, packed24=True)
+    def _reserve(self, n: int, levels: int, device, fmt: str | None = None):
+        if fmt and fmt != "plain":  # torch mode: cut draws where the run allows (rng.Generator.reserve)
+            return self._gen.reserve(n, levels, device=device, backend=self.backend, fmt=fmt)
         return self._gen.reserve(n, levels, device=device, backend=self.backend)
 
 
@@ -79,7 +79,7 @@ class QSGDMaxNormCompressor(_Base):
     # packed, SUM-all-reduce-compatible stream (carry-free lanes for `world`)
     def encode(self, norm, tensor, world=1, idx=None, out=None):
         n = idx.numel() if idx is not None else tensor.numel()
-        rng = self._reserve(n, 1, tensor.device, packed24=PACKED24_DRAWS)
+        rng = self._reserve(n, 1, tensor.device, fmt=TORCH_DRAW_FORMAT)
         return self.backend.qsgd_encode(tensor, norm, self._quantization_level, rng, world, idx, out)
 
     def decode(self, norm, words, n, world=1, alpha=1.0, idx=None, out=None):

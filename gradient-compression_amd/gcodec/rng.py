@@ -112,11 +112,14 @@ class Generator:
         """The Philox key the next reservation uses (seed, + rank if per_rank)."""
         return self.seed + (_process_rank() if self.per_rank else 0)
 
-    def reserve(self, n: int, levels: int = 1, device=None, backend=None, packed24: bool = False) -> Reservation:
+    def reserve(self, n: int, levels: int = 1, device=None, backend=None, packed24: bool = False,
+                fmt: str | None = None) -> Reservation:
         """Reserve n*levels draws (advances the stream like torch's generator).
-        packed24 (torch mode, one level): the draws' low 24 bits packed 3 bytes
-        each where the run allows it (codec.mt19937_draws); only the QSGD
-        encode (gc_qsgd_encode) takes such a reservation."""
+        Torch mode, one level: fmt "packed24" (or packed24=True) / "split8" /
+        "split16" cuts the draws to the 24 bits the rounding reads where the
+        run allows it (codec.mt19937_reserve), else the plain 32-bit draws are
+        returned; only the QSGD encode (gc_qsgd_encode) takes such a
+        reservation."""
         count = n * levels
         if self.mode == "philox":
             r = Reservation(_lib.GC_RNG_PHILOX, self.reserve_key(), self.offset, None, n, levels)
@@ -124,7 +127,11 @@ class Generator:
             return r
         if backend is None:
             from . import codec as backend
-        if packed24 and levels == 1:
+        fmt = fmt or ("packed24" if packed24 else "plain")
+        if fmt != "plain" and levels == 1 and hasattr(backend, "mt19937_reserve"):
+            stream, kind = backend.mt19937_reserve(count, device, fmt)
+            return Reservation(kind, 0, 0, stream, n, levels)
+        if fmt == "packed24" and levels == 1:
             stream = backend.mt19937_draws(count, device, packed24=True)
             kind = _lib.GC_RNG_STREAM24 if count and stream.numel() != count else _lib.GC_RNG_STREAM
             return Reservation(kind, 0, 0, stream, n, levels)
@@ -132,9 +139,16 @@ class Generator:
         return Reservation(_lib.GC_RNG_STREAM, 0, 0, stream, n, levels)
 
 
-# the stream every compressor / reducer / pipeline uses when none is passed:
-# one object per process, keyed per rank (see Generator)
-default_generator = Generator(per_rank=True)
+# The mode of the stream every compressor / reducer / pipeline uses when none
+# is passed: "torch", so the reference-named classes give the reference's
+# integers with no mode call (torch.manual_seed(s) then compress, exactly as
+# compressors.py:299-316 under seed.py:6-11).  "philox" is the fast,
+# non-identical stream: gcodec.manual_seed(seed, mode="philox"),
+# gcodec.set_rng_mode("philox") or an explicit gcodec.Generator(seed, "philox").
+DEFAULT_MODE = "torch"
+
+# one object per process; in philox mode keyed per rank (see Generator)
+default_generator = Generator(per_rank=True, mode=DEFAULT_MODE)
 
 
 def manual_seed(seed: int, mode: str | None = None, per_rank: bool | None = None) -> Generator:

@@ -76,11 +76,20 @@ extern "C" {
  * level: gc_qsgd_encode only (the torch-mode encode's draws from
  * gc_mt19937_generate_split24_j); stream 4-byte aligned */
 #define GC_RNG_STREAM24 2u
+/* caller-supplied draws cut into two planes (torch-mode encode): of draw i's
+ * low 24 bits, the top hb bits (hb = 8: SPLIT8, 16: SPLIT16) in the HI plane
+ * (hb/8 bytes per draw, little-endian) and the rest in the LO plane, which
+ * starts at stream + roundup(n * hb/8, 16) bytes; gc_rng_split_bytes(n, hb)
+ * bytes in all.  The encode reads the LO plane only for the quads whose HI
+ * bits leave the rounding undecided (about 1 draw in 2^hb).  One level:
+ * gc_qsgd_encode only; stream 16-byte aligned (gc_mt19937_generate_multi_split_j) */
+#define GC_RNG_SPLIT8 3u
+#define GC_RNG_SPLIT16 4u
 
 typedef void *gc_stream_t; /* hipStream_t */
 
 typedef struct gc_rng {
-    uint32_t kind;          /* GC_RNG_PHILOX | GC_RNG_STREAM | GC_RNG_STREAM24 */
+    uint32_t kind;          /* GC_RNG_PHILOX | GC_RNG_STREAM | GC_RNG_STREAM24 | GC_RNG_SPLIT8 | GC_RNG_SPLIT16 */
     uint32_t reserved;      /* 0 */
     uint64_t seed;          /* PHILOX key */
     uint64_t offset;        /* PHILOX: draws consumed before this call (counter high words) */
@@ -222,8 +231,14 @@ int gc_randk_encode_w1_segments(const gc_segments *segs, const int64_t *idx, uin
  * workspace: gc_greedy4[_unpack]_workspace_size bytes, device.  The PACK
  * workspace must be zero-filled before its first use and is left that way by
  * every call (after status 4: zero it again); the unpack workspace needs no
- * initialisation.  One pack at a time per pack workspace.  unpack emits whole
- * words (the caller truncates, as compressors.py:371 does). */
+ * initialisation.  One pack at a time per pack workspace, and one pack in
+ * flight per DEVICE: the pack is persistent (one block per CU, each waiting
+ * for every block of its launch), so two packs running at once on different
+ * streams can hold the CUs each other's blocks need until both time out —
+ * order packs on different streams with events.  Status 4 = some block
+ * waited longer than ~1.3 s (every block's timeout is collected); the words
+ * are then incomplete.  unpack emits whole words (the caller truncates, as
+ * compressors.py:371 does). */
 size_t gc_greedy4_workspace_size(uint64_t n);
 int gc_greedy4_pack_device(const int32_t *src, uint64_t n, int32_t *out, uint64_t cap, uint64_t *nwords,
                            uint32_t *status, void *workspace, gc_stream_t stream);
@@ -416,6 +431,20 @@ int gc_mt19937_generate_multi_j(uint32_t *state_dev, const uint32_t *table_dev, 
 int gc_mt19937_generate_multi24_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
                                   const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint64_t idx,
                                   uint32_t *ends_out, uint32_t *out, void *workspace, int phase, gc_stream_t stream);
+/* gc_mt19937_generate_multi_j writing split-plane draws (GC_RNG_SPLIT8 /
+ * SPLIT16 for hi_bits 8 / 16): call k's draws form one region of
+ * gc_rng_split_bytes(per_end, hi_bits) bytes at out + slot * that, slot = k
+ * (ring = 0) or (ring0 + k) % ring (ring >= 2: a ring of regions, ring0 <
+ * ring).  Phase 2 runs generators g_first .. g_first + g_count - 1 of the run
+ * (g_count = UINT64_MAX: all); generator g's draws [g J, (g + 1) J) may end in
+ * the next call's region.  Any read index and per_end (>= 624); out 16-byte
+ * aligned.  gc_rng_split_bytes returns 0 for other hi_bits. */
+uint64_t gc_rng_split_bytes(uint64_t n, uint32_t hi_bits);
+int gc_mt19937_generate_multi_split_j(uint32_t *state_dev, const uint32_t *table_dev, uint64_t table_gens, uint64_t J,
+                                      const uint32_t *end_coefs, uint32_t nend, uint64_t per_end, uint64_t idx,
+                                      uint32_t hi_bits, uint32_t *ends_out, void *out, uint32_t ring, uint32_t ring0,
+                                      uint64_t g_first, uint64_t g_count, void *workspace, int phase,
+                                      gc_stream_t stream);
 /* gc_mt19937_generate_split_j with the draws packed to 24 bits (the
  * GC_RNG_STREAM24 layout: 3 count / 4 words of out).  idx = the state's read
  * index (state_dev[624], which the caller sent); idx and count must be

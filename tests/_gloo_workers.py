@@ -232,12 +232,14 @@ def topology_world(rank, world, init_file, out_dir, local_size):
 
 def default_generator_world(rank, world, init_file, out_dir):
     """QSGDMaxNormCompressor.encode with NO generator argument on identical
-    inputs on every rank (oracle codec on CPU)."""
+    inputs on every rank (oracle codec on CPU), the default generator in its
+    philox mode (the per-rank key; the default mode is torch)."""
     import gcodec
     import oracle_codec
     from oracle import oracle as O
 
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    gcodec.set_rng_mode("philox")
     x = O.gen_input(10_001, seed=3)
     comp = gcodec.QSGDMaxNormCompressor(torch.device("cpu"), 4)
     comp.backend = oracle_codec

@@ -20,3 +20,17 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture(autouse=True)
+def _default_rng_mode():
+    """Every test starts and ends with the package's default RNG mode (a test
+    that switches the default generator's mode must not leak it)."""
+    yield
+    try:
+        import gcodec
+    except Exception:  # the package did not import: nothing to restore
+        return
+    g = gcodec.rng.default_generator
+    if g.mode != gcodec.rng.DEFAULT_MODE:
+        g.set_mode(gcodec.rng.DEFAULT_MODE)

@@ -44,7 +44,7 @@ def torch_mode():
     try:
         yield
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
 
 
 def _x(meta):

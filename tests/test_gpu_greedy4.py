@@ -197,3 +197,50 @@ def test_device_unpack_capacity_writes_nothing(nwords):
             assert torch.equal(out[:need], codec.greedy4_unpack(w))
         else:
             assert status == 2 and bool((out == -7).all())
+
+
+def test_late_block_timeout_is_reported_and_workspace_rearmed():
+    """a pack whose block 0 starts ~1.5 s late (the
+    header's test_delay field; 0 in every product workspace).  Every other
+    block times out waiting for block 0's round-0 granules and writes none of
+    its words; block 0 then sees every granule and, alone, would have
+    reported status 0.  Every block's timeout is collected now: the status is
+    4 and result() raises.  It also zeroes the workspace again before raising
+    (late blocks tag granules with the next launch's tags), so the
+    next pack on the same object is exact."""
+    rng = np.random.default_rng(5)
+    src = rng.choice([0, 1, 3, 9, 15, 100, 255], 3_000_000).astype(np.int32)
+    a = torch.from_numpy(src).to(DEV)
+    want = codec.greedy4_pack(a.cpu()).numpy()
+    pk = codec.Greedy4Device(a.numel(), DEV, unpack_words=0)
+    pk.pack(a)
+    assert np.array_equal(pk.words[:pk.result()].cpu().numpy(), want)
+    # G1Hdr: seq u64 @0, done u32 @8, tmo u32 @12, test_delay u64 @16 (100 MHz ticks)
+    pk.ws[16:24] = torch.tensor([150_000_000], dtype=torch.int64).view(torch.uint8).to(DEV)
+    pk.pack(a)
+    with pytest.raises(gcodec.GCodecError):
+        pk.result()
+    assert int(pk.ws.count_nonzero()) == 0
+    pk.pack(a)
+    assert np.array_equal(pk.words[:pk.result()].cpu().numpy(), want)
+
+
+def test_packs_on_two_streams_run_one_at_a_time():
+    """one persistent pack in flight per device — a pack enqueued
+    on a second stream waits for the first stream's pack (event), so the two
+    never hold each other's CUs; both results are exact."""
+    rng = np.random.default_rng(6)
+    srcs = [torch.from_numpy(rng.choice([0, 3, 15, 200], 2_000_000).astype(np.int32)).to(DEV) for _ in range(2)]
+    want = [codec.greedy4_pack(s.cpu()).numpy() for s in srcs]
+    s1, s2 = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+    for s in (s1, s2):
+        s.wait_stream(torch.cuda.current_stream(DEV))
+    pks = [codec.Greedy4Device(s.numel(), DEV, unpack_words=0) for s in srcs]
+    with torch.cuda.stream(s1):
+        torch.cuda._sleep(20_000_000)  # the first pack starts late: the second must wait for it
+        pks[0].pack(srcs[0])
+    with torch.cuda.stream(s2):
+        pks[1].pack(srcs[1])
+    torch.cuda.synchronize()
+    for pk, w in zip(pks, want):
+        assert np.array_equal(pk.words[:pk.result()].cpu().numpy(), w)

@@ -250,7 +250,29 @@ def test_facade_compress_matches_reference(case):
         w, L, M = O.lane_layout(x.size, 2 * s, 1)
         assert bits_eq(u32(words), O.lane_pack(q.astype(np.int32), s, w, L, M))
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
+
+
+def test_default_mode_is_reference_identical():
+    """with NO mode call, the reference-named class gives
+    the reference's integers (golden.json:qsgd_b4_1e6_k0, made by importing
+    compressors.py) after torch.manual_seed, and its packed encode the same q
+    lane-packed; philox stays an explicit opt-in."""
+    import hashlib
+
+    assert gcodec.rng.default_generator.mode == "torch"
+    meta = json.load(open(os.path.join(GOLD, "golden.json")))["digests"]["qsgd_b4_1e6_k0"]
+    x = O.gen_input(meta["n"], seed=42, kind=meta["kind"])
+    xd = dev(x)
+    norm = codec.absmax(xd)
+    torch.manual_seed(42)
+    q = gcodec.QSGDMaxNormCompressor(DEV, meta["bits"]).compress(norm, xd)
+    assert hashlib.sha256(q.cpu().numpy().tobytes()).hexdigest() == meta["q"]
+    torch.manual_seed(42)
+    words = gcodec.QSGDMaxNormCompressor(DEV, meta["bits"]).encode(norm, xd)
+    s = (1 << meta["bits"]) - 1
+    w, L, M = O.lane_layout(x.size, 2 * s, 1)
+    assert bits_eq(u32(words), O.lane_pack(q.cpu().numpy().astype(np.int32), s, w, L, M))
 
 
 def test_torch_generator_state_advances_like_reference():
@@ -264,7 +286,7 @@ def test_torch_generator_state_advances_like_reference():
         torch.bernoulli(torch.full((3001,), 0.5))
         assert torch.equal(after, torch.rand(5))
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
 
 
 def test_mt19937_kernel_matches_oracle():
@@ -375,7 +397,7 @@ def test_large_digest_torch_mode(name):
         d = c.decompress(norm, q)
         assert hashlib.sha256(d.cpu().numpy().tobytes()).hexdigest() == meta["dec"]
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
 
 
 # --------------------------------------------------------------------------- two-/multi-scale
@@ -400,7 +422,7 @@ def test_two_scale_facade_matches_reference(lohi):
         d = comp.decompress(nt, q, h)
         assert bits_eq(u32(d), z[f"{c}/dec"].view(np.uint32))
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
 
 
 @pytest.mark.parametrize("levels", [(2, 4), (4, 8), (2, 4, 6), (3, 5, 7, 9), (6, 10)])
@@ -420,7 +442,7 @@ def test_multi_scale_facade_matches_reference(levels):
         d = comp.decompress(nt, q, mask)
         assert bits_eq(u32(d), z[f"{c}/dec"].view(np.uint32))
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
 
 
 @pytest.mark.parametrize("levels", [(2, 4), (4, 8), (2, 4, 6), (3, 5, 7, 9)])
@@ -563,7 +585,7 @@ def test_grandk_torch_mode_matches_reference(case):
         qk = c.compress(nk, bd[dev(idx)])
         assert bits_eq(qk.cpu().numpy(), q)
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
 
 
 # --------------------------------------------------------------------------- packers
@@ -686,7 +708,7 @@ def test_chunked_pipeline_world1(chunks):
         torch.cuda.synchronize()
         assert bits_eq(u32(got), u32(ref))
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
     gen = gcodec.Generator(99, "philox")
     pipe = gcodec.ChunkedQSGDAllReduce(n, bits, DEV, chunks=chunks, generator=gen)
     got = pipe(xd).cpu().numpy()
@@ -757,7 +779,7 @@ def test_config5_chunked_8bit_1e8(world):
         torch.cuda.synchronize()
         assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
     pipe = _IdenticalRanks(n, bits, DEV, chunks=chunks, world=world, generator=gcodec.Generator(99, "philox"))
     out = pipe(x)
     torch.cuda.synchronize()
@@ -824,7 +846,7 @@ def test_ms_large_digest_torch_mode(name):
         assert sha(qp) == meta["q"]
         assert sha(cp.decode(norm, words, mw, x.size).cpu().numpy()) == meta["dec"]
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
 
 
 @pytest.mark.parametrize("levels", [(2, 4), (4, 8)])
@@ -993,7 +1015,7 @@ def test_qsgdbp_compressor_matches_reference_vectors():
             d = comp.decompress(norm_s, sp, xp, x.size)
             assert bits_eq(u32(d), z[f"{c}/dec"].view(np.uint32)), c
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
 
 
 # --------------------------------------------------------------------------- one-pass W = 1 multi-scale
@@ -1087,4 +1109,4 @@ def test_ms_encode_w1_torch_mode_digests(name):
         d = c.decode(norm, words, mw, x.size)
         assert hashlib.sha256(d.cpu().numpy().tobytes()).hexdigest() == meta["dec"]
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)

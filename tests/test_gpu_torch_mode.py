@@ -129,7 +129,7 @@ def test_torch_mode_compressor_back_to_back_vs_oracle():
             exp = O.qsgd_quantize(x, norm, bits, O.stream_rng(ref_draws))
             assert np.array_equal(q.cpu().numpy().astype(np.int32), np.asarray(exp, dtype=np.int32)), i
     finally:
-        gcodec.set_rng_mode("philox")
+        gcodec.set_rng_mode(gcodec.rng.DEFAULT_MODE)
 
 
 @pytest.mark.parametrize("idx,count", [(0, 1), (623, 1), (624, 1), (5, 619), (5, 620), (0, 624), (624, 624),
@@ -253,3 +253,181 @@ def test_packed24_encode_back_to_back_matches_plain_and_falls_back():
     for i, (u, v) in enumerate(zip(a, b)):
         assert np.array_equal(u, v), i
     assert sa[1] == sb[1] and np.array_equal(sa[0], sb[0])
+
+
+def _split_planes(got, count, hb):
+    """(hi, lo) integer arrays of one call's split-plane region"""
+    b = got.cpu().numpy().view(np.uint8)
+    hpad = (count * (hb // 8) + 15) // 16 * 16
+    if hb == 8:
+        hi = b[:count].astype(np.uint32)
+        lo = b[hpad:hpad + 2 * count].view(np.uint16).astype(np.uint32)
+    else:
+        hi = b[:2 * count].view(np.uint16).astype(np.uint32)
+        lo = b[hpad:hpad + count].astype(np.uint32)
+    return hi, lo
+
+
+@pytest.mark.parametrize("fmt,hb", [("split8", 8), ("split16", 16)])
+@pytest.mark.parametrize("count", [624, 100_000, 2 * 262_080 + 8])
+def test_split_draws_are_the_planes_of_the_low_24_bits(fmt, hb, count):
+    """gc_mt19937_generate_multi_split_j through mt19937_reserve: every call's
+    region holds the top hb of each draw's low 24 bits in the HI plane and the
+    rest in the LO plane, for the serial stream's draws, call after call (the
+    speculative multi-call runs: one region per call), and torch's state after
+    each call is the serial generator's."""
+    from gcodec import _lib
+    codec.mt_release()
+    torch.manual_seed(hb * 100 + count % 97)
+    kind = _lib.GC_RNG_SPLIT8 if hb == 8 else _lib.GC_RNG_SPLIT16
+    for i in range(11):
+        ref, w2, i2 = _oracle_next(count)
+        got, k = codec.mt19937_reserve(count, DEV, fmt)
+        torch.cuda.synchronize()
+        assert k == kind and got.numel() == codec.mt_format_bytes(count, fmt), i
+        hi, lo = _split_planes(got, count, hb)
+        r24 = np.asarray(ref, np.uint32) & 0xFFFFFF
+        assert np.array_equal(hi, r24 >> (24 - hb)), i
+        assert np.array_equal(lo, r24 & ((1 << (24 - hb)) - 1)), i
+        words, idx = torch_mt_state()
+        assert idx == i2 and np.array_equal(words, w2), i
+    codec.mt_release()
+
+
+@pytest.mark.parametrize("bits", [1, 2, 4, 8])
+@pytest.mark.parametrize("fmt", ["split8", "split16"])
+def test_split_encode_back_to_back_matches_plain_and_falls_back(fmt, bits):
+    """The torch-mode QSGD encode from split-plane draws (the HI plane decides
+    unless the rounding ties, then the LO plane is read) gives the words of
+    the plain 32-bit draws call after call, across the narrow (b <= 7) and wide
+    (b = 8) integer paths, L = 16 / 10 / 6 / 4 lanes per word, and read indices
+    that are not multiples of 4 (torch.rand(1) in between).  The inputs hit the
+    tie path: the test counts, on the host, elements whose HI bits equal those
+    of ceil(p 2^24) - 1."""
+    from gcodec import _lib
+    n = 1_000_003  # odd: every call's region starts mid-quad of the stream
+    x = torch.from_numpy(O.gen_input(n, seed=bits)).to(DEV)
+    x[:4096] = 0.0  # zeros and exact multiples: F = 0 and tiny-F quads
+    nm = codec.absmax(x)
+    lanes = codec.qsgd_layout(n, bits, 1)
+    gen = gcodec.Generator(0, "torch")
+    kind = _lib.GC_RNG_SPLIT8 if fmt == "split8" else _lib.GC_RNG_SPLIT16
+
+    def run(f, steps):
+        torch.manual_seed(4321 + bits)
+        outs, kinds = [], []
+        for i in range(steps):
+            if i == 3:
+                torch.rand(1)  # read index now 1 mod 4
+            if i == 5:
+                torch.rand(3)  # and back to a multiple of 4
+            r = gen.reserve(n, fmt=f)
+            kinds.append(r.kind)
+            outs.append(codec.qsgd_encode(x, nm, bits, r, 1, lanes=lanes).cpu().numpy())
+        return outs, kinds, torch_mt_state()
+
+    codec.mt_release()
+    a, ka, sa = run(fmt, 9)
+    codec.mt_release()
+    b, kb, sb = run("plain", 9)
+    assert set(ka) == {kind}  # any read index (torch.rand(1) leaves it odd)
+    assert set(kb) == {_lib.GC_RNG_STREAM}
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert np.array_equal(u, v), i
+    assert sa[1] == sb[1] and np.array_equal(sa[0], sb[0])
+    # the words above equal the oracle's too (first call, plain stream = torch's)
+    torch.manual_seed(4321 + bits)
+    ref, _, _ = _oracle_next(n)
+    xs = x.cpu().numpy()
+    exp = O.qsgd_encode(xs, float(nm.item()), bits, 1, O.stream_rng(ref))
+    assert np.array_equal(a[0].view(np.uint32), np.asarray(exp, np.uint32))
+    # and the first call went through the tie path: F = ceil(frac(l) 2^24)
+    hb = 8 if fmt == "split8" else 16
+    lv = (np.abs(xs) / np.float32(nm.item())).astype(np.float32) * np.float32((1 << bits) - 1)
+    F = np.ceil((lv - np.floor(lv)).astype(np.float64) * 2.0 ** 24).astype(np.int64)
+    r24 = np.asarray(ref, np.int64) & 0xFFFFFF
+    ties = int(np.count_nonzero((F >= 1) & (((F - 1) >> (24 - hb)) == (r24 >> (24 - hb)))))
+    assert ties >= 1
+    codec.mt_release()
+
+
+def test_mt_reserved_bytes_counts_the_queue_and_release_frees_it():
+    """mt_reserved_bytes reports the draws queued ahead (plus workspaces and
+    tables) and mt_release drops them."""
+    codec.mt_release()
+    torch.manual_seed(3)
+    for _ in range(4):
+        codec.mt19937_reserve(1_000_000, DEV, "split16")
+    held = codec.mt_reserved_bytes(DEV)
+    assert held >= codec.mt_format_bytes(1_000_000, "split16")
+    codec.mt_release(DEV)
+    assert codec.mt_reserved_bytes(DEV) < held
+    assert DEV.index not in codec._MT_SPEC
+
+
+def _as_draws24(got, kind, count):
+    """The low 24 bits of each draw from a reservation of any format"""
+    from gcodec import _lib
+    if kind == _lib.GC_RNG_STREAM:
+        return got.cpu().numpy().view(np.uint32) & 0xFFFFFF
+    if kind == _lib.GC_RNG_STREAM24:
+        b = got.cpu().numpy().view(np.uint8).reshape(-1, 3).astype(np.uint32)
+        return b[:, 0] | b[:, 1] << 8 | b[:, 2] << 16
+    hb = 8 if kind == _lib.GC_RNG_SPLIT8 else 16
+    hi, lo = _split_planes(got, count, hb)
+    return hi << (24 - hb) | lo
+
+
+def test_randomised_schedule_vs_serial_stream():
+    """200 torch-mode calls on a seeded random schedule,
+    each call's draws (plain: all 32 bits; cut formats: the 24 the rounding
+    reads) and torch's generator state after it compared with the serial
+    MT19937 oracle.  The schedule mixes counts below / at / above 624 and
+    multiples / non-multiples of 4 (repeated often, so the speculation and the
+    multi-call runs are used), all four draw formats, changes of depth,
+    calls per run and budget, interleaved torch.rand and torch.manual_seed,
+    mt_release, and calls made on a side stream."""
+    import random
+    from gcodec import _lib
+    rnd = random.Random(20261018)
+    counts = [1, 3, 4, 100, 623, 624, 625, 1248, 4000, 4001, 20_000, 100_003, 262_084]
+    fmts = ["plain", "packed24", "split8", "split16"]
+    side = torch.cuda.Stream(DEV)
+    saved = (codec.MT_SPECULATE_DEPTH, codec.MT_MULTI_CALLS, codec.MT_SPECULATE_BUDGET)
+    codec.mt_release()
+    torch.manual_seed(1)
+    count, fmt = 624, "plain"
+    try:
+        for i in range(200):
+            op = rnd.random()
+            if op < 0.05:
+                torch.rand(rnd.randint(1, 9))
+            elif op < 0.08:
+                torch.manual_seed(rnd.randint(0, 2 ** 31))
+            elif op < 0.10:
+                codec.mt_release()
+            elif op < 0.13:
+                codec.MT_SPECULATE_DEPTH = rnd.choice([0, 1, 2, 4, 8, 16])
+            elif op < 0.16:
+                codec.MT_MULTI_CALLS = rnd.choice([1, 2, 3, 8])
+            elif op < 0.18:
+                codec.MT_SPECULATE_BUDGET = rnd.choice([None, 4_000, 100_000, 1 << 30])
+            if rnd.random() > 0.65:
+                count = rnd.choice(counts)
+            if rnd.random() > 0.75:
+                fmt = rnd.choice(fmts)
+            on_side = rnd.random() < 0.15
+            ref, w2, i2 = _oracle_next(count)
+            with torch.cuda.stream(side if on_side else torch.cuda.current_stream(DEV)):
+                got, kind = codec.mt19937_reserve(count, DEV, fmt)
+            torch.cuda.synchronize()
+            tag = (i, count, fmt, kind, on_side)
+            if kind == _lib.GC_RNG_STREAM:
+                assert np.array_equal(got.cpu().numpy().view(np.uint32), ref), tag
+            else:
+                assert np.array_equal(_as_draws24(got, kind, count), np.asarray(ref, np.uint32) & 0xFFFFFF), tag
+            words, idx = torch_mt_state()
+            assert idx == i2 and np.array_equal(words, w2), tag
+    finally:
+        codec.MT_SPECULATE_DEPTH, codec.MT_MULTI_CALLS, codec.MT_SPECULATE_BUDGET = saved
+        codec.mt_release()

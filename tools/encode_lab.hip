@@ -18,9 +18,10 @@
 
 #include "gcodec.h"
 #include "absmax.h"
-#include "qsgd_encode.h"
+#include "encode_lab_kernel.h"
 
 using namespace gc;
+using namespace gclab;
 
 #define CK(x)                                                                               \
     do {                                                                                    \
@@ -347,7 +348,7 @@ int main(int argc, char **argv)
         CK(hipDeviceSynchronize());
         auto encp = [&](const float *xb, uint32_t *wb, uint64_t Mp) {
             return [=] {
-                hipLaunchKernelGGL((k_qsgd_encode<6, 0, 0, 0>), dim3(2048), dim3(256), 0, 0, xb,
+                hipLaunchKernelGGL((gclab::k_qsgd_encode<6, 0, 0, 0>), dim3(2048), dim3(256), 0, 0, xb,
                                    (const int64_t *)nullptr, n, norm, s, qmax, ln.bits, Mp, ra, wb);
             };
         };
@@ -384,25 +385,25 @@ int main(int argc, char **argv)
     for (unsigned g : {2048u, 8192u, 16384u, 32768u}) {
         char nm[96];
         snprintf(nm, sizeof nm, "encode ABL=0 (exact) g=%u", g);
-        row(nm, T.run(enc(k_qsgd_encode<6, 0, 0, 0>, g)), enc_bytes);
+        row(nm, T.run(enc(gclab::k_qsgd_encode<6, 0, 0, 0>, g)), enc_bytes);
     }
-    row("encode philox impl 0 (64b mad, xor2)", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PHX0>, 2048)), enc_bytes);
-    row("encode philox impl 2 (mul_hi/lo, xor3)", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PHX2>, 2048)), enc_bytes);
-    row("encode max+min clamp", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 2048)), enc_bytes);
-    row("encode max+min clamp g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_MED3>, 16384)), enc_bytes);
-    row("encode NORNG|NODIV g=16384", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 16384)), enc_bytes);
+    row("encode philox impl 0 (64b mad, xor2)", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_PHX0>, 2048)), enc_bytes);
+    row("encode philox impl 2 (mul_hi/lo, xor3)", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_PHX2>, 2048)), enc_bytes);
+    row("encode max+min clamp", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_MED3>, 2048)), enc_bytes);
+    row("encode max+min clamp g=16384", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_MED3>, 16384)), enc_bytes);
+    row("encode NORNG|NODIV g=16384", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 16384)), enc_bytes);
     for (int rep = 0; rep < 3; ++rep) {
-        row("A/B: encode product (MINW=1) g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, 0>, 2048)), enc_bytes);
-        row("A/B: encode PF g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PF>, 2048)), enc_bytes);
-        row("A/B: encode PF g=1536", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PF>, 1536)), enc_bytes);
-        row("A/B: encode PF g=3072", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PF>, 3072)), enc_bytes);
-        row("A/B: encode PF MINW=4 g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_PF, 4>, 2048)), enc_bytes);
-        row("A/B: encode planes in pairs", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_GRP2>, 2048)), enc_bytes);
-        row("A/B: encode planes in triples", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_GRP3>, 2048)), enc_bytes);
-        row("A/B: encode SEQ planes", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_SEQ>, 2048)), enc_bytes);
-        row("A/B: encode SEQ planes >=6 waves", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_SEQ, 6>, 2048)), enc_bytes);
-        row("A/B: encode SEQ planes >=8 waves", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>, 2048)), enc_bytes);
-        row("A/B: encode SEQ planes >=8 waves g=4096", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>, 4096)), enc_bytes);
+        row("A/B: encode product (MINW=1) g=2048", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, 0>, 2048)), enc_bytes);
+        row("A/B: encode PF g=2048", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_PF>, 2048)), enc_bytes);
+        row("A/B: encode PF g=1536", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_PF>, 1536)), enc_bytes);
+        row("A/B: encode PF g=3072", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_PF>, 3072)), enc_bytes);
+        row("A/B: encode PF MINW=4 g=2048", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_PF, 4>, 2048)), enc_bytes);
+        row("A/B: encode planes in pairs", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_GRP2>, 2048)), enc_bytes);
+        row("A/B: encode planes in triples", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_GRP3>, 2048)), enc_bytes);
+        row("A/B: encode SEQ planes", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_SEQ>, 2048)), enc_bytes);
+        row("A/B: encode SEQ planes >=6 waves", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_SEQ, 6>, 2048)), enc_bytes);
+        row("A/B: encode SEQ planes >=8 waves", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>, 2048)), enc_bytes);
+        row("A/B: encode SEQ planes >=8 waves g=4096", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>, 4096)), enc_bytes);
     }
     {
         // Infinity-Cache reuse inside one step: flush 600 MB, then time absmax -> encode
@@ -435,23 +436,23 @@ int main(int argc, char **argv)
             hipLaunchKernelGGL(k_absmax_rev, dim3(256), dim3(1024), 0, 0, (const float4 *)x, n / 4, (uint32_t *)norm);
         };
         for (int rep = 0; rep < 2; ++rep) {
-            pair("COLD step: absmax fwd + encode fwd", am_fwd, enc(k_qsgd_encode<6, 0, 0, 0>, 2048));
-            pair("COLD step: absmax fwd + encode REV", am_fwd, enc(k_qsgd_encode<6, 0, 0, ENC_REV>, 2048));
-            pair("COLD step: absmax REV + encode fwd", am_rev, enc(k_qsgd_encode<6, 0, 0, 0>, 2048));
-            pair("COLD step: absmax REV + encode REV", am_rev, enc(k_qsgd_encode<6, 0, 0, ENC_REV>, 2048));
+            pair("COLD step: absmax fwd + encode fwd", am_fwd, enc(gclab::k_qsgd_encode<6, 0, 0, 0>, 2048));
+            pair("COLD step: absmax fwd + encode REV", am_fwd, enc(gclab::k_qsgd_encode<6, 0, 0, ENC_REV>, 2048));
+            pair("COLD step: absmax REV + encode fwd", am_rev, enc(gclab::k_qsgd_encode<6, 0, 0, 0>, 2048));
+            pair("COLD step: absmax REV + encode REV", am_rev, enc(gclab::k_qsgd_encode<6, 0, 0, ENC_REV>, 2048));
         }
-        pair("COLD encode only (after flush)", [] {}, enc(k_qsgd_encode<6, 0, 0, 0>, 2048));
+        pair("COLD encode only (after flush)", [] {}, enc(gclab::k_qsgd_encode<6, 0, 0, 0>, 2048));
         pair("COLD absmax only (after flush)", am_fwd, [] {});
         CK(hipFree(fl));
     }
-    row("encode COMPUTE ONLY (16KB window) g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 2048)), enc_bytes);
-    row("encode COMPUTE ONLY g=8192", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 8192)), enc_bytes);
-    row("encode COMPUTE ONLY, no Philox", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2 | ENC_ABL_NORNG>, 2048)), enc_bytes);
-    row("encode COMPUTE ONLY, no div", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_L2 | ENC_ABL_NODIV>, 2048)), enc_bytes);
-    row("encode ABL=NORNG g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG>, 2048)), enc_bytes);
-    row("encode ABL=NODIV g=2048", T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NODIV>, 2048)), enc_bytes);
+    row("encode COMPUTE ONLY (16KB window) g=2048", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 2048)), enc_bytes);
+    row("encode COMPUTE ONLY g=8192", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_ABL_L2>, 8192)), enc_bytes);
+    row("encode COMPUTE ONLY, no Philox", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_ABL_L2 | ENC_ABL_NORNG>, 2048)), enc_bytes);
+    row("encode COMPUTE ONLY, no div", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_ABL_L2 | ENC_ABL_NODIV>, 2048)), enc_bytes);
+    row("encode ABL=NORNG g=2048", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG>, 2048)), enc_bytes);
+    row("encode ABL=NODIV g=2048", T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_ABL_NODIV>, 2048)), enc_bytes);
     row("encode ABL=NORNG|NODIV g=2048",
-        T.run(enc(k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 2048)), enc_bytes);
+        T.run(enc(gclab::k_qsgd_encode<6, 0, 0, ENC_ABL_NORNG | ENC_ABL_NODIV>, 2048)), enc_bytes);
 
     // the same product rows again, late in the process (clock / power ramp check)
     row("late: product gc_qsgd_encode", T.run([&] { gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr); }),
@@ -512,22 +513,22 @@ int main(int argc, char **argv)
             std::vector<float> t;
         };
         std::vector<V> vs;
-        vs.push_back({"AB: encode product", enc(k_qsgd_encode<6, 0, 0, 0>, 2048), enc_bytes, {}});
-        vs.push_back({"AB: encode DIV2 (two corrections)", enc(k_qsgd_encode<6, 0, 0, ENC_DIV2>, 2048), enc_bytes, {}});
-        vs.push_back({"AB: encode NT loads", enc(k_qsgd_encode<6, 0, 0, ENC_NT>, 2048), enc_bytes, {}});
-        vs.push_back({"AB: encode NT + DIV2", enc(k_qsgd_encode<6, 0, 0, ENC_DIV2 | ENC_NT>, 2048), enc_bytes, {}});
+        vs.push_back({"AB: encode product", enc(gclab::k_qsgd_encode<6, 0, 0, 0>, 2048), enc_bytes, {}});
+        vs.push_back({"AB: encode DIV2 (two corrections)", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_DIV2>, 2048), enc_bytes, {}});
+        vs.push_back({"AB: encode NT loads", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_NT>, 2048), enc_bytes, {}});
+        vs.push_back({"AB: encode NT + DIV2", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_DIV2 | ENC_NT>, 2048), enc_bytes, {}});
         vs.push_back({"AB: absmax product", [&] { gc_absmax_f32(x, nullptr, n, norm, ws, nullptr); }, rd_bytes, {}});
         vs.push_back({"AB: step product (absmax+encode)", [&] {
                           gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
-                          enc(k_qsgd_encode<6, 0, 0, 0>, 2048)();
+                          enc(gclab::k_qsgd_encode<6, 0, 0, 0>, 2048)();
                       }, 8.0 * n + 4.0 * M, {}});
         vs.push_back({"AB: step absmax + encode DIV2", [&] {
                           gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
-                          enc(k_qsgd_encode<6, 0, 0, ENC_DIV2>, 2048)();
+                          enc(gclab::k_qsgd_encode<6, 0, 0, ENC_DIV2>, 2048)();
                       }, 8.0 * n + 4.0 * M, {}});
         vs.push_back({"AB: step absmax + encode NT", [&] {
                           gc_absmax_f32(x, nullptr, n, norm, ws, nullptr);
-                          enc(k_qsgd_encode<6, 0, 0, ENC_NT>, 2048)();
+                          enc(gclab::k_qsgd_encode<6, 0, 0, ENC_NT>, 2048)();
                       }, 8.0 * n + 4.0 * M, {}});
         settle();
         for (int rep = 0; rep < 7; ++rep)
@@ -539,7 +540,7 @@ int main(int argc, char **argv)
         }
     }
     // the lab's ABL=0 instantiation must equal the product's words
-    hipLaunchKernelGGL((k_qsgd_encode<6, 0, 0, 0>), dim3(2048), dim3(256), 0, 0, x, (const int64_t *)nullptr, n, norm,
+    hipLaunchKernelGGL((gclab::k_qsgd_encode<6, 0, 0, 0>), dim3(2048), dim3(256), 0, 0, x, (const int64_t *)nullptr, n, norm,
                        s, qmax, ln.bits, (uint64_t)M, ra, words2);
     gc_qsgd_encode(x, nullptr, n, norm, bits, &ln, &rng, words, nullptr);
     CK(hipDeviceSynchronize());
@@ -555,17 +556,17 @@ int main(int argc, char **argv)
         CK(hipMemcpy(b.data(), words2, (size_t)M * 4, hipMemcpyDeviceToHost));
         printf("%-28s == product: %s\n", nm, memcmp(a.data(), b.data(), (size_t)M * 4) == 0 ? "yes" : "NO");
     };
-    same("philox impl 0", k_qsgd_encode<6, 0, 0, ENC_PHX0>);
-    same("philox impl 2", k_qsgd_encode<6, 0, 0, ENC_PHX2>);
-    same("max+min clamp", k_qsgd_encode<6, 0, 0, ENC_MED3>);
-    same(">=8 waves/SIMD", k_qsgd_encode<6, 0, 0, 0, 8>);
-    same("reverse tile order", k_qsgd_encode<6, 0, 0, ENC_REV>);
-    same("planes in pairs", k_qsgd_encode<6, 0, 0, ENC_GRP2>);
-    same("SEQ planes", k_qsgd_encode<6, 0, 0, ENC_SEQ>);
-    same("SEQ planes >=8 waves", k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>);
-    same("register prefetch", k_qsgd_encode<6, 0, 0, ENC_PF>);
-    same("register prefetch MINW=4", k_qsgd_encode<6, 0, 0, ENC_PF, 4>);
-    same("two-correction division", k_qsgd_encode<6, 0, 0, ENC_DIV2>);
-    same("nontemporal loads", k_qsgd_encode<6, 0, 0, ENC_NT>);
+    same("philox impl 0", gclab::k_qsgd_encode<6, 0, 0, ENC_PHX0>);
+    same("philox impl 2", gclab::k_qsgd_encode<6, 0, 0, ENC_PHX2>);
+    same("max+min clamp", gclab::k_qsgd_encode<6, 0, 0, ENC_MED3>);
+    same(">=8 waves/SIMD", gclab::k_qsgd_encode<6, 0, 0, 0, 8>);
+    same("reverse tile order", gclab::k_qsgd_encode<6, 0, 0, ENC_REV>);
+    same("planes in pairs", gclab::k_qsgd_encode<6, 0, 0, ENC_GRP2>);
+    same("SEQ planes", gclab::k_qsgd_encode<6, 0, 0, ENC_SEQ>);
+    same("SEQ planes >=8 waves", gclab::k_qsgd_encode<6, 0, 0, ENC_SEQ, 8>);
+    same("register prefetch", gclab::k_qsgd_encode<6, 0, 0, ENC_PF>);
+    same("register prefetch MINW=4", gclab::k_qsgd_encode<6, 0, 0, ENC_PF, 4>);
+    same("two-correction division", gclab::k_qsgd_encode<6, 0, 0, ENC_DIV2>);
+    same("nontemporal loads", gclab::k_qsgd_encode<6, 0, 0, ENC_NT>);
     return 0;
 }

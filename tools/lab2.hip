@@ -16,9 +16,10 @@
 
 #include "gcodec.h"
 #include "absmax.h"
-#include "qsgd_encode.h"
+#include "encode_lab_kernel.h"
 
 using namespace gc;
+using namespace gclab;
 
 #define CK(x)                                                                               \
     do {                                                                                    \
@@ -269,10 +270,10 @@ int main(int argc, char **argv)
             bad += a[i] != b[i];
         printf("%-40s == product: %s (%llu words differ)\n", nm, bad == 0 ? "yes" : "NO", (unsigned long long)bad);
     };
-    same("ENC_INT", enc(k_qsgd_encode<6, 0, 0, ENC_INT>, 2048, words2));
-    same("ENC_INT | ENC_REV", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_REV>, 2048, words2));
-    same("ENC_INT | ENC_NT", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 8192, words2));
-    same("ENC_INT | ENC_NT | ENC_NTS", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 8192, words2));
+    same("ENC_INT", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT>, 2048, words2));
+    same("ENC_INT | ENC_REV", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_REV>, 2048, words2));
+    same("ENC_INT | ENC_NT", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 8192, words2));
+    same("ENC_INT | ENC_NT | ENC_NTS", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 8192, words2));
     {
         // lab decode == product decode
         float *d2;
@@ -334,16 +335,16 @@ int main(int argc, char **argv)
         vs.push_back({"roof: planar R+W NT loads g=12288", cp(k_copy_planar<6, true, false>, 12288), enc_bytes, {}});
         vs.push_back({"roof: planar R+W NT ld+st g=12288", cp(k_copy_planar<6, true, true>, 12288), enc_bytes, {}});
         vs.push_back({"roof: planar R+W NT ld+st g=16384", cp(k_copy_planar<6, true, true>, 16384), enc_bytes, {}});
-        vs.push_back({"AB: encode INT NT g=12288 (product)", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 12288, words2), enc_bytes, {}});
-        vs.push_back({"AB: encode INT NT NTS g=12288", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 12288, words2), enc_bytes, {}});
-        vs.push_back({"AB: encode INT NT g=16384", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 16384, words2), enc_bytes, {}});
-        vs.push_back({"AB: encode INT NT NTS g=16384", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 16384, words2), enc_bytes, {}});
-        vs.push_back({"AB: encode INT NT g=24576", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 24576, words2), enc_bytes, {}});
-        vs.push_back({"AB: encode INT NT MINW=5 g=12288", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT, 5>, 12288, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT g=12288 (product)", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 12288, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT NTS g=12288", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 12288, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT g=16384", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 16384, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT NTS g=16384", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 16384, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT g=24576", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT>, 24576, words2), enc_bytes, {}});
+        vs.push_back({"AB: encode INT NT MINW=5 g=12288", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT, 5>, 12288, words2), enc_bytes, {}});
         vs.push_back({"AB: step product", step(product_am, product_enc), step_bytes, {}});
-        vs.push_back({"AB: step + NTS", step(product_am, enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 12288, words2)), step_bytes, {}});
-        vs.push_back({"AB: step + NTS g=16384", step(product_am, enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 16384, words2)), step_bytes, {}});
-        vs.push_back({"AB: compute only INT g=12288", enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_ABL_L2>, 12288, words2), enc_bytes, {}});
+        vs.push_back({"AB: step + NTS", step(product_am, enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 12288, words2)), step_bytes, {}});
+        vs.push_back({"AB: step + NTS g=16384", step(product_am, enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_NT | ENC_NTS>, 16384, words2)), step_bytes, {}});
+        vs.push_back({"AB: compute only INT g=12288", enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_ABL_L2>, 12288, words2), enc_bytes, {}});
         const double dec_bytes = 4.0 * n + 4.0 * M;
         auto dec = [&](auto kern, unsigned g) {
             return [=] {
@@ -446,13 +447,13 @@ int main(int argc, char **argv)
         cold("MALL: planar read fwd then planar rev", pl(false), pl(true), rd_bytes, rd_bytes);
         cold("MALL: planar read fwd then planar fwd", pl(false), pl(false), rd_bytes, rd_bytes);
         cold("step: absmax -> encode product", product_am, product_enc, enc_bytes, rd_bytes);
-        cold("step: absmax -> encode INT", product_am, enc(k_qsgd_encode<6, 0, 0, ENC_INT>, 2048, words2), enc_bytes,
+        cold("step: absmax -> encode INT", product_am, enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT>, 2048, words2), enc_bytes,
              rd_bytes);
-        cold("step: absmax -> encode INT REV", product_am, enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_REV>, 2048, words2),
+        cold("step: absmax -> encode INT REV", product_am, enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_REV>, 2048, words2),
              enc_bytes, rd_bytes);
         cold("step: planar read fwd -> encode INT REV", pl(false),
-             enc(k_qsgd_encode<6, 0, 0, ENC_INT | ENC_REV>, 2048, words2), enc_bytes, rd_bytes);
-        cold("step: planar read fwd -> encode INT", pl(false), enc(k_qsgd_encode<6, 0, 0, ENC_INT>, 2048, words2),
+             enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT | ENC_REV>, 2048, words2), enc_bytes, rd_bytes);
+        cold("step: planar read fwd -> encode INT", pl(false), enc(gclab::k_qsgd_encode<6, 0, 0, ENC_INT>, 2048, words2),
              enc_bytes, rd_bytes);
     }
     return 0;

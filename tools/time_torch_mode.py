@@ -63,11 +63,14 @@ def _per_call(fn):
     return min(best)
 
 
-PACKED = os.environ.get("PACKED24", "0") == "1"  # 24-bit packed draws (the product: 32-bit)
+FMT = os.environ.get("FMT", "plain")  # draw format: plain / packed24 / split8 / split16
+if os.environ.get("BUDGET"):  # speculation budget in bytes (codec.MT_SPECULATE_BUDGET)
+    codec.MT_SPECULATE_BUDGET = int(float(os.environ["BUDGET"]))
+PACKED = FMT == "packed24"
 
 
 def enc():
-    codec.qsgd_encode(x, nm, 4, gen.reserve(n, packed24=PACKED), 1, out=words, lanes=lanes)
+    codec.qsgd_encode(x, nm, 4, gen.reserve(n, fmt=FMT), 1, out=words, lanes=lanes)
 
 
 def step():
@@ -75,11 +78,24 @@ def step():
     enc()
 
 
+if os.environ.get("AB_FMTS"):  # interleaved A/B of draw formats, e.g. AB_FMTS=plain,split8,split16
+    for rep in range(int(os.environ.get("AB_REPS", "3"))):
+        for f in os.environ["AB_FMTS"].split(","):
+            FMT = f
+            codec.mt_release()
+            e, s_ = per_call(enc), per_call(step)
+            held = codec.mt_reserved_bytes(dev) if hasattr(codec, "mt_reserved_bytes") else -1
+            plan = codec._mt_plan(n, f, True) if hasattr(codec, "_mt_plan") else None
+            print(f"AB rep {rep} fmt={f}{' cadence' if CADENCE else ''} budget {codec.MT_SPECULATE_BUDGET} "
+                  f"(calls/run, depth) {plan}: encode {e:.3f} ms, absmax + encode "
+                  f"{s_:.3f} ms per call, held {held / 1e9:.2f} GB", flush=True)
+    sys.exit(0)
+
 if os.environ.get("AB") == "1":  # interleaved A/B of the packed and plain draws, the product's G and depth
     codec.mt_release()
     for rep in range(4):
         for packed in (True, False):
-            PACKED = packed
+            FMT = "packed24" if packed else "plain"
             codec.mt_release()
             print(f"AB rep {rep} packed24={packed}: encode {per_call(enc):.3f} ms, absmax + encode "
                   f"{per_call(step):.3f} ms per call", flush=True)
