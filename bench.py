@@ -723,17 +723,20 @@ def torch_mode_leg(torch, np, gcodec, codec, x, n, bits, words, lanes, dev, pgen
     encode only (norm fixed), absmax + encode per call (what a reducer does),
     and a training cadence (each call behind a few ms of unrelated GPU work,
     the backward, so the speculation has time to run ahead)."""
+    from gcodec import compressors as gcomp
+
     pgen = gcodec.Generator(0, "torch")
     torch.manual_seed(42)
     nm = codec.absmax(x)
     pgen.reserve(n)  # warm: builds the jump table once per process
     codec.qsgd_encode_torch(x, nm, bits, 1, out=words, lanes=lanes)
+    fmt = gcomp.TORCH_DRAW_FORMAT  # the draw format the compressors' packed encode asks for
 
-    def enc_torch():  # the product's form: 32-bit draws
-        codec.qsgd_encode(x, nm, bits, pgen.reserve(n), 1, out=words, lanes=lanes)
+    def enc_fmt(f):
+        codec.qsgd_encode(x, nm, bits, pgen.reserve(n, fmt=f), 1, out=words, lanes=lanes)
 
-    def enc_torch24():  # the draws packed to 24 bits (GC_RNG_STREAM24; slower on MI355X, kept measured)
-        codec.qsgd_encode(x, nm, bits, pgen.reserve(n, packed24=True), 1, out=words, lanes=lanes)
+    def enc_torch():  # the product's form (QSGDMaxNormCompressor.encode in torch mode)
+        enc_fmt(fmt)
 
     def step_torch():
         codec.absmax(x, out=nm)
@@ -760,7 +763,14 @@ def torch_mode_leg(torch, np, gcodec, codec, x, n, bits, words, lanes, dev, pgen
         return min(best), best
 
     enc_ms, enc_runs = per_call_ms(enc_torch)
-    enc24_ms, _ = per_call_ms(enc_torch24)
+    held = codec.mt_reserved_bytes(dev)  # what the speculation holds while calls repeat
+    plan = codec._mt_plan(n, fmt, True)
+    other_fmts = {}
+    for f in ("plain", "split16", "packed24"):
+        if f != fmt:
+            codec.mt_release(dev)
+            other_fmts[f] = per_call_ms(lambda: enc_fmt(f))[0]
+    codec.mt_release(dev)
     stp_ms, stp_runs = per_call_ms(step_torch)
     enc_px, _ = per_call_ms(enc_philox)
     stp_px, _ = per_call_ms(step_philox)
@@ -792,8 +802,13 @@ def torch_mode_leg(torch, np, gcodec, codec, x, n, bits, words, lanes, dev, pgen
     return {
         "n": n,
         "encode_only": {"ms_per_call": enc_ms, "grad_floats_per_s": n / (enc_ms * 1e-3), "runs_ms": enc_runs,
-                        "draws": "32-bit", "packed24_draws_ms_per_call": enc24_ms,
+                        "draws": fmt, "other_draw_formats_ms_per_call": other_fmts,
                         "philox_ms_per_call": enc_px, "frac_of_philox_rate": enc_px / enc_ms},
+        "speculation": {"held_device_bytes": held, "budget_bytes": codec.MT_SPECULATE_BUDGET,
+                        "calls_per_run": plan[0], "calls_ahead": plan[1],
+                        "bytes_per_call": codec.mt_format_bytes(n, fmt),
+                        "note": "device memory the torch-mode speculation holds between calls "
+                                "(codec.mt_reserved_bytes: queued draws, workspaces, tables)"},
         "absmax_plus_encode": {"ms_per_call": stp_ms, "grad_floats_per_s": n / (stp_ms * 1e-3), "runs_ms": stp_runs,
                                "philox_ms_per_call": stp_px, "frac_of_philox_rate": stp_px / stp_ms},
         "training_cadence": {"backward_standin_ms": bw_ms, "torch_added_ms_per_call": cad_torch - bw_ms,

@@ -33,10 +33,6 @@
 #include "gc_host.h"
 #include "qsgd_encode.h"
 
-#ifndef GC_SPLIT_LAB
-#define GC_SPLIT_LAB 0
-#endif
-
 namespace gc {
 
 constexpr uint32_t kMtN = 624;
@@ -426,18 +422,14 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
             uint8_t *r = nx ? rn : rc;
             const uint64_t loc = e - (nx ? bnd : bnd - so.per_end);
             if constexpr (HB == 8) {
-                if (GC_SPLIT_LAB != 2)
                 *reinterpret_cast<uint32_t *>(r + loc) =
                     ((a >> 16) & 0xFFu) | ((b >> 8) & 0xFF00u) | (c & 0xFF0000u) | ((d << 8) & 0xFF000000u);
-                if (GC_SPLIT_LAB != 1)
                 *reinterpret_cast<uint2 *>(r + hpad + 2 * loc) =
                     make_uint2((a & 0xFFFFu) | (b << 16), (c & 0xFFFFu) | (d << 16));
             } else {
-                if (GC_SPLIT_LAB != 2)
                 *reinterpret_cast<uint2 *>(r + 2 * loc) =
                     make_uint2(((a >> 8) & 0xFFFFu) | ((b << 8) & 0xFFFF0000u),
                                ((c >> 8) & 0xFFFFu) | ((d << 8) & 0xFFFF0000u));
-                if (GC_SPLIT_LAB != 1)
                 *reinterpret_cast<uint32_t *>(r + hpad + loc) =
                     (a & 0xFFu) | ((b & 0xFFu) << 8) | ((c & 0xFFu) << 16) | (d << 24);
             }

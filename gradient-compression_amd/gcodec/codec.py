@@ -970,8 +970,11 @@ MT_SPECULATE_DEPTH = 16  # calls' draws kept enqueued ahead of the current one (
 MT_SPECULATE_MAX_DRAWS = 1 << 30  # per run (a run of MT_MULTI_CALLS calls holds that many times count)
 # device bytes the draws of the runs in flight (the current run's and those queued ahead) may hold
 # (bounded, visible through mt_reserved_bytes): the calls per run and the depth shrink to
-# fit it (_mt_plan); None = min(1 GiB, two runs of MT_MULTI_CALLS calls)
+# fit it (_mt_plan); None = min(MT_SPECULATE_DEFAULT_BYTES, two runs of MT_MULTI_CALLS calls).
+# Measured at 1e8 per call: 1 GiB leaves one call ahead and doubles the call
+# time; 4 GiB costs ~5 % against an unbounded queue
 MT_SPECULATE_BUDGET = None
+MT_SPECULATE_DEFAULT_BYTES = 4 << 30
 MT_MAX_SLOTS = 8  # workspace / pinned-state slots of the runs in flight
 # calls per run once a count repeats: one set of generators (and of generator
 # jumps, the LDS-bound part) makes the draws of this many consecutive calls,
@@ -1158,8 +1161,8 @@ def _mt_plan(count: int, fmt: str, multi: bool):
     """(calls per run, calls kept ahead) for repeated calls of `count` draws in
     format fmt under the speculation budget: the draws of the current run and
     of the runs ahead, mt_format_bytes(count, fmt) per call, fit in
-    MT_SPECULATE_BUDGET bytes (default: the smaller of 1 GiB and two runs of
-    MT_MULTI_CALLS calls).  A run takes at most half of what fits, the rest is
+    MT_SPECULATE_BUDGET bytes (default: the smaller of
+    MT_SPECULATE_DEFAULT_BYTES and two runs of MT_MULTI_CALLS calls).  A run takes at most half of what fits, the rest is
     depth (at most MT_SPECULATE_DEPTH).  When not even one call fits ahead the
     speculation is off for this count (warned once: the calls then wait for
     their draws)."""
@@ -1167,7 +1170,7 @@ def _mt_plan(count: int, fmt: str, multi: bool):
     bpc = max(1, mt_format_bytes(count, fmt))
     budget = MT_SPECULATE_BUDGET
     if budget is None:
-        budget = min(1 << 30, 2 * calls_max * bpc)
+        budget = min(int(MT_SPECULATE_DEFAULT_BYTES), 2 * calls_max * bpc)
     hold = int(budget) // bpc
     calls = max(1, min(calls_max, hold // 2))
     depth = max(0, min(int(MT_SPECULATE_DEPTH), hold - calls))

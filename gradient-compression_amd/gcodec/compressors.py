@@ -41,7 +41,11 @@ def _qdtype(bits: int) -> torch.dtype:
 # "packed24" (3 bytes per draw), or the split planes "split8" / "split16"
 # (the encode reads 1 / 2 bytes per draw and the rest only where the rounding
 # is undecided).  Formats the run cannot take fall back to plain draws.
-TORCH_DRAW_FORMAT = "split16"
+# Plain: the split16 encode is faster alone (122 against 145 us per 1e8), but
+# its generator takes 1.2-1.4 against 0.81 ms per 64-walker run and the
+# pipelined call came out equal back to back and slower in a training cadence
+# (profiles/r06*_torch_*.log)
+TORCH_DRAW_FORMAT = "plain"
 
 
 class _Base:
