@@ -395,10 +395,13 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
         const uint64_t hpad = split_hpad(so.per_end, HB);
         uint64_t kc = pos0 / so.per_end;         // call of the current block's first draw
         uint64_t bnd = (kc + 1) * so.per_end;    // first draw of the next call
-        auto region = [&](uint64_t k) {
-            const uint64_t slot = so.ring ? (so.ring0 + k) % so.ring : k;
-            return so.base + slot * so.bytes;
-        };
+        // the regions of calls kc and kc + 1, moved on at a call boundary (the
+        // ring slot is stepped, not divided, per block: uniform but on the
+        // tempering waves' per-block path)
+        uint64_t slot = so.ring ? (so.ring0 + kc) % so.ring : kc;
+        auto next_slot = [&](uint64_t sl) { return so.ring ? (sl + 1 == so.ring ? 0 : sl + 1) : sl + 1; };
+        uint8_t *rcur = so.base + slot * so.bytes, *rnxt = so.base + next_slot(slot) * so.bytes;
+        auto region = [&](uint64_t k) { return k == kc ? rcur : rnxt; };  // k is kc or kc + 1
         auto emit1 = [&](uint64_t e, uint32_t raw, uint8_t *rc, uint8_t *rn) {
             const uint32_t y = mtj_temper(raw);
             const bool nx = e >= bnd;
@@ -415,35 +418,62 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
         // whole quads (read index and per_end multiples of 4: every quad's four
         // draws sit in one call, 8- / 4-byte aligned): thread ct tempers draws
         // 4q .. 4q+3 and stores one HI word pair / word and one LO word / pair
-        auto emit4 = [&](uint64_t e, const uint32_t *src, uint8_t *rc, uint8_t *rn) {
+        // The plane pointers of a block are uniform: quads j = 4q < cut go to
+        // call kc's region, the rest (a block that crosses a call boundary) to
+        // call kc + 1's; each quad adds its own offset and picks one of the two
+        // bases, and the byte shuffles are v_perm_b32 (VALU per quad about that
+        // of the packed24 mode)
+        constexpr uint32_t HS = HB / 8, LS = (24u - HB) / 8;  // bytes per draw in each plane
+        struct Bases {
+            uint8_t *hc, *lc, *hn, *ln;
+            uint32_t cut;
+        };
+        auto bases = [&](uint64_t at0) {
+            Bases B;
+            uint8_t *r0 = region(kc);
+            const uint64_t off0 = at0 - (bnd - so.per_end);  // element offset of at0 in call kc
+            B.hc = r0 + HS * off0;
+            B.lc = r0 + hpad + LS * off0;
+            const uint64_t toend = bnd - at0;                // this block's draws still in call kc
+            if (toend < kMtN) {
+                uint8_t *r1 = region(kc + 1);
+                B.cut = (uint32_t)toend;
+                B.hn = r1 - HS * toend;                      // + HS * j for j >= cut: call kc + 1
+                B.ln = r1 + hpad - LS * toend;
+            } else {
+                B.cut = kMtN;
+                B.hn = B.hc;
+                B.ln = B.lc;
+            }
+            return B;
+        };
+        auto emit4 = [&](uint32_t j, const uint32_t *src, const Bases &B) {
             const uint4 w = *reinterpret_cast<const uint4 *>(src);  // 16-byte aligned: ptr0 % 4 == 0
             const uint32_t a = mtj_temper(w.x), b = mtj_temper(w.y), c = mtj_temper(w.z), d = mtj_temper(w.w);
-            const bool nx = e >= bnd;
-            uint8_t *r = nx ? rn : rc;
-            const uint64_t loc = e - (nx ? bnd : bnd - so.per_end);
-            if constexpr (HB == 8) {
-                *reinterpret_cast<uint32_t *>(r + loc) =
-                    ((a >> 16) & 0xFFu) | ((b >> 8) & 0xFF00u) | (c & 0xFF0000u) | ((d << 8) & 0xFF000000u);
-                *reinterpret_cast<uint2 *>(r + hpad + 2 * loc) =
-                    make_uint2((a & 0xFFFFu) | (b << 16), (c & 0xFFFFu) | (d << 16));
-            } else {
-                *reinterpret_cast<uint2 *>(r + 2 * loc) =
-                    make_uint2(((a >> 8) & 0xFFFFu) | ((b << 8) & 0xFFFF0000u),
-                               ((c >> 8) & 0xFFFFu) | ((d << 8) & 0xFFFF0000u));
-                *reinterpret_cast<uint32_t *>(r + hpad + loc) =
-                    (a & 0xFFu) | ((b & 0xFFu) << 8) | ((c & 0xFFu) << 16) | (d << 24);
+            const bool nx = j >= B.cut;
+            uint8_t *h = (nx ? B.hn : B.hc) + HS * j;
+            uint8_t *l = (nx ? B.ln : B.lc) + LS * j;
+            if constexpr (HB == 8) {  // HI: bytes 2 of a, b, c, d; LO: bytes 0-1 of each
+                const uint32_t x = __builtin_amdgcn_perm(b, a, 0x0C0C0602u), y = __builtin_amdgcn_perm(d, c, 0x0C0C0602u);
+                *reinterpret_cast<uint32_t *>(h) = __builtin_amdgcn_perm(y, x, 0x05040100u);
+                *reinterpret_cast<uint2 *>(l) =
+                    make_uint2(__builtin_amdgcn_perm(b, a, 0x05040100u), __builtin_amdgcn_perm(d, c, 0x05040100u));
+            } else {  // HI: bytes 1-2 of each; LO: byte 0 of each
+                *reinterpret_cast<uint2 *>(h) =
+                    make_uint2(__builtin_amdgcn_perm(b, a, 0x06050201u), __builtin_amdgcn_perm(d, c, 0x06050201u));
+                const uint32_t x = __builtin_amdgcn_perm(b, a, 0x0C0C0400u), y = __builtin_amdgcn_perm(d, c, 0x0C0C0400u);
+                *reinterpret_cast<uint32_t *>(l) = __builtin_amdgcn_perm(y, x, 0x05040100u);
             }
         };
         const bool quads = (ptr0 & 3u) == 0 && (so.per_end & 3u) == 0;  // uniform
-        {
+        if (quads) {
+            const Bases B = bases(pos0);
+            for (uint32_t q = ct; 4 * q < head; q += kMtTemperThreads)
+                emit4(4 * q, &buf[0][ptr0 + 4 * q], B);
+        } else {
             uint8_t *rc = region(kc), *rn = region(kc + 1);
-            if (quads) {
-                for (uint32_t q = ct; 4 * q < head; q += kMtTemperThreads)
-                    emit4(pos0 + 4 * q, &buf[0][ptr0 + 4 * q], rc, rn);
-            } else {
-                for (uint32_t i = ct; i < head; i += kMtTemperThreads)
-                    emit1(pos0 + i, buf[0][ptr0 + i], rc, rn);
-            }
+            for (uint32_t i = ct; i < head; i += kMtTemperThreads)
+                emit1(pos0 + i, buf[0][ptr0 + i], rc, rn);
         }
         lds_barrier();
         for (uint32_t t = 1; t <= twists; ++t) {
@@ -453,12 +483,16 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
             if (at >= bnd) {  // uniform: the block starts in the next call
                 ++kc;
                 bnd += so.per_end;
+                slot = next_slot(slot);
+                rcur = rnxt;
+                rnxt = so.base + next_slot(slot) * so.bytes;
             }
-            uint8_t *rc = region(kc), *rn = region(kc + 1);
             if (quads) {
+                const Bases B = bases(at);
                 for (uint32_t q = ct; 4 * q < take; q += kMtTemperThreads)
-                    emit4(at + 4 * q, cur + 4 * q, rc, rn);
+                    emit4(4 * q, cur + 4 * q, B);
             } else {
+                uint8_t *rc = region(kc), *rn = region(kc + 1);
 #pragma unroll
                 for (uint32_t r = 0; r < kMtRounds; ++r) {
                     const uint32_t i = ct + kMtTemperThreads * r;
