@@ -170,7 +170,7 @@ __device__ __forceinline__ void absmax_finish(uint32_t m, uint32_t *__restrict__
 // MODE 0: float4 dense, 1: scalar dense, 2: gather.  U float4 loads in flight
 // per thread; NT: nontemporal loads (streamed once).  (Round 5 measured a
 // reverse walk meant to leave x's front in the Infinity Cache for the encode:
-// no gain)
+// no gain, DESIGN_HISTORY §5.1.)
 template <int MODE, bool WS, unsigned BT = kAbsmaxThreads, int U = 4, bool NT = false, unsigned G = kAbsmaxGroups>
 __global__ __launch_bounds__(BT) void k_absmax(const float *__restrict__ x, const int64_t *__restrict__ idx,
                                                uint64_t n, uint32_t *__restrict__ out, uint32_t *__restrict__ ws)

@@ -971,11 +971,36 @@ __global__ __launch_bounds__(G4U_SCAN_THREADS) void k_g4u_scan(const uint32_t *_
     }
 }
 
+// the block's tot staged values (bytes, obuf) to dst as int32: the elements up
+// to dst's first 16-byte boundary one per thread, then four per thread (two
+// aligned LDS dwords, v_alignbyte by the uniform misalignment, one 16-byte
+// nontemporal store: the values are written once), then the tail
+__device__ __forceinline__ void g4u_store_values(const uint8_t *obuf, uint32_t tot, int32_t *__restrict__ dst,
+                                                 uint32_t t)
+{
+    const uint32_t lead = min((uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u) / 4u, tot);
+    if (t < lead)
+        dst[t] = (int32_t)obuf[t];
+    const uint32_t body = (tot - lead) & ~3u, sh = lead & 3u;
+    const uint32_t *ow = reinterpret_cast<const uint32_t *>(obuf);
+    for (uint32_t b = lead + 4 * t; b < lead + body; b += 4 * G4_THREADS) {
+        const uint32_t a = b >> 2;
+        const uint32_t v = __builtin_amdgcn_alignbyte(ow[a + 1], ow[a], sh);  // bytes b .. b+3
+        typedef int32_t i4v __attribute__((ext_vector_type(4)));
+        const i4v o = {(int32_t)(v & 0xFFu), (int32_t)((v >> 8) & 0xFFu), (int32_t)((v >> 16) & 0xFFu),
+                       (int32_t)(v >> 24)};
+        __builtin_nontemporal_store(o, reinterpret_cast<i4v *>(dst + b));
+    }
+    const uint32_t k = lead + body + t;
+    if (k < tot)
+        dst[k] = (int32_t)obuf[k];
+}
+
 __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit(const int32_t *__restrict__ words, uint64_t nw,
                                                          const uint64_t *__restrict__ bbase, int32_t *__restrict__ out,
                                                          const uint32_t *__restrict__ status)
 {
-    __shared__ uint8_t obuf[G4U_BLOCK_WORDS * 15];
+    __shared__ __attribute__((aligned(16))) uint8_t obuf[G4U_BLOCK_WORDS * 15 + 8];
     if (*status != 0)
         return;
     const uint64_t w0 = (uint64_t)blockIdx.x * G4U_BLOCK_WORDS + (uint64_t)threadIdx.x * G4U_PER_THREAD;
@@ -998,9 +1023,7 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit(const int32_t *__restri
         o += cnt;
     }
     __syncthreads();
-    const uint64_t base = bbase[blockIdx.x];
-    for (uint32_t k = threadIdx.x; k < tot; k += G4_THREADS)
-        out[base + k] = (int32_t)obuf[k];
+    g4u_store_values(obuf, tot, out + bbase[blockIdx.x], threadIdx.x);
 }
 
 // the emit without a scan launch: each block sums the block totals before it
@@ -1024,7 +1047,7 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit_nb(const int32_t *__res
                                                             int32_t *__restrict__ out, uint64_t cap,
                                                             uint64_t *__restrict__ count, uint32_t *__restrict__ status)
 {
-    __shared__ uint8_t obuf[G4U_BLOCK_WORDS * 15];
+    __shared__ __attribute__((aligned(16))) uint8_t obuf[G4U_BLOCK_WORDS * 15 + 8];
     __shared__ uint64_t red[2][G4_THREADS / 64];
     const unsigned t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint64_t b = blockIdx.x;
@@ -1072,8 +1095,7 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit_nb(const int32_t *__res
         o += cnt;
     }
     __syncthreads();
-    for (uint32_t k = t; k < tot; k += G4_THREADS)
-        out[base + k] = (int32_t)obuf[k];
+    g4u_store_values(obuf, tot, out + base, t);
 }
 
 // unpack workspace layout (bytes, 256-aligned pieces)

@@ -77,7 +77,7 @@ enum : int {
                         // against 45.0 us, profiles/r04n_lab_ms.log)
     MSV_UFLAG = 1024,   // octet mask kernel: the per-lane tail tests behind a wave-uniform flag
                         // (round 5 also measured two planes per loop trip and a second copy of the
-                        // plane code for full tiles: slower, removed)
+                        // plane code for full tiles: slower, removed; DESIGN_HISTORY §5.2)
     MSV_PLAINST = 2048, // plain (temporal) stores of the words / mask words instead of nontemporal ones:
                         // the next kernel of a step reads them at once (profiles/r05zh, r05zj_lab_ms.log)
 };

@@ -244,7 +244,7 @@ constexpr uint32_t kMtPre = 4;  // blocks of x in flight per tempering thread (q
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // RN(|x| / norm) as the reference computes it: Markstein's one-correction
-// quotient where it is exact (DESIGN §4.1, the encode's per-tile check made
+// quotient where it is exact (DESIGN §4.2, the encode's per-tile check made
 // per element), else the IEEE division
 __device__ __forceinline__ float mt_quot(float v, const DivNorm &dv)
 {

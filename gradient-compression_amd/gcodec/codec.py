@@ -796,7 +796,7 @@ def mt_generator_draws(count: int) -> int:
     0.37 us of chip time per generator and a generator about 0.34 us per
     624-draw block (latency-bound: measured with 382 and 256 generators), so
     G = sqrt(count * 0.34 / (624 * 0.37)) generators balance the two kernels
-    (DESIGN §7); J is a multiple of 624.  1e8 draws: G = 383, J = 261,456."""
+    (DESIGN_HISTORY §7); J is a multiple of 624.  1e8 draws: G = 383, J = 261,456."""
     g = int(min(MT_MAX_GENERATORS, max(1, round((count * 1.47e-3) ** 0.5))))
     return 624 * max(1, -(-count // (624 * g)))
 
@@ -982,7 +982,7 @@ MT_MAX_SLOTS = 8  # workspace / pinned-state slots of the runs in flight
 MT_MULTI_CALLS = 8
 # generators per pipelined run (mt19937_draws): None = mt_pipe_generators(count).  With the runs
 # made calls ahead, a generator's latency no longer bounds the call; fewer generators cut the
-# jump work, which shares the chip with the encodes
+# jump work, which shares the chip with the encodes (DESIGN_HISTORY section 7)
 MT_PIPE_GENERATORS = None
 MT_WAIT_NEXT_JUMPS = False  # consumers also wait for the speculative run's jumps (mt19937_draws)
 # side-stream priorities ("high" or "normal") of the jumps and of the generators

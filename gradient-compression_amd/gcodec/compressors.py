@@ -73,7 +73,7 @@ class QSGDMaxNormCompressor(_Base):
         # torch mode: the draws are generated on the GPU into a buffer, then
         # quantized by the full-chip kernel.  (codec.qsgd_quantize_torch, the
         # generator kernel consuming its own draws, gives the same q but runs
-        # slower on MI355X: DESIGN §7.)
+        # slower on MI355X: DESIGN_HISTORY §7.)
         rng = self._reserve(tensor.numel(), 1, tensor.device)
         return self.backend.qsgd_quantize(tensor, norm, self._quantization_level, rng, 0, self._dtype)
 
@@ -182,7 +182,7 @@ class _MultiScalePacked(_Base):
     encode (encode_w1, no cache needed); at W > 1 the cache pays, because the
     select then runs no Philox at all (ResNet50 bucket, MI355X r02y: mask 41.2
     + select 15.3 us with the cache against 25.7 + 38.5 us without; both
-    kernels are VALU-issue bound, DESIGN.md section 5.2).  True / False force
+    kernels are VALU-issue bound, DESIGN.md section 4.5).  True / False force
     it on / off."""
 
     def __init__(self, device, generator=None, q_cache=None):

@@ -220,7 +220,7 @@ int gc_randk_encode_w1_segments(const gc_segments *segs, const int64_t *idx, uin
 
 /* ---- greedy 4-mode packer on the device --------------------------------------
  * The format of gc_greedy4_pack (Extension CPU/bitpacking.cpp:5-124) produced by
- * a parallel scan over 16-entry segment tables (DESIGN.md §5.6).
+ * a parallel scan over 16-entry segment tables (DESIGN.md §4.8).
  * Results are asynchronous: *nwords / *count (device uint64) receive the
  * number of words / values, *status (device uint32) 0 or a bit set: 1 = a
  * value outside [0, 255], 2 = more than cap outputs, 4 = (pack) a block of the

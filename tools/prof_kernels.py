@@ -30,7 +30,8 @@ g = torch.Generator(device=dev).manual_seed(11)
 n3 = 23_520_842
 x3 = torch.randn(n3, device=dev, generator=g).mul_(0.01)
 gen = gcodec.Generator(5, "philox")
-ms = gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen)
+LV = [int(v) for v in os.environ.get("LEVELS", "2,4").split(",")]  # the two-scale levels (the reference's runs: 4,8)
+ms = gcodec.QSGDMaxNormTwoScaleCompressor(dev, LV[0], LV[1], generator=gen)
 nrm = codec.absmax(x3)
 t0 = time.perf_counter()
 while time.perf_counter() - t0 < SETTLE:  # clocks ramp over ~0.1-0.3 s of sustained load
@@ -47,12 +48,14 @@ for _ in range(REPS):
     ms.decode(nrm, w2, m2, n3, 1, 1.0, out=dout)
 # the W > 1 default (q_cache): mask pass + q cache cells, then the select from
 # the cache, at W = 2 lane sizing (one rank's mask: timing only)
-msc = gcodec.QSGDMaxNormTwoScaleCompressor(dev, 2, 4, generator=gen, q_cache=True)
+msc = gcodec.QSGDMaxNormTwoScaleCompressor(dev, LV[0], LV[1], generator=gen, q_cache=True)
 for _ in range(REPS):
     m3 = msc.encode_mask(nrm, x3, 2)
     w3 = msc.encode(nrm, x3, m3, 2)
 torch.cuda.synchronize()
 del x3
+if os.environ.get("MS_ONLY") == "1":  # the config-3 kernels only
+    sys.exit(0)
 st = torch.from_numpy(codec.mt19937_seed_state(42).view(np.int32)).to(dev)
 d = torch.empty(100_000_000, dtype=torch.int32, device=dev)
 for _ in range(REPS):
