@@ -686,6 +686,7 @@ def reduce_legs(torch, dist, codec, step, words, dec, norm, n, bits, world, lane
         rp["wire_bytes_fp32_over_packed"] = 4 * n / pb
         rp["busbw_note"] = ("busbw = 2(N-1)/N x bytes / t (ring all-reduce); MI355X xGMI: 7 links x ~153 GB/s per "
                             "GPU, one ring uses one link each way")
+    rp["rng"] = "philox (the headline's explicit Generator; torch mode is timed in torch_parity_mode)"
     res["reduce_path"] = rp
     if world >= 4 and world % 2 == 0:
         # intra reduce-scatter, "inter-node" all-reduce of 1/L of the words, intra
@@ -1165,6 +1166,8 @@ def main():
         out["pcie_inclusive"] = pcie_inclusive(torch, codec, gen, x, n, bits, world, lanes, K)
     cfg = other_configs(torch, dist, gcodec, codec, dev, world, rank, K, legs, args.n5)
     if cfg:
+        cfg["rng"] = ("philox (explicit Generator(seed, 'philox') in every config leg; the package default, "
+                      "torch mode, is the reference-identical stream timed in torch_parity_mode)")
         out["configs"] = cfg
     if "packers" in legs:
         out["packers"] = packers_leg(torch, gcodec, codec, dev, gen, rank)
