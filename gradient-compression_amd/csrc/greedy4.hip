@@ -971,28 +971,13 @@ __global__ __launch_bounds__(G4U_SCAN_THREADS) void k_g4u_scan(const uint32_t *_
     }
 }
 
-// the block's tot staged values (bytes, obuf) to dst as int32: the elements up
-// to dst's first 16-byte boundary one per thread, then four per thread (two
-// aligned LDS dwords, v_alignbyte by the uniform misalignment, one 16-byte
-// nontemporal store: the values are written once), then the tail
+// the block's tot staged values (bytes, obuf) to dst as int32, consecutive
+// lanes consecutive values (4-byte stores: the 16-byte forms, nontemporal or
+// not, and direct stores without the LDS staging measured slower)
 __device__ __forceinline__ void g4u_store_values(const uint8_t *obuf, uint32_t tot, int32_t *__restrict__ dst,
                                                  uint32_t t)
 {
-    const uint32_t lead = min((uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u) / 4u, tot);
-    if (t < lead)
-        dst[t] = (int32_t)obuf[t];
-    const uint32_t body = (tot - lead) & ~3u, sh = lead & 3u;
-    const uint32_t *ow = reinterpret_cast<const uint32_t *>(obuf);
-    for (uint32_t b = lead + 4 * t; b < lead + body; b += 4 * G4_THREADS) {
-        const uint32_t a = b >> 2;
-        const uint32_t v = __builtin_amdgcn_alignbyte(ow[a + 1], ow[a], sh);  // bytes b .. b+3
-        typedef int32_t i4v __attribute__((ext_vector_type(4)));
-        const i4v o = {(int32_t)(v & 0xFFu), (int32_t)((v >> 8) & 0xFFu), (int32_t)((v >> 16) & 0xFFu),
-                       (int32_t)(v >> 24)};
-        __builtin_nontemporal_store(o, reinterpret_cast<i4v *>(dst + b));
-    }
-    const uint32_t k = lead + body + t;
-    if (k < tot)
+    for (uint32_t k = t; k < tot; k += G4_THREADS)
         dst[k] = (int32_t)obuf[k];
 }
 
@@ -1000,7 +985,7 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit(const int32_t *__restri
                                                          const uint64_t *__restrict__ bbase, int32_t *__restrict__ out,
                                                          const uint32_t *__restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t obuf[G4U_BLOCK_WORDS * 15 + 8];
+    __shared__ uint8_t obuf[G4U_BLOCK_WORDS * 15];
     if (*status != 0)
         return;
     const uint64_t w0 = (uint64_t)blockIdx.x * G4U_BLOCK_WORDS + (uint64_t)threadIdx.x * G4U_PER_THREAD;
@@ -1047,7 +1032,7 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit_nb(const int32_t *__res
                                                             int32_t *__restrict__ out, uint64_t cap,
                                                             uint64_t *__restrict__ count, uint32_t *__restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t obuf[G4U_BLOCK_WORDS * 15 + 8];
+    __shared__ uint8_t obuf[G4U_BLOCK_WORDS * 15];
     __shared__ uint64_t red[2][G4_THREADS / 64];
     const unsigned t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     const uint64_t b = blockIdx.x;
@@ -1096,69 +1081,6 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_emit_nb(const int32_t *__res
     }
     __syncthreads();
     g4u_store_values(obuf, tot, out + base, t);
-}
-
-// The emit with no LDS staging (GC_G4U_DIRECT=1, A/B against k_g4u_emit_nb):
-// thread t owns words t, t + 256, t + 512, t + 768 of the block (a wave's word
-// loads stay coalesced), finds each word's output offset from two block scans
-// of packed 16-bit counts (a round's sum is at most 256 x 15), and stores the
-// word's values straight to `out`: a wave's j-th stores cover its words' runs
-// densely over a few KB, so the L2 merges whole lines.
-__global__ __launch_bounds__(G4_THREADS) void k_g4u_emit_direct(const int32_t *__restrict__ words, uint64_t nw,
-                                                                const uint32_t *__restrict__ bsum, uint64_t nb,
-                                                                int32_t *__restrict__ out, uint64_t cap,
-                                                                uint64_t *__restrict__ count,
-                                                                uint32_t *__restrict__ status)
-{
-    __shared__ uint64_t red[2][G4_THREADS / 64];
-    const unsigned t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    const uint64_t b = blockIdx.x;
-    uint64_t pre = 0, all = 0;
-    for (uint64_t k = t; k < nb; k += G4_THREADS) {
-        const uint32_t v = bsum[k];
-        all += v;
-        pre += k < b ? v : 0u;
-    }
-    pre = g4u_wave_sum(pre);
-    all = g4u_wave_sum(all);
-    if (lane == 0) {
-        red[0][wv] = pre;
-        red[1][wv] = all;
-    }
-    const uint64_t w0 = b * G4U_BLOCK_WORDS + t;
-    uint32_t code[4], cnt[4];
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) {
-        const uint64_t w = w0 + (uint64_t)G4_THREADS * i;
-        code[i] = w < nw ? (uint32_t)words[w] : 0u;
-        cnt[i] = w < nw ? g4_cnt(code[i] >> 30) : 0u;
-    }
-    uint32_t t01, t23;
-    const uint32_t e01 = block_excl_scan<G4_THREADS>(cnt[0] | (cnt[1] << 16), &t01);  // its barriers publish red
-    const uint32_t e23 = block_excl_scan<G4_THREADS>(cnt[2] | (cnt[3] << 16), &t23);
-    uint64_t base = 0, total = 0;
-#pragma unroll
-    for (unsigned i = 0; i < G4_THREADS / 64; ++i) {
-        base += red[0][i];
-        total += red[1][i];
-    }
-    if (b == 0 && t == 0) {
-        *count = total;
-        *status = total > cap ? G4_STATUS_NOSPC : 0u;
-    }
-    if (total > cap)
-        return;
-    const uint32_t s0 = t01 & 0xFFFFu, s1 = t01 >> 16, s2 = t23 & 0xFFFFu;
-    const uint32_t off[4] = {e01 & 0xFFFFu, s0 + (e01 >> 16), s0 + s1 + (e23 & 0xFFFFu), s0 + s1 + s2 + (e23 >> 16)};
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) {
-        const uint32_t mode = code[i] >> 30, c = cnt[i], top = g4_top(mode), bb = g4_bits(mode);
-        int32_t *o = out + base + off[i];
-#pragma unroll
-        for (uint32_t j = 0; j < 15; ++j)
-            if (j < c)
-                o[j] = (int32_t)__builtin_amdgcn_ubfe(code[i], top - j * bb, bb);
-    }
 }
 
 // unpack workspace layout (bytes, 256-aligned pieces)
@@ -1213,17 +1135,6 @@ static bool greedy4_stage()
     static const bool on = [] {
         const char *e = getenv("GC_G4_STAGE");
         return !(e && atol(e) == 0);
-    }();
-    return on;
-}
-
-// lab A/B of the unpack's emit (read once per process): GC_G4U_DIRECT=1 takes
-// k_g4u_emit_direct instead of the LDS-staged k_g4u_emit_nb
-static bool greedy4_unpack_direct()
-{
-    static const bool on = [] {
-        const char *e = getenv("GC_G4U_DIRECT");
-        return e && atol(e) == 1;
     }();
     return on;
 }
@@ -1298,12 +1209,8 @@ int gc_greedy4_unpack_device(const int32_t *words, uint64_t nwords, int32_t *out
     const uint64_t nb = (nwords + G4U_BLOCK_WORDS - 1) / G4U_BLOCK_WORDS;
     if (nwords > 0 && nb <= G4U_NB_DIRECT) {  // every block sums the block totals itself: two launches
         hipLaunchKernelGGL(k_g4u_sums, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bsum);
-        if (greedy4_unpack_direct())
-            hipLaunchKernelGGL(k_g4u_emit_direct, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bsum,
-                               nb, out, cap, count, status);
-        else
-            hipLaunchKernelGGL(k_g4u_emit_nb, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bsum, nb,
-                               out, cap, count, status);
+        hipLaunchKernelGGL(k_g4u_emit_nb, dim3((unsigned)nb), dim3(G4_THREADS), 0, st, words, nwords, w.bsum, nb, out,
+                           cap, count, status);
         return launch_status("gc_greedy4_unpack_device");
     }
     hipLaunchKernelGGL(k_g4p_empty, dim3(1), dim3(1), 0, st, count, status);
