@@ -307,7 +307,27 @@ struct SplitOut {
     uint32_t ring, ring0;
 };
 
-template <int MODE>
+// draws stored non-temporally (GC_MT_NT=0: plain stores, A/B)
+static uint32_t mt_nt_stores()
+{
+    static const uint32_t on = [] {
+        const char *e = getenv("GC_MT_NT");
+        return (uint32_t)!(e && atol(e) == 0);
+    }();
+    return on;
+}
+
+// one draw word to HBM, non-temporal when NT
+template <bool NT>
+__device__ __forceinline__ void mt_st(uint32_t *p, uint32_t v)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <int MODE, bool NT = false>
 __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__ ws, uint64_t gens, uint64_t jumps,
                                                          uint64_t J, uint64_t count,
                                                          void *__restrict__ out, uint32_t *__restrict__ state,
@@ -367,7 +387,7 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
             store_q(twists);
     } else if constexpr (MODE == 0) {
         for (uint32_t i = ct; i < head; i += kMtTemperThreads)
-            mt_emit<0>(out, pos0 + i, mtj_temper(buf[0][ptr0 + i]), x, DivNorm{}, s);
+            mt_st<NT>(reinterpret_cast<uint32_t *>(out) + (pos0 + i), mtj_temper(buf[0][ptr0 + i]));
         lds_barrier();
         for (uint32_t t = 1; t <= twists; ++t) {
             const uint32_t *cur = buf[t & 1u];
@@ -378,11 +398,11 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
                 for (uint32_t r = 0; r < kMtRounds; ++r) {
                     const uint32_t i = ct + kMtTemperThreads * r;
                     if (i < kMtN)
-                        mt_emit<0>(out, at + i, mtj_temper(cur[i]), x, DivNorm{}, s);
+                        mt_st<NT>(reinterpret_cast<uint32_t *>(out) + (at + i), mtj_temper(cur[i]));
                 }
             } else {
                 for (uint32_t i = ct; i < take; i += kMtTemperThreads)
-                    mt_emit<0>(out, at + i, mtj_temper(cur[i]), x, DivNorm{}, s);
+                    mt_st<NT>(reinterpret_cast<uint32_t *>(out) + (at + i), mtj_temper(cur[i]));
             }
             lds_barrier();
         }
@@ -453,16 +473,17 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
             const bool nx = j >= B.cut;
             uint8_t *h = (nx ? B.hn : B.hc) + HS * j;
             uint8_t *l = (nx ? B.ln : B.lc) + LS * j;
+            uint32_t *h32 = reinterpret_cast<uint32_t *>(h), *l32 = reinterpret_cast<uint32_t *>(l);
             if constexpr (HB == 8) {  // HI: bytes 2 of a, b, c, d; LO: bytes 0-1 of each
                 const uint32_t x = __builtin_amdgcn_perm(b, a, 0x0C0C0602u), y = __builtin_amdgcn_perm(d, c, 0x0C0C0602u);
-                *reinterpret_cast<uint32_t *>(h) = __builtin_amdgcn_perm(y, x, 0x05040100u);
-                *reinterpret_cast<uint2 *>(l) =
-                    make_uint2(__builtin_amdgcn_perm(b, a, 0x05040100u), __builtin_amdgcn_perm(d, c, 0x05040100u));
+                mt_st<NT>(h32, __builtin_amdgcn_perm(y, x, 0x05040100u));
+                mt_st<NT>(l32, __builtin_amdgcn_perm(b, a, 0x05040100u));
+                mt_st<NT>(l32 + 1, __builtin_amdgcn_perm(d, c, 0x05040100u));
             } else {  // HI: bytes 1-2 of each; LO: byte 0 of each
-                *reinterpret_cast<uint2 *>(h) =
-                    make_uint2(__builtin_amdgcn_perm(b, a, 0x06050201u), __builtin_amdgcn_perm(d, c, 0x06050201u));
+                mt_st<NT>(h32, __builtin_amdgcn_perm(b, a, 0x06050201u));
+                mt_st<NT>(h32 + 1, __builtin_amdgcn_perm(d, c, 0x06050201u));
                 const uint32_t x = __builtin_amdgcn_perm(b, a, 0x0C0C0400u), y = __builtin_amdgcn_perm(d, c, 0x0C0C0400u);
-                *reinterpret_cast<uint32_t *>(l) = __builtin_amdgcn_perm(y, x, 0x05040100u);
+                mt_st<NT>(l32, __builtin_amdgcn_perm(y, x, 0x05040100u));
             }
         };
         const bool quads = (ptr0 & 3u) == 0 && (so.per_end & 3u) == 0;  // uniform
@@ -515,7 +536,10 @@ __global__ __launch_bounds__(kMtGenThreads) void k_mt_gen(uint32_t *__restrict__
             p.x = (a & 0xFFFFFFu) | (b << 24);
             p.y = ((b >> 8) & 0xFFFFu) | (c << 16);
             p.z = ((c >> 16) & 0xFFu) | (d << 8);
-            *reinterpret_cast<uint3 *>(o + (e >> 2) * 3) = p;
+            uint32_t *o3 = o + (e >> 2) * 3;
+            mt_st<NT>(o3, p.x);
+            mt_st<NT>(o3 + 1, p.y);
+            mt_st<NT>(o3 + 2, p.z);
         };
         for (uint32_t q = ct; 4 * q < head; q += kMtTemperThreads)
             emit4(pos0 + 4 * q, &buf[0][ptr0 + 4 * q]);
@@ -782,10 +806,17 @@ static int mt_multi(const char *what, int mode, uint32_t *state_dev, const uint3
         if (g_first >= g1)
             return launch_status(what);
         const dim3 grid((unsigned)(g1 - g_first));
-#define GC_MTG(M_)                                                                                                   \
-    hipLaunchKernelGGL(k_mt_gen<M_>, grid, dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps, J, count,          \
+#define GC_MTG1(M_, NT_)                                                                                             \
+    hipLaunchKernelGGL((k_mt_gen<M_, NT_>), grid, dim3(kMtGenThreads), 0, st, ws, gens, (uint64_t)jumps, J, count,   \
                        (void *)out, (uint32_t *)nullptr, (const float *)nullptr, (const float *)nullptr, 0.0f, g_first, \
                        so)
+#define GC_MTG(M_)                                                                                                   \
+    do {                                                                                                             \
+        if (mt_nt_stores())                                                                                          \
+            GC_MTG1(M_, true);                                                                                       \
+        else                                                                                                         \
+            GC_MTG1(M_, false);                                                                                      \
+    } while (0)
         if (mode == 3)
             GC_MTG(3);
         else if (mode == 4)
@@ -795,6 +826,7 @@ static int mt_multi(const char *what, int mode, uint32_t *state_dev, const uint3
         else
             GC_MTG(0);
 #undef GC_MTG
+#undef GC_MTG1
     }
     return launch_status(what);
 }

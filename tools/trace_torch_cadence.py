@@ -17,7 +17,7 @@ import gcodec  # noqa: E402
 from gcodec import codec  # noqa: E402
 
 CALLS = int(os.environ.get("CALLS", "8"))
-PACKED = os.environ.get("PACKED24", "0") == "1"
+FMT = os.environ.get("FMT", "plain")  # draw format: plain / packed24 / split8 / split16
 dev = torch.device("cuda", 0)
 n = 100_000_000
 x = torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(1)).mul_(0.01)
@@ -37,7 +37,7 @@ def backward():
 
 def step():
     codec.absmax(x, out=nm)
-    codec.qsgd_encode(x, nm, 4, gen.reserve(n, packed24=PACKED), 1, out=words, lanes=lanes)
+    codec.qsgd_encode(x, nm, 4, gen.reserve(n, fmt=FMT), 1, out=words, lanes=lanes)
 
 
 for _ in range(4):  # warm: jump tables, end coefficients, the speculation started
