@@ -7,6 +7,7 @@ SUM); the bits are the uint32 lane words of include/gcodec.h.
 """
 from __future__ import annotations
 
+import collections
 import ctypes as C
 import operator
 import functools
@@ -1023,9 +1024,26 @@ def _mt_side(device):
     return s
 
 
+def _mt_upload_side(dev, host: np.ndarray) -> torch.Tensor:
+    """host (uint32) on the device, copied on the jump stream: every reader
+    of the end coefficients runs on that stream or after its phase-1 event.
+    A pinned, non-blocking copy: a pageable .to(dev) on the caller's stream
+    blocked the host until that stream drained (the GEMMs of a backward), and
+    the call's encode then started only after the host caught up
+    (profiles/r06t_host_torch_mode.log: 2.7-3.8 ms host stalls at the calls
+    that enqueue a speculative run with new end blocks)."""
+    js = _mt_side(dev)[0]
+    src = torch.from_numpy(np.ascontiguousarray(host).view(np.int32)).pin_memory()
+    with torch.cuda.stream(js):
+        t = torch.empty(src.shape, dtype=torch.int32, device=dev)
+        t.copy_(src, non_blocking=True)
+    return t
+
+
 def _mt_end_coef(dev, block: int):
     """Coefficients of the jump to raw block `block` (x^(624 block - 1) mod P)
-    on the device, cached: a bucket size takes at most two end blocks."""
+    on the device (uploaded on the jump stream), cached: a bucket size takes
+    at most two end blocks."""
     if block == 0:
         return None
     key = (dev.index, block)
@@ -1036,7 +1054,7 @@ def _mt_end_coef(dev, block: int):
               "gc_mt19937_jump_table_j")
         if len(_MT_END) >= 64:
             _MT_END.clear()
-        t = _MT_END[key] = torch.from_numpy(host.view(np.int32)).to(dev)  # synchronous: ready on any stream
+        t = _MT_END[key] = _mt_upload_side(dev, host)
     return t
 
 
@@ -1131,10 +1149,10 @@ _MT_END_HOST = {}  # end block -> host coefficients of x^(624 block - 1) mod P (
 def _mt_end_coefs(dev, blocks: tuple) -> torch.Tensor:
     """The end coefficient tables of a multi-call run, one per end block,
     contiguous on the device (cached: a bucket size takes a few tuples).
-    Built on the host and uploaded synchronously, so the table is ready for
-    the side streams whatever the caller's stream is doing (a device-side
-    stack would run on the caller's stream: the table growth test holds that
-    stream busy)."""
+    Built on the host and uploaded on the jump stream (_mt_upload_side), so
+    the side streams never wait for the caller's stream (a device-side stack
+    would run on the caller's stream: the table growth test holds that stream
+    busy)."""
     key = (dev.index, blocks)
     t = _MT_ENDCAT.get(key)
     if t is None:
@@ -1150,7 +1168,7 @@ def _mt_end_coefs(dev, blocks: tuple) -> torch.Tensor:
                 check(_lib.load().gc_mt19937_jump_table_j(624 * b, 1, 1, h.ctypes.data_as(C.c_void_p)),
                       "gc_mt19937_jump_table_j")
             host[i] = h
-        t = _MT_ENDCAT[key] = torch.from_numpy(host.view(np.int32)).to(dev)  # synchronous: ready on any stream
+        t = _MT_ENDCAT[key] = _mt_upload_side(dev, host)
     return t
 
 
@@ -1380,7 +1398,11 @@ def mt19937_reserve(count: int, device, fmt: str = "plain"):
 
     if queue and untouched and queue[0].count == count and queue[0].packed == fmt:
         run = queue[0]
+        _MT_STATS["queued"] += 1
     else:
+        _MT_STATS["fresh"] += 1
+        _MT_STATS["fresh_" + ("dropped" if dropped else "touched" if not untouched and last is not None else
+                              "mismatch" if queue else "empty" if last is not None else "first")] += 1
         if queue or dropped or not untouched:  # dst is not torch's state: send it
             with torch.cuda.stream(js):
                 h = hin.numpy().view(np.uint32)  # free: earlier copies from it were waited for
@@ -1401,6 +1423,7 @@ def mt19937_reserve(count: int, device, fmt: str = "plain"):
         while ahead < depth and behind < nslot - 1:
             tail_idx = queue[-1].idx_end if queue else run.idx_end
             queue.append(enqueue(tail_idx, calls))
+            _MT_STATS["speculative_runs"] += 1
             ahead += queue[-1].calls
             behind += 1
     elif run.k >= run.calls:
@@ -1422,6 +1445,23 @@ def mt19937_reserve(count: int, device, fmt: str = "plain"):
     set_torch_mt_state(w2, i2)
     _MT_LAST[d] = (w2, i2)
     return out, _FMT_KIND[run.packed]
+
+
+_MT_STATS = collections.Counter()
+
+
+def mt_stats(reset: bool = False) -> dict:
+    """Counters of mt19937_reserve since the last reset: calls served from
+    the speculative queue ("queued") or from a run made on demand ("fresh",
+    split by why: "fresh_first" / "fresh_empty" (no run queued) /
+    "fresh_touched" (torch's generator moved since the last call) /
+    "fresh_mismatch" (a queued run of another count or format) /
+    "fresh_dropped" (the slot rotation changed)), and the speculative runs
+    enqueued."""
+    out = dict(_MT_STATS)
+    if reset:
+        _MT_STATS.clear()
+    return out
 
 
 def mt_reserved_bytes(device=None) -> int:

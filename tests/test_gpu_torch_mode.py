@@ -365,6 +365,39 @@ def test_mt_reserved_bytes_counts_the_queue_and_release_frees_it():
     assert DEV.index not in codec._MT_SPEC
 
 
+def test_repeated_calls_are_served_from_the_queue_without_host_stalls():
+    """Once a size repeats, every call takes its draws from the speculative
+    queue (codec.mt_stats: no run made on demand), and a call that enqueues
+    the next run does not block the host on the caller's stream: the end
+    coefficients go up on the jump stream (_mt_upload_side).  The caller's
+    stream is held busy meanwhile, so a synchronous upload on it would take
+    the host as long as that work."""
+    codec.mt_release()
+    torch.manual_seed(11)
+    count = 1_000_003
+    for _ in range(3):
+        codec.mt19937_reserve(count, DEV, "plain")
+    codec._MT_ENDCAT.clear()  # new end blocks: every enqueue uploads again
+    codec._MT_END_HOST.clear()
+    codec.mt_stats(reset=True)
+    a = torch.randn(4096, 4096, device=DEV)
+    import time
+    worst = 0.0
+    for _ in range(12):
+        for _ in range(4):
+            a = a @ a
+            a /= a.abs().max()  # keeps the caller's stream busy for milliseconds
+        t0 = time.perf_counter()
+        codec.mt19937_reserve(count, DEV, "plain")
+        worst = max(worst, time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    st = codec.mt_stats()
+    assert st.get("queued", 0) == 12 and st.get("fresh", 0) == 0, st
+    assert st.get("speculative_runs", 0) >= 1, st
+    # the queued runs' host work is milliseconds at most; the busy stream holds ~4 x 4 GEMMs of 4096^3
+    assert worst < 0.02, worst
+
+
 def _as_draws24(got, kind, count):
     """The low 24 bits of each draw from a reservation of any format"""
     from gcodec import _lib

@@ -56,10 +56,16 @@ if os.environ.get("TIME") == "1":
 
     bw = min(per(backward) for _ in range(3))
     both = min(per(lambda: (backward(), step())) for _ in range(3))
-    print(f"backward {bw:.3f} ms, backward + step {both:.3f} ms, added {both - bw:.3f} ms per call")
+    print(f"backward {bw:.3f} ms, backward + step {both:.3f} ms, added {both - bw:.3f} ms per call; "
+          f"reserve paths {codec.mt_stats()}")
 else:
+    codec.mt_stats(reset=True)
+    paths = []
     for _ in range(CALLS):
         backward()
         step()
+        st = codec.mt_stats(reset=True)
+        paths.append("+".join(sorted(k for k in st if k != "fresh")) or "-")
     torch.cuda.synchronize()
+    print("per call:", " | ".join(paths))
 print("done")

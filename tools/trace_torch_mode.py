@@ -82,6 +82,7 @@ def run():
     for _ in range(int(os.environ.get("WARM", "24"))):
         step()
     torch.cuda.synchronize()
+    codec.mt_stats(reset=True)
     reps = int(os.environ.get("REPS", "40"))
     t0 = time.perf_counter()
     host = []
@@ -92,6 +93,7 @@ def run():
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
+    print("reserve paths in the timed loop:", codec.mt_stats(), flush=True)
     host.sort()
     print(f"fmt {fmt}: wall {(t2 - t0) / reps * 1e3:.3f} ms per call, host enqueue {(t1 - t0) / reps * 1e3:.3f} ms "
           f"per call (median {host[reps // 2] * 1e3:.3f}, max {host[-1] * 1e3:.3f})", flush=True)
