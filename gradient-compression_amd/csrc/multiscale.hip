@@ -349,15 +349,23 @@ static unsigned ms_grid(uint64_t quads)
 // 38.7 / 42.6 / 54.6 us at 1 / 2 / 3 / 4 tiles, mask + cache 35.7 / 38.5 /
 // 41.5 / 46.4 us; profiles/r03k_lab_ms_t*.log).  GC_MS_FUSED_TILES overrides
 // it (measurement only)
-static uint64_t ms_tiles()
+static uint64_t ms_tiles_env()
 {
     static const uint64_t t = [] {
         const char *e = getenv("GC_MS_FUSED_TILES");
         const long v = e ? atol(e) : 0;
-        return (uint64_t)(v >= 1 && v <= 64 ? v : 1);
+        return (uint64_t)(v >= 1 && v <= 64 ? v : 0);
     }();
     return t;
 }
+
+static uint64_t ms_tiles() { return ms_tiles_env() ? ms_tiles_env() : 1; }
+
+// tiles per block of the W = 1 one-pass octet kernel with r waves per block:
+// two from r = 5 (the 5-bit q lanes of levels (4, 8): 6 per word), whose
+// blocks of five waves run 5 x 6 planes per tile (38.8 -> 35.3 us on the
+// ResNet50 bucket, 3 tiles 39.7: profiles/r06y_ms_tiles_ab.json); one below
+static uint64_t ms_w1_tiles(uint32_t r) { return ms_tiles_env() ? ms_tiles_env() : (r >= 5 ? 2 : 1); }
 
 // planes per load batch of the one-pass W = 1 encode (k_ms_fused_w1's U) for
 // two levels with Philox draws: 2 (33.7-33.9 against 34.9-35.0 us at U = 1 on
@@ -468,7 +476,7 @@ int gc_ms_encode_w1(const float *x, uint64_t n, const float *norm, const gc_leve
                        fa, ra, Mm, r, q_lanes->per_word, q_lanes->bits, qmax, Cw, pend, mask_words, words)
     if (levels->count == 2) {
         if (rng->kind == GC_RNG_PHILOX && Mm % 8 == 0) {  // the octet kernel: dense draws shared by 8 elements
-            const unsigned g8 = (unsigned)std::max<uint64_t>(1, (ms_grid(Mm >> 3) + ms_tiles() - 1) / ms_tiles());
+            const unsigned g8 = (unsigned)std::max<uint64_t>(1, (ms_grid(Mm >> 3) + ms_w1_tiles(r) - 1) / ms_w1_tiles(r));
 #define GC_FW8(VAR_)                                                                                                \
     hipLaunchKernelGGL((k_ms_fused_w1_o2<VAR_>), dim3(g8), dim3(64 * r), 0, st, x, (uint32_t)n, norm, la, fa, ra, Mm, r, \
                        q_lanes->per_word, q_lanes->bits, qmax, Cw, pend, mask_words, words)
