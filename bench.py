@@ -763,6 +763,7 @@ def torch_mode_leg(torch, np, gcodec, codec, x, n, bits, words, lanes, dev, pgen
             best.append((time.perf_counter() - t0) / reps * 1e3)
         return min(best), best
 
+    codec.mt_stats(reset=True)
     enc_ms, enc_runs = per_call_ms(enc_torch)
     held = codec.mt_reserved_bytes(dev)  # what the speculation holds while calls repeat
     plan = codec._mt_plan(n, fmt, True)
@@ -793,6 +794,7 @@ def torch_mode_leg(torch, np, gcodec, codec, x, n, bits, words, lanes, dev, pgen
     cad_torch, _ = per_call_ms(lambda: (backward(), step_torch()), reps=10)
     cad_px, _ = per_call_ms(lambda: (backward(), step_philox()), reps=10)
     del a, c
+    paths = codec.mt_stats(reset=True)
 
     st = codec.mt19937_seed_state(42)
     sd = torch.from_numpy(st.view(np.int32)).to(dev)
@@ -808,8 +810,11 @@ def torch_mode_leg(torch, np, gcodec, codec, x, n, bits, words, lanes, dev, pgen
         "speculation": {"held_device_bytes": held, "budget_bytes": codec.MT_SPECULATE_BUDGET,
                         "calls_per_run": plan[0], "calls_ahead": plan[1],
                         "bytes_per_call": codec.mt_format_bytes(n, fmt),
+                        "reserve_paths": paths,
                         "note": "device memory the torch-mode speculation holds between calls "
-                                "(codec.mt_reserved_bytes: queued draws, workspaces, tables)"},
+                                "(codec.mt_reserved_bytes: queued draws, workspaces, tables); reserve_paths = "
+                                "codec.mt_stats() over this leg's torch-mode calls (queued = served from the "
+                                "speculative queue, fresh_* = made on demand, and why)"},
         "absmax_plus_encode": {"ms_per_call": stp_ms, "grad_floats_per_s": n / (stp_ms * 1e-3), "runs_ms": stp_runs,
                                "philox_ms_per_call": stp_px, "frac_of_philox_rate": stp_px / stp_ms},
         "training_cadence": {"backward_standin_ms": bw_ms, "torch_added_ms_per_call": cad_torch - bw_ms,
