@@ -57,7 +57,7 @@
 
 namespace gc {
 
-constexpr unsigned G4_THREADS = 256;                    // unpack blocks
+constexpr unsigned G4_THREADS = 512;                    // unpack blocks (256: 24.7 us, 512: 23.6, 1024: 33.5 on the ResNet50 xi words; profiles/r06af_g4u_block_threads_ab.json)
 constexpr uint32_t G4_SEG = 32;                         // positions per table block
 constexpr uint32_t G4_DEAD = 15;                        // table state: the chain has passed n
 constexpr uint32_t G4_STATUS_RANGE = 1u, G4_STATUS_NOSPC = 2u, G4_STATUS_TIMEOUT = 4u;
@@ -871,7 +871,7 @@ __global__ void k_g4p_empty(uint64_t *nwords, uint32_t *status)
 
 // ---- unpack ---------------------------------------------------------------
 constexpr uint32_t G4U_PER_THREAD = 4;
-constexpr uint32_t G4U_BLOCK_WORDS = G4_THREADS * G4U_PER_THREAD;  // 1024 words -> <= 15360 values
+constexpr uint32_t G4U_BLOCK_WORDS = G4_THREADS * G4U_PER_THREAD;  // 2048 words -> <= 30720 values
 
 __device__ __forceinline__ uint32_t g4_count(int32_t w) { return g4_cnt((uint32_t)w >> 30); }
 
@@ -937,7 +937,7 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_sums(const int32_t *__restri
 }
 
 constexpr unsigned G4U_SCAN_THREADS = 1024;
-// up to this many unpack blocks (4 M words) each emit block sums the block
+// up to this many unpack blocks (8 M words) each emit block sums the block
 // totals itself (k_g4u_emit_nb: <= 16 loads per thread from L2) instead of a
 // one-block scan launch
 constexpr uint64_t G4U_NB_DIRECT = 4096;
