@@ -938,7 +938,7 @@ __global__ __launch_bounds__(G4_THREADS) void k_g4u_sums(const int32_t *__restri
 
 constexpr unsigned G4U_SCAN_THREADS = 1024;
 // up to this many unpack blocks (8 M words) each emit block sums the block
-// totals itself (k_g4u_emit_nb: <= 16 loads per thread from L2) instead of a
+// totals itself (k_g4u_emit_nb: <= 8 loads per thread from L2) instead of a
 // one-block scan launch
 constexpr uint64_t G4U_NB_DIRECT = 4096;
 
